@@ -1,0 +1,557 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Python restatement of the reference's host-side scene pipeline, used to check
+that the product's loader (brown-cs2240-path-tracer_amd/node/lib/*.js) emits the
+reference's packed buffers float-for-float.  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg may import this module.
+
+Follows, in order:
+  parse_ini_file / ini_file_to_ini_scene   src/ts-util/parse-ini.ts:9-55
+  scene XML traversal (xml-js compact)     src/index.ts:26-113
+  parse_obj (OBJ + MTL)                    src/ts-util/parse-obj.ts:4-150
+  bounds_of_vec3 / overlap / area          src/ts-util/math.ts:14-56
+  BVH.construct (f64)                      src/ts-util/bvh.ts:25-187
+  pack_scene_object_group                  src/packer.ts:4-81
+  pack_bvh                                 src/packer.ts:83-137
+  BVH inputs (first primitive only)        src/index.ts:116-161
+  meta block                               src/program-raymarch.ts:55-92
+  resolution rounding                      src/index.ts:173-176
+
+Parity notes: `@toysinbox3dprinting/js-geometry ^1.0.12` (vector/matrix helpers,
+world_to_camera, mat4_invert) is not vendored and its version is unpinned, so the
+matrix conventions below are our own explicit choice ("parity unpinned at that
+boundary").  For every config scene the CTM is a translation or a
+0-degree rotation, for which the vertex transform is exactly the identity.
+"""
+from __future__ import annotations
+
+import math
+import re
+import struct
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass, field
+
+import numpy as np
+
+# ----------------------------------------------------------------------------
+# JS number parsing helpers (parseFloat / parseInt prefix semantics)
+# ----------------------------------------------------------------------------
+_FLOAT_RE = re.compile(r"^\s*([+-]?(?:Infinity|(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?))")
+_INT_RE = re.compile(r"^\s*([+-]?\d+)")
+
+
+def js_parse_float(s) -> float:
+    if s is None:
+        return math.nan
+    m = _FLOAT_RE.match(str(s))
+    if not m:
+        return math.nan
+    t = m.group(1)
+    if t.endswith("Infinity"):
+        return -math.inf if t.startswith("-") else math.inf
+    return float(t)
+
+
+def js_parse_int(s) -> float:
+    m = _INT_RE.match(str(s))
+    return float(int(m.group(1))) if m else math.nan
+
+
+def f32(x: float) -> float:
+    return struct.unpack("<f", struct.pack("<f", x))[0]
+
+
+# ----------------------------------------------------------------------------
+# INI (parse-ini.ts:9-55)
+# ----------------------------------------------------------------------------
+def parse_ini_file(raw: str) -> dict:
+    groups: dict = {}
+    cur: dict = {}
+    for line in raw.split("\n"):
+        if line[:1] == "[":
+            m = re.search(r"(?<=\[).+?(?=\])", line)
+            name = m.group(0).strip() if m else ""
+            groups[name] = {}
+            cur = groups[name]
+        else:
+            if "=" not in line:
+                continue
+            name = line.split("=", 1)[0].strip()
+            data = line.split("=", 1)[1].strip()
+            cur[name] = data
+    return groups
+
+
+def ini_file_to_ini_scene(f: dict) -> dict:
+    try:
+        io, st = f["IO"], f["Settings"]
+        return {
+            "IO": {"output": io.get("output"), "scene": io.get("scene")},
+            "Settings": {
+                "directLightingOnly": st.get("directLightingOnly") == "true",
+                "imageHeight": js_parse_int(st.get("imageHeight")),
+                "imageWidth": js_parse_int(st.get("imageWidth")),
+                "numDirectLightingSamples": js_parse_int(st.get("numDirectLightingSamples")),
+                "pathContinuationProb": js_parse_float(st.get("pathContinuationProb")),
+                "samplesPerPixel": js_parse_int(st.get("samplesPerPixel")),
+            },
+        }
+    except Exception as e:  # parse-ini.ts:52-53
+        raise ValueError("Error in ini file to ini scene file conversion") from e
+
+
+# ----------------------------------------------------------------------------
+# Matrices: row-major 4x4 lists, column-vector convention (our explicit choice)
+# ----------------------------------------------------------------------------
+def mat4_identity():
+    return [1.0 if r == c else 0.0 for r in range(4) for c in range(4)]
+
+
+def mat4_scale(x, y, z):
+    m = mat4_identity(); m[0] = x; m[5] = y; m[10] = z
+    return m
+
+
+def mat4_translate(x, y, z):
+    m = mat4_identity(); m[3] = x; m[7] = y; m[11] = z
+    return m
+
+
+def mat4_rot_axis(x, y, z, theta):  # math.ts:3-12 (theta in radians, as the reference passes degrees)
+    ct, st = math.cos(theta), math.sin(theta)
+    return [
+        ct + x * x * (1 - ct), x * y * (1 - ct) + z * st, x * z * (1 - ct) - y * st, 0,
+        x * y * (1 - ct) - z * st, ct + y * y * (1 - ct), y * z * (1 - ct) + x * st, 0,
+        x * z * (1 - ct) + y * st, y * z * (1 - ct) - x * st, ct + z * z * (1 - ct), 0,
+        0, 0, 0, 1,
+    ]
+
+
+def mat4_matmul(a, b):
+    return [sum(a[r * 4 + k] * b[k * 4 + c] for k in range(4)) for r in range(4) for c in range(4)]
+
+
+def mat4_invert(m):
+    """Cofactor inverse in f64 (exact for the translation / 0-degree rotation CTMs of the config scenes)."""
+    a = [m[i * 4:(i + 1) * 4] for i in range(4)]
+
+    def minor(r, c):
+        sub = [[a[i][j] for j in range(4) if j != c] for i in range(4) if i != r]
+        return (sub[0][0] * (sub[1][1] * sub[2][2] - sub[1][2] * sub[2][1])
+                - sub[0][1] * (sub[1][0] * sub[2][2] - sub[1][2] * sub[2][0])
+                + sub[0][2] * (sub[1][0] * sub[2][1] - sub[1][1] * sub[2][0]))
+
+    cof = [[((-1) ** (r + c)) * minor(r, c) for c in range(4)] for r in range(4)]
+    det = sum(a[0][c] * cof[0][c] for c in range(4))
+    return [cof[c][r] / det for r in range(4) for c in range(4)]
+
+
+def mat3_vecmul(m3, v):
+    return [m3[r * 3] * v[0] + m3[r * 3 + 1] * v[1] + m3[r * 3 + 2] * v[2] for r in range(3)]
+
+
+def mat4_to_mat3(m):
+    return [m[r * 4 + c] for r in range(3) for c in range(3)]
+
+
+def mat3_transpose(m):
+    return [m[c * 3 + r] for r in range(3) for c in range(3)]
+
+
+def mat4_vecmul(m, v):
+    return [m[r * 4] * v[0] + m[r * 4 + 1] * v[1] + m[r * 4 + 2] * v[2] + m[r * 4 + 3] * v[3] for r in range(4)]
+
+
+# ----------------------------------------------------------------------------
+# OBJ + MTL (parse-obj.ts:4-150)
+# ----------------------------------------------------------------------------
+def _norm_line(raw: str) -> str:
+    line = re.sub(r"\s+", " ", raw)
+    line = re.sub(r"#.*$", "", line)
+    return line.strip()
+
+
+def parse_obj(obj_data: str, mtl_data: str, ctm) -> dict:
+    vertices: list = []
+    vertex_normals: list = []
+    objects = [{"name": "default", "indices": []}]
+    ctm_inv = mat4_invert(ctm)
+    vm = mat3_transpose(mat4_to_mat3(ctm_inv))
+    for raw in obj_data.split("\n"):
+        line = _norm_line(raw)
+        if len(line) == 0 or line[0] == "#":
+            continue
+        if line[:2] == "v ":
+            data = [js_parse_float(t) for t in line[2:].strip().split(" ")]
+            vertices.extend(mat3_vecmul(vm, data)[:3])
+        elif line[:3] == "vn ":
+            data = [js_parse_float(t) for t in line[3:].strip().split(" ")]
+            vertex_normals.extend(mat4_vecmul(ctm, data + [1.0])[:3])
+        elif line[:2] == "f ":
+            nv = len(vertices) // 3
+            idx = []
+            for trip in line[2:].strip().split(" "):
+                i = js_parse_int(trip.split("/")[0])
+                idx.append(i if i > 0 else nv + i + 1)
+            if len(idx) == 3:
+                objects[-1]["indices"].extend(idx)
+            elif len(idx) == 4:
+                objects[-1]["indices"].extend([idx[0], idx[1], idx[2], idx[0], idx[2], idx[3]])
+            else:
+                raise ValueError("5+ sides encountered")
+        elif line[:6] == "usemtl":
+            parts = line.split(" ")
+            objects.append({"name": parts[1] if len(parts) > 1 else None, "indices": []})
+    objects = [o for o in objects if len(o["indices"]) > 0]
+
+    materials: dict = {}
+    cur = "default"
+    for raw in mtl_data.split("\n"):
+        line = _norm_line(raw)
+        if len(line) == 0 or line[0] == "#":
+            continue
+        parts = line.split(" ")
+        if line[:6] == "newmtl":
+            cur = parts[1] if len(parts) > 1 else None
+            materials[cur] = {"Ns": 0.0, "Ni": 0.0, "illum": 0.0, "Ka": [0.0] * 3, "Kd": [0.0] * 3,
+                              "Ks": [0.0] * 3, "Ke": [0.0] * 3}
+            continue
+        key = None
+        for k in ("Ns", "Ni"):
+            if line[:2] == k:
+                key = k
+        if key is None and line[:5] == "illum":
+            key = "illum"
+        if key is not None:
+            if cur not in materials:
+                raise TypeError("material property before newmtl")
+            materials[cur][key] = js_parse_float(parts[1] if len(parts) > 1 else None)
+            continue
+        for k in ("Ka", "Kd", "Ks", "Ke"):
+            if line[:2] == k:
+                if cur not in materials:
+                    raise TypeError("material property before newmtl")
+                materials[cur][k] = [js_parse_float(t) for t in parts[1:4]]
+                break
+    for o in objects:
+        o["material"] = materials.get(o["name"])
+    return {"vertices": vertices, "vertex_normals": vertex_normals, "objects": objects}
+
+
+# ----------------------------------------------------------------------------
+# Packing (packer.ts:4-81)
+# ----------------------------------------------------------------------------
+def pack_scene_object_group(g: dict) -> np.ndarray:
+    objs = g["objects"]
+    for o in objs:
+        if o["material"] is None:
+            raise TypeError(f"object '{o['name']}' has no material")
+    object_indices = []
+    for oid, o in enumerate(objs):
+        ni = []
+        ind = o["indices"]
+        for i in range(0, len(ind), 3):
+            ni.extend([ind[i], ind[i + 1], ind[i + 2], oid])
+        object_indices.append(ni)
+    flat = [v for ni in object_indices for v in ni]
+    emissive_ids = [i for i, o in enumerate(objs) if any(n > 0 for n in o["material"]["Ke"])]
+    sizes = [len(ni) for ni in object_indices]
+    offsets = [16 + len(g["vertices"])]
+    for s in sizes:
+        offsets.append(offsets[-1] + s)
+    offsets = offsets[:-1]
+    em = [[offsets[i], offsets[i] + sizes[i]] for i in emissive_ids]
+
+    def pack_mat(m):
+        return [m["Ns"], m["Ni"], m["illum"], *m["Ka"], *m["Kd"], *m["Ks"], *m["Ke"]]
+
+    mats = [v for o in objs for v in pack_mat(o["material"])]
+    V, I, M = len(g["vertices"]), len(flat), len(mats)
+    header = [V / 3, len(objs), 16, 16 + V, 16 + V + I, 16 + V + I + M, len(g["vertex_normals"]), 0]
+    for k in range(4):
+        header += em[k] if k < len(em) else [-1, -1]
+    group = header + list(g["vertices"]) + flat + mats + list(g["vertex_normals"])
+    group += [0] * (16 - len(group) % 16)
+    return np.array(group, dtype=np.float64).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------
+# BVH (bvh.ts:25-187), f64, spatial split with duplication
+# ----------------------------------------------------------------------------
+@dataclass
+class Node:
+    is_leaf: bool
+    axis: int
+    bmin: list
+    bmax: list
+    objs: np.ndarray  # indices into the object arrays
+    left: "Node | None" = None
+    right: "Node | None" = None
+
+
+def bounds_of_vec3(verts):  # math.ts:14-34
+    mn = list(verts[0]); mx = list(verts[0])
+    for v in verts:
+        for a in range(3):
+            if v[a] <= mn[a]:
+                mn[a] = v[a]
+            if v[a] >= mx[a]:
+                mx[a] = v[a]
+    return mn, mx
+
+
+def _overlap(omin, omax, bmin, bmax):  # math.ts:45-49, vectorised over objects
+    return ((bmin[0] <= omax[:, 0]) & (omin[:, 0] <= bmax[0]) &
+            (bmin[1] <= omax[:, 1]) & (omin[:, 1] <= bmax[1]) &
+            (bmin[2] <= omax[:, 2]) & (omin[:, 2] <= bmax[2]))
+
+
+def build_bvh(omin: np.ndarray, omax: np.ndarray, outer_min, outer_max, stats: dict | None = None) -> Node:
+    MAX_DEPTH, MAX_OBJ = 16, 16
+
+    def split_coord(axis, w0, bmin, bmax):
+        w1 = 1.0 - w0
+        return w0 * bmax[axis] + w1 * bmin[axis]
+
+    def recurse(node: Node, depth: int):
+        if depth >= MAX_DEPTH:
+            node.is_leaf = True
+            return
+        sx = node.bmax[0] - node.bmin[0]; sy = node.bmax[1] - node.bmin[1]; sz = node.bmax[2] - node.bmin[2]
+        if sx >= sy and sx >= sz:
+            axis = 0
+        elif sy >= sx and sy >= sz:
+            axis = 1
+        else:
+            axis = 2
+        split, cost = 0.5, math.inf
+        step = 0.05
+        s = step
+        lo, hi = omin[node.objs], omax[node.objs]
+        while s <= 1.0 - step:
+            c = split_coord(axis, s, node.bmin, node.bmax)
+            lmax = list(node.bmax); lmax[axis] = c
+            hmin = list(node.bmin); hmin[axis] = c
+            n_low = int(np.count_nonzero(_overlap(lo, hi, node.bmin, lmax)))
+            n_high = int(np.count_nonzero(_overlap(lo, hi, hmin, node.bmax)))
+            avg = (n_low + n_high) * 0.5
+            cur = abs(n_low - avg) + abs(n_high - avg)
+            if cur < cost:
+                split, cost = s, cur
+            s += step
+        c = split_coord(axis, split, node.bmin, node.bmax)
+        lmax = list(node.bmax); lmax[axis] = c
+        rmin = list(node.bmin); rmin[axis] = c
+        lsel = node.objs[_overlap(lo, hi, node.bmin, lmax)]
+        rsel = node.objs[_overlap(lo, hi, rmin, node.bmax)]
+        node.left = Node(False, -1, list(node.bmin), lmax, lsel)
+        if len(lsel) <= MAX_OBJ or len(lsel) == len(node.objs):
+            node.left.is_leaf = True
+        else:
+            recurse(node.left, depth + 1)
+        node.right = Node(False, -1, rmin, list(node.bmax), rsel)
+        if len(rsel) <= MAX_OBJ or len(rsel) == len(node.objs):
+            node.right.is_leaf = True
+        else:
+            recurse(node.right, depth + 1)
+
+    root = Node(False, 0, list(outer_min), list(outer_max), np.arange(len(omin)))
+    recurse(root, 1)
+    return root
+
+
+def pack_bvh(root: Node, outer_min, outer_max, obj_records: np.ndarray) -> np.ndarray:
+    """packer.ts:83-137; obj_records[i] = (i0, i1, i2, mat) for BVH object i."""
+    out: list = [*outer_min, *outer_max]
+
+    def rec(node: Node):
+        children = obj_records[node.objs].reshape(-1).tolist() if node.is_leaf else []
+        cur = len(out)
+        left_off = cur + 5 + 12 + len(children)
+        right_idx = cur + 3
+        out.extend([1 if node.is_leaf else 0, node.axis, -1 if node.is_leaf else left_off, -1,
+                    len(children) if node.is_leaf else -2])
+        for ch in (node.left, node.right):
+            if ch is not None:
+                out.extend([*ch.bmin, *ch.bmax])
+            else:
+                out.extend([0, 0, 0, 0, 0, 0])
+        out.extend(children)
+        if not node.is_leaf and node.left is not None:
+            rec(node.left)
+        if not node.is_leaf and node.right is not None:
+            out[right_idx] = len(out)
+            rec(node.right)
+
+    rec(root)
+    return np.array(out, dtype=np.float64).astype(np.float32)
+
+
+def bvh_stats(root: Node) -> dict:
+    st = {"nodes": 0, "leaves": 0, "refs": 0, "max_leaf": 0, "depth": 0}
+
+    def rec(n, d):
+        st["nodes"] += 1
+        st["depth"] = max(st["depth"], d)
+        if n.is_leaf:
+            st["leaves"] += 1
+            st["refs"] += len(n.objs)
+            st["max_leaf"] = max(st["max_leaf"], len(n.objs))
+            return
+        rec(n.left, d + 1); rec(n.right, d + 1)
+
+    rec(root, 1)
+    return st
+
+
+# ----------------------------------------------------------------------------
+# Scene XML traversal (index.ts:26-113), xml-js compact grouping by tag name
+# ----------------------------------------------------------------------------
+def _children(el, tag):
+    return [c for c in el if c.tag == tag]
+
+
+def load_scene_xml(xml_text: str):
+    root = ET.fromstring(xml_text)
+    if root.tag != "scenefile":
+        raise ValueError("not a scenefile")
+    cd = _children(root, "cameradata")[0]
+
+    def attr3(tag):
+        a = _children(cd, tag)[0].attrib
+        return [js_parse_float(a.get("x")), js_parse_float(a.get("y")), js_parse_float(a.get("z"))]
+
+    camera = {"focus": attr3("focus"), "pos": attr3("pos"), "up": attr3("up"),
+              "heightangle": js_parse_float(_children(cd, "heightangle")[0].attrib.get("v"))}
+    prims = []
+
+    def traverse(obj, ctm):
+        t = obj.attrib.get("type")
+        if t == "tree":
+            for o in _children(obj, "object"):
+                traverse(o, ctm)
+            for tb in _children(obj, "transblock"):
+                new = ctm
+                for tag in ("rotate", "scale", "translate"):
+                    els = _children(tb, tag)
+                    if not els:
+                        continue
+                    if len(els) > 1:
+                        raise TypeError(f"multiple <{tag}> in one transblock")
+                    a = els[0].attrib
+                    if tag == "rotate":
+                        m = mat4_rot_axis(js_parse_float(a.get("x")), js_parse_float(a.get("y")),
+                                          js_parse_float(a.get("z")), js_parse_float(a.get("angle")))
+                    elif tag == "scale":
+                        m = mat4_scale(js_parse_float(a.get("x")), js_parse_float(a.get("y")), js_parse_float(a.get("z")))
+                    else:
+                        m = mat4_translate(js_parse_float(a.get("x")), js_parse_float(a.get("y")),
+                                           js_parse_float(a.get("z")))
+                    new = mat4_matmul(m, new)
+                for o in _children(tb, "object"):
+                    traverse(o, new)
+        elif t == "primitive":
+            prims.append({"name": obj.attrib.get("name"), "path": "/scene_assets/" + obj.attrib.get("filename", ""),
+                          "ctm": ctm})
+        else:
+            raise ValueError(f"unknown type of object {t} to parse")
+
+    for o in _children(root, "object"):
+        traverse(o, mat4_scale(1, 1, 1))
+    return camera, prims
+
+
+@dataclass
+class PackedScene:
+    triangle_data: np.ndarray
+    bvh_data: np.ndarray
+    bounds_min: list
+    bounds_max: list
+    stats: dict = field(default_factory=dict)
+
+
+def pack_primitive(obj_text: str, mtl_text: str, ctm) -> PackedScene:
+    """index.ts:128-161 for one primitive."""
+    g = parse_obj(obj_text, mtl_text, ctm)
+    tri = pack_scene_object_group(g)
+    V = g["vertices"]
+    verts = [V[i:i + 3] for i in range(0, len(V), 3)]
+    bmin, bmax = bounds_of_vec3(verts)
+    recs, omin, omax = [], [], []
+    for mat_i, o in enumerate(g["objects"]):
+        ind = o["indices"]
+        for i in range(0, len(ind), 3):
+            i0, i1, i2 = (int(ind[i]) - 1) * 3, (int(ind[i + 1]) - 1) * 3, (int(ind[i + 2]) - 1) * 3
+            tmin, tmax = bounds_of_vec3([V[i0:i0 + 3], V[i1:i1 + 3], V[i2:i2 + 3]])
+            recs.append([ind[i], ind[i + 1], ind[i + 2], mat_i])
+            omin.append(tmin); omax.append(tmax)
+    omin_a, omax_a = np.array(omin, dtype=np.float64), np.array(omax, dtype=np.float64)
+    root = build_bvh(omin_a, omax_a, bmin, bmax)
+    bvh = pack_bvh(root, bmin, bmax, np.array(recs, dtype=np.float64))
+    return PackedScene(tri, bvh, bmin, bmax, bvh_stats(root))
+
+
+def load_scene(scene_xml_path: str, asset_root: str):
+    """Loads the XML, packs the FIRST primitive (index.ts:116), returns (camera, PackedScene)."""
+    import os
+    with open(scene_xml_path) as f:
+        camera, prims = load_scene_xml(f.read())
+    if not prims:
+        raise ValueError("scene has no primitives")
+    p = prims[0]
+    path = os.path.join(asset_root, p["path"].lstrip("/").split("/", 1)[1])
+    with open(path) as f:
+        obj_text = f.read()
+    try:
+        with open(path[:-3] + "mtl") as f:
+            mtl_text = f.read()
+    except OSError:
+        mtl_text = ""
+    return camera, pack_primitive(obj_text, mtl_text, p["ctm"])
+
+
+# ----------------------------------------------------------------------------
+# Camera + meta block (program-raymarch.ts:55-92)
+# ----------------------------------------------------------------------------
+def _norm(v):
+    l = math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    return [v[0] / l, v[1] / l, v[2] / l]
+
+
+def _cross(a, b):
+    return [a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]]
+
+
+def camera_matrices(pos, look, up):
+    """Look-at: w = -look, v = up orthogonalised against w, u = v x w.  Column-major (WGSL mat4x4)
+    arrays: cam_to_world columns = (u, v, w, pos); world_to_cam = its inverse."""
+    w = _norm([-look[0], -look[1], -look[2]])
+    d = up[0] * w[0] + up[1] * w[1] + up[2] * w[2]
+    v = _norm([up[0] - d * w[0], up[1] - d * w[1], up[2] - d * w[2]])
+    u = _cross(v, w)
+    c2w = [*u, 0.0, *v, 0.0, *w, 0.0, *pos, 1.0]
+    tx = -(u[0] * pos[0] + u[1] * pos[1] + u[2] * pos[2])
+    ty = -(v[0] * pos[0] + v[1] * pos[1] + v[2] * pos[2])
+    tz = -(w[0] * pos[0] + w[1] * pos[1] + w[2] * pos[2])
+    # world_to_cam rows are u, v, w; column-major storage
+    w2c = [u[0], v[0], w[0], 0.0, u[1], v[1], w[1], 0.0, u[2], v[2], w[2], 0.0, tx, ty, tz, 1.0]
+    return w2c, c2w
+
+
+def screen_dimension(settings: dict):  # index.ts:173-176
+    x = settings["imageWidth"]
+    aspect = x / settings["imageHeight"]
+    r4 = lambda n: math.floor(n / 4) * 4
+    return [r4(x), r4(x / aspect)]
+
+
+def make_meta(screen, camera, settings, t: float = 0.0) -> np.ndarray:
+    W, H = screen
+    pos = camera["pos"]
+    look = _norm([camera["focus"][i] - pos[i] for i in range(3)])
+    w2c, c2w = camera_matrices(pos, look, camera["up"])
+    meta = [W, H, 1.0, camera["heightangle"] * math.pi / 180, pos[0], pos[1], pos[2], 1.0,
+            1 / W, 1 / H, W / H, t, *w2c, *c2w,
+            settings["samplesPerPixel"], settings["pathContinuationProb"],
+            1.0 if settings["directLightingOnly"] else -1.0, 0.0]
+    return np.array(meta, dtype=np.float64).astype(np.float32)
