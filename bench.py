@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s (paths/s) on CornellBox 1024^2, depth 8 (BASELINE.json configs[1]).
+
+One step = the whole render of the configured frames (default 256 spp = 268,435,456 camera
+paths) into a zeroed f32 accumulator resident in HBM, split across ranks by frame
+(rank r renders frames k = r, r+N, ... — sample-interleaved), followed for
+N > 1 by ONE RCCL sum-reduce of the W*H*3 accumulator to rank 0.  Strong scaling: the total
+work is fixed as N grows.  The scene is packed by the product's Node host
+(node/bin/pt-pack.js) before timing; scene upload is outside the timed region.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` for the
+render kernel (algorithmic bytes per launch from the GPU's own work counters, SURVEY.md §8d:
+B_alg = 48*Q + 96*Q_ext + 24 bytes per sample, over the kernel's HIP-event duration) and
+`cpu_baseline` (the C oracle, oracle/pt_oracle.c, on the host cores, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "brown-cs2240-path-tracer_amd")
+sys.path.insert(0, PKG)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def pack_scene(scene: str, out_dir: str, W: int, H: int, spp: int):
+    xml = os.path.join(ROOT, "scenes", "scene_assets", scene + ".xml")
+    subprocess.run(["node", os.path.join(PKG, "node", "bin", "pt-pack.js"), xml, out_dir, "--width", str(W),
+                    "--height", str(H), "--spp", str(spp), "--rr", "0.9"], check=True)
+    tri = np.fromfile(os.path.join(out_dir, "triangle_data.f32"), np.float32)
+    bvh = np.fromfile(os.path.join(out_dir, "bvh_data.f32"), np.float32)
+    meta = np.fromfile(os.path.join(out_dir, "meta.f32"), np.float32)
+    return tri, bvh, meta
+
+
+def cpu_baseline(tri, bvh, meta, depth, target_s=12.0):
+    """C oracle on the host cores over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg only)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    W, H = int(meta[0]), int(meta[1])
+    # calibrate on 1/16 of the rows, one frame
+    rows = max(1, H // 16)
+    y0 = (H - rows) // 2
+    t = time.perf_counter()
+    oracle.render(tri, bvh, meta, 0, 1, 1, depth, y0=y0, y1=y0 + rows, nthreads=threads)
+    dt = time.perf_counter() - t
+    per_row = dt / rows
+    n_rows = int(min(H, max(8, target_s / max(per_row, 1e-9))))
+    y0 = (H - n_rows) // 2
+    t = time.perf_counter()
+    _, c = oracle.render(tri, bvh, meta, 0, 1, 1, depth, y0=y0, y1=y0 + n_rows, nthreads=threads)
+    dt = time.perf_counter() - t
+    return {"value": round(c["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/pt_oracle.c (CPU restatement of the reference WGSL; no CPU WebGPU adapter exists here), "
+                      f"{W}x{n_rows} central rows of the {W}x{H} frame 0, depth {depth}, {threads} OpenMP threads, "
+                      f"{c['samples']} samples in {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="CornellBox")
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--mode", default="auto", choices=["auto", "megakernel", "wavefront"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import pt_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    with tempfile.TemporaryDirectory() as td:
+        tri, bvh, meta = pack_scene(args.scene, td, args.width, args.height, args.spp)
+    W, H = int(meta[0]), int(meta[1])
+    mode = {"auto": pt_amd.MODE_AUTO, "megakernel": pt_amd.MODE_MEGAKERNEL, "wavefront": pt_amd.MODE_WAVEFRONT}[args.mode]
+    scene = pt_amd.Scene(tri, bvh, device=local_rank)
+    # frames of this rank: k = rank, rank + world, ...
+    nframes = len(range(rank, args.spp, world))
+    stream = torch.cuda.Stream(device=dev)
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+
+    def step():
+        with torch.cuda.stream(stream):
+            acc.zero_()
+            scene.render_async(meta, rank, nframes, world, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
+            if world > 1:
+                dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+
+    # work counters for the roofline's algorithmic bytes (separate pass, not timed)
+    cnt = torch.zeros(6, dtype=torch.int64, device=dev)
+    with torch.cuda.stream(stream):
+        tmp = torch.zeros_like(acc)
+        scene.render_async(meta, rank, nframes, world, args.depth, mode, tmp.data_ptr(), stream.cuda_stream,
+                           d_counters_ptr=cnt.data_ptr())
+    stream.synchronize()
+    c = cnt.cpu().tolist()
+    samples_c, q_ext, q_sh = c[0], c[1], c[2]
+    del tmp
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        with torch.cuda.stream(stream):
+            acc.zero_()
+            ev0.record(stream)
+            scene.render_async(meta, rank, nframes, world, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
+            ev1.record(stream)
+            if world > 1:
+                dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+        ev1.synchronize()
+        kernel_ms.append(ev0.elapsed_time(ev1))
+    stream.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_samples = W * H * args.spp
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_samples / (elapsed / args.steps) / 1e6
+    k_ms = float(np.mean(kernel_ms))
+    b_alg = (48.0 * (q_ext + q_sh) + 96.0 * q_ext + 24.0 * samples_c)  # bytes per launch
+    achieved = b_alg / (k_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": "Msamples/s (paths/s) CornellBox 1024^2 depth 8",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference CornellBox.xml scene packed by the Node host; RNG salts t_k = k)",
+            "config": {"workload": f"{args.scene}.xml {W}x{H} {args.spp}spp depth {args.depth}, rr 0.9, "
+                                   f"frames sharded k mod {world}" + (", RCCL sum-reduce of the f32 accumulator"
+                                                                        if world > 1 else ""),
+                       "mode": args.mode, "samples_per_step": total_samples},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_mega", "kernel_ms": round(k_ms, 3),
+                         "bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
+                         "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(tri, bvh, meta, args.depth)
+        print(json.dumps(out), flush=True)
+    scene.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

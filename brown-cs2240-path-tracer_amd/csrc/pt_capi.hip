@@ -1,0 +1,422 @@
+// pt_capi.hip — C ABI (include/pt_hip.h): scene upload/re-encoding, render entry points.
+// Host code only; kernels live in pt_kernels.hip.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pt_hip.h"
+#include "pt_kernels.h"
+
+using namespace pt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess) return fail(PT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// WGSL i32(f32): truncate toward zero, saturating.
+int32_t wgsl_i32(float f) {
+    if (std::isnan(f)) return 0;
+    if (f >= 2147483647.0f) return INT32_MAX;
+    if (f <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)f;
+}
+
+// Reads of the packed triangle buffer with Dawn/Tint robustness (index clamped to len-1),
+// as the WGSL reads primitive_0 in sample_area_lights (intersection-logic.wgsl:260-279).
+struct Packed {
+    const float* p;
+    size_t n;
+    float at(int32_t i) const {
+        uint32_t u = (uint32_t)i;
+        if (u >= n) u = (uint32_t)(n - 1);
+        return p[u];
+    }
+};
+
+struct HostLayout {
+    std::vector<Node> nodes;
+    std::vector<Tri> tris;
+    std::vector<Material> mats;
+    std::vector<Light> lights;
+    pt_scene_info info{};
+    int32_t ntri = 0;
+};
+
+// Re-encode packer.ts layouts into pt_layout.h.
+int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_len, HostLayout& L) {
+    if (tri_len < 16 || tri_len > (size_t)INT32_MAX) return fail(PT_ERR_SCENE, "triangle_data shorter than its 16-float header");
+    if (bvh_len < 6 + 17 || bvh_len > (size_t)INT32_MAX) return fail(PT_ERR_SCENE, "bvh_data shorter than bounds + one node");
+    Packed P{tri, tri_len};
+    const float nverts_f = tri[0], nobj_f = tri[1];
+    if (!(nverts_f >= 0 && nverts_f == std::floor(nverts_f)) || !(nobj_f >= 1 && nobj_f == std::floor(nobj_f)))
+        return fail(PT_ERR_SCENE, "bad vertex/object counts in triangle_data header");
+    const int64_t nverts = (int64_t)nverts_f, nobj = (int64_t)nobj_f;
+    const int64_t v_start = wgsl_i32(tri[2]), m_start = wgsl_i32(tri[4]);
+    if (v_start < 0 || v_start + 3 * nverts > (int64_t)tri_len) return fail(PT_ERR_SCENE, "vertex section out of range");
+    if (m_start < 0 || m_start + 15 * nobj > (int64_t)tri_len) return fail(PT_ERR_SCENE, "material section out of range");
+    L.info.vertices = (uint32_t)nverts;
+
+    // materials (program-raymarch.wgsl:87-102): Ns Ni illum Ka Kd Ks Ke
+    L.mats.resize((size_t)nobj);
+    for (int64_t id = 0; id < nobj; ++id) {
+        const float* m = tri + m_start + 15 * id;
+        Material& o = L.mats[(size_t)id];
+        std::memset(&o, 0, sizeof o);
+        o.Ns = m[0]; o.Ni = m[1]; o.illum = m[2];
+        for (int c = 0; c < 3; ++c) { o.Kd[c] = m[6 + c]; o.Ks[c] = m[9 + c]; o.Ke[c] = m[12 + c]; }
+    }
+    L.info.materials = (uint32_t)nobj;
+
+    auto vertex = [&](int64_t one_based, float out[3]) -> bool {
+        if (one_based < 1 || one_based > nverts) return false;
+        const float* v = tri + v_start + 3 * (one_based - 1);
+        out[0] = v[0]; out[1] = v[1]; out[2] = v[2];
+        return true;
+    };
+
+    // BVH: pre-order tree from offset 6 (intersection-logic.wgsl:4-16).
+    if (bvh[6] == 1.0f) return fail(PT_ERR_SCENE, "BVH root is a leaf (the reference never builds one)");
+    struct Item { int32_t off; int32_t node; int32_t depth; };
+    std::vector<Item> work;
+    L.nodes.push_back(Node{});
+    work.push_back({6, 0, 0});
+    const size_t node_cap = bvh_len / 17 + 1;
+    uint32_t max_depth = 0;
+    while (!work.empty()) {
+        Item it = work.back();
+        work.pop_back();
+        const int32_t o = it.off;
+        if (o < 0 || (size_t)o + 17 > bvh_len) return fail(PT_ERR_SCENE, "BVH node offset out of range");
+        max_depth = std::max<uint32_t>(max_depth, (uint32_t)it.depth);
+        Node nd{};
+        for (int c = 0; c < 3; ++c) {
+            nd.lmin[c] = bvh[o + 5 + c]; nd.lmax[c] = bvh[o + 8 + c];
+            nd.rmin[c] = bvh[o + 11 + c]; nd.rmax[c] = bvh[o + 14 + c];
+        }
+        int32_t child_off[2] = {wgsl_i32(bvh[o + 2]), wgsl_i32(bvh[o + 3])};
+        int32_t refs[2], cnts[2];
+        for (int side = 0; side < 2; ++side) {
+            const int32_t c = child_off[side];
+            if (c < 0 || (size_t)c + 17 > bvh_len) return fail(PT_ERR_SCENE, "BVH child pointer out of range");
+            if (bvh[c] == 1.0f) {  // leaf: (i0,i1,i2,mat) 1-based entries after the 17-float header
+                const float nf = bvh[c + 4];
+                if (!(nf >= 0) || std::fmod(nf, 4.0f) != 0.0f || (size_t)c + 17 + (size_t)nf > bvh_len)
+                    return fail(PT_ERR_SCENE, "BVH leaf payload malformed");
+                const int32_t n = (int32_t)(nf / 4.0f);
+                refs[side] = (int32_t)L.tris.size();
+                cnts[side] = n;
+                for (int32_t k = 0; k < n; ++k) {
+                    const float* e = bvh + c + 17 + 4 * k;
+                    float v0[3], v1[3], v2[3];
+                    if (!vertex(wgsl_i32(e[0]), v0) || !vertex(wgsl_i32(e[1]), v1) || !vertex(wgsl_i32(e[2]), v2))
+                        return fail(PT_ERR_SCENE, "BVH leaf references a vertex out of range");
+                    const int32_t mat = wgsl_i32(e[3]);
+                    if (mat < 0 || mat >= nobj) return fail(PT_ERR_SCENE, "BVH leaf references a material out of range");
+                    Tri t{};
+                    for (int q = 0; q < 3; ++q) {
+                        t.v0[q] = v0[q];
+                        t.e1[q] = v1[q] - v0[q];  // ray-triangle-intersection.wgsl:6
+                        t.e2[q] = v2[q] - v0[q];  // :7
+                    }
+                    t.mat = mat;
+                    L.tris.push_back(t);
+                }
+                L.info.leaves++;
+                L.info.leaf_refs += (uint32_t)n;
+                L.info.max_leaf = std::max<uint32_t>(L.info.max_leaf, (uint32_t)n);
+            } else {
+                if (L.nodes.size() >= node_cap) return fail(PT_ERR_SCENE, "BVH is not a tree (node count exceeds buffer)");
+                refs[side] = (int32_t)L.nodes.size();
+                cnts[side] = -1;
+                L.nodes.push_back(Node{});
+                work.push_back({c, refs[side], it.depth + 1});
+            }
+        }
+        nd.lref = refs[0]; nd.rref = refs[1]; nd.lcnt = cnts[0]; nd.rcnt = cnts[1];
+        L.nodes[(size_t)it.node] = nd;
+    }
+    L.info.nodes = (uint32_t)L.nodes.size();
+    // The device stack parks at most one left child per internal ancestor.
+    L.info.max_stack = max_depth + 1;
+    if (L.info.max_stack >= (uint32_t)kStackMax) return fail(PT_ERR_SCENE, "BVH deeper than the device traversal stack");
+
+    // Light table (intersection-logic.wgsl:217-285): entry k for k in [0, Ntri].
+    int32_t es[4], ee[4], n[4];
+    int32_t ntri = 0;
+    for (int s = 0; s < 4; ++s) {
+        es[s] = wgsl_i32(tri[8 + 2 * s]);
+        ee[s] = wgsl_i32(tri[9 + 2 * s]);
+        n[s] = (es[s] != -1) ? (ee[s] - es[s]) / 4 : 0;
+        ntri += n[s];
+    }
+    if (ntri <= 0) return fail(PT_ERR_SCENE, "scene has no emissive triangles (sample_area_lights needs one)");
+    L.ntri = ntri;
+    const int32_t vs = wgsl_i32(P.at(2));
+    for (int32_t k = 0; k <= ntri; ++k) {
+        int32_t idx;
+        if (k < n[0]) idx = k * 4 + es[0];
+        else if (k < n[0] + n[1]) idx = (k - n[0]) * 4 + es[1];
+        else if (k < n[0] + n[1] + n[2]) idx = (k - n[0] - n[1]) * 4 + es[2];
+        else idx = (k - n[0] - n[1] - n[2]) * 4 + es[3];
+        Light lt{};
+        float* dst[3] = {lt.p0, lt.p1, lt.p2};
+        for (int j = 0; j < 3; ++j) {
+            const int32_t i = (wgsl_i32(P.at(idx + j)) - 1) * 3;
+            for (int c = 0; c < 3; ++c) dst[j][c] = P.at(vs + i + c);
+        }
+        L.lights.push_back(lt);
+    }
+    L.info.emissive_tris = (uint32_t)ntri;
+    return PT_OK;
+}
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct pt_scene {
+    int device = 0;
+    void* d_mem = nullptr;
+    SceneView view{};
+    pt_scene_info info{};
+    hipStream_t stream = nullptr;
+    float* d_accum = nullptr;  // scratch for the blocking host-buffer calls
+    size_t accum_cap = 0;
+    Counters* d_counters = nullptr;
+};
+
+extern "C" {
+
+int pt_abi_version(void) { return PT_ABI_VERSION; }
+
+const char* pt_last_error(void) { return g_err.c_str(); }
+
+int pt_device_count(int* count_out) {
+    if (!count_out) return fail(PT_ERR_INVALID, "count_out is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count_out = n;
+    return PT_OK;
+}
+
+int pt_scene_create(const float* triangle_data, size_t triangle_len, const float* bvh_data, size_t bvh_len, int device,
+                    pt_scene** scene_out) {
+    if (!triangle_data || !bvh_data || !scene_out) return fail(PT_ERR_INVALID, "null argument");
+    *scene_out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PT_ERR_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(PT_ERR_NODEVICE, "device ordinal out of range");
+    HostLayout L;
+    int rc = build_layout(triangle_data, triangle_len, bvh_data, bvh_len, L);
+    if (rc != PT_OK) return rc;
+    HIP_TRY(hipSetDevice(device));
+    const size_t o_nodes = 0;
+    const size_t o_tris = align_up(o_nodes + L.nodes.size() * sizeof(Node), 256);
+    const size_t o_mats = align_up(o_tris + std::max<size_t>(1, L.tris.size()) * sizeof(Tri), 256);
+    const size_t o_lights = align_up(o_mats + L.mats.size() * sizeof(Material), 256);
+    const size_t o_cnt = align_up(o_lights + L.lights.size() * sizeof(Light), 256);
+    const size_t total = align_up(o_cnt + sizeof(Counters), 256);
+    pt_scene* s = new pt_scene();
+    s->device = device;
+    if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
+    char* base = static_cast<char*>(s->d_mem);
+    auto up = [&](size_t off, const void* src, size_t bytes) { return bytes ? hipMemcpy(base + off, src, bytes, hipMemcpyHostToDevice) : hipSuccess; };
+    if (up(o_nodes, L.nodes.data(), L.nodes.size() * sizeof(Node)) != hipSuccess ||
+        up(o_tris, L.tris.data(), L.tris.size() * sizeof(Tri)) != hipSuccess ||
+        up(o_mats, L.mats.data(), L.mats.size() * sizeof(Material)) != hipSuccess ||
+        up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess ||
+        hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        pt_scene_destroy(s);
+        return fail(PT_ERR_HIP, "scene upload failed");
+    }
+    s->view.nodes = reinterpret_cast<const Node*>(base + o_nodes);
+    s->view.tris = reinterpret_cast<const Tri*>(base + o_tris);
+    s->view.mats = reinterpret_cast<const Material*>(base + o_mats);
+    s->view.lights = reinterpret_cast<const Light*>(base + o_lights);
+    s->view.n_nodes = (int32_t)L.nodes.size();
+    s->view.n_tris = (int32_t)L.tris.size();
+    s->view.n_mats = (int32_t)L.mats.size();
+    s->view.n_lights = L.ntri;
+    s->view.f_ntri = (float)L.ntri;
+    s->view.inv_ntri = 1.0f / (float)L.ntri;  // intersection-logic.wgsl:284
+    s->view.max_stack = (int32_t)L.info.max_stack;
+    s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);
+    s->info = L.info;
+    s->info.device_bytes = total;
+    *scene_out = s;
+    return PT_OK;
+}
+
+void pt_scene_destroy(pt_scene* s) {
+    if (!s) return;
+    hipSetDevice(s->device);
+    if (s->stream) { hipStreamSynchronize(s->stream); hipStreamDestroy(s->stream); }
+    if (s->d_accum) hipFree(s->d_accum);
+    if (s->d_mem) hipFree(s->d_mem);
+    delete s;
+}
+
+int pt_scene_get_info(const pt_scene* s, pt_scene_info* out) {
+    if (!s || !out) return fail(PT_ERR_INVALID, "null argument");
+    *out = s->info;
+    return PT_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// meta (program-raymarch.ts:79-92) -> FrameParams.  view_half_h uses the pinned tan
+// (program-raymarch.wgsl:62); it is uniform, so it is evaluated once here.
+int make_params(const float* meta, int max_depth, FrameParams& fp) {
+    if (!meta) return fail(PT_ERR_INVALID, "meta is NULL");
+    const float W = meta[0], H = meta[1];
+    if (!(W >= 1.0f && H >= 1.0f && W <= 32768.0f && H <= 32768.0f) || W != std::floor(W) || H != std::floor(H))
+        return fail(PT_ERR_INVALID, "meta[0..1] must be integral resolutions in [1, 32768]");
+    if (max_depth < -1 || max_depth > 1024) return fail(PT_ERR_INVALID, "max_depth out of range");
+    std::memset(&fp, 0, sizeof fp);
+    fp.W = W; fp.H = H;
+    fp.inv_w = meta[8]; fp.inv_h = meta[9];
+    fp.aspect = meta[10];
+    fp.focal = meta[2];
+    fp.view_half_h = (2.0f * meta[2]) * tan_p(meta[3] * 0.5f);
+    fp.rr_prob = meta[45];
+    for (int i = 0; i < 4; ++i) fp.cam[i] = meta[4 + i];
+    for (int i = 0; i < 16; ++i) fp.M[i] = meta[28 + i];
+    fp.width = (uint32_t)W; fp.height = (uint32_t)H;
+    fp.direct_only = meta[46] > 0.0f ? 1 : 0;
+    fp.max_depth = max_depth < 0 ? 16 : max_depth;
+    return PT_OK;
+}
+
+int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframes, uint32_t stride, int max_depth,
+                int mode, bool accum, float* d_out, Counters* d_cnt, hipStream_t stream) {
+    FrameParams fp;
+    int rc = make_params(meta, max_depth, fp);
+    if (rc != PT_OK) return rc;
+    if (mode != PT_MODE_AUTO && mode != PT_MODE_MEGAKERNEL && mode != PT_MODE_WAVEFRONT)
+        return fail(PT_ERR_INVALID, "unknown mode");
+    if (accum && (uint64_t)frame0 + (uint64_t)(nframes ? nframes - 1 : 0) * stride >= (1ull << 24))
+        return fail(PT_ERR_INVALID, "frame index >= 2^24 (t_k = u32(f32(k)) would round)");
+    HIP_TRY(hipSetDevice(s->device));
+    if (nframes == 0) return PT_OK;
+    HIP_TRY(launch_mega(s->view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt, stream));
+    return PT_OK;
+}
+
+int ensure_accum(pt_scene* s, size_t n) {
+    if (s->accum_cap >= n) return PT_OK;
+    if (s->d_accum) hipFree(s->d_accum);
+    s->d_accum = nullptr;
+    s->accum_cap = 0;
+    if (hipMalloc(&s->d_accum, n * sizeof(float)) != hipSuccess) return fail(PT_ERR_NOMEM, "hipMalloc accumulator");
+    s->accum_cap = n;
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pt_render_async(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
+                    int max_depth, int mode, float* d_accum, pt_counters* d_counters, void* stream) {
+    if (!s || !d_accum) return fail(PT_ERR_INVALID, "null argument");
+    return render_impl(s, meta, frame0, nframes, frame_stride, max_depth, mode, true, d_accum,
+                       reinterpret_cast<Counters*>(d_counters), static_cast<hipStream_t>(stream));
+}
+
+int pt_render(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
+              int max_depth, int mode, float* accum, pt_counters* counters) {
+    if (!s || !accum || !meta) return fail(PT_ERR_INVALID, "null argument");
+    FrameParams fp;
+    int rc = make_params(meta, max_depth, fp);
+    if (rc != PT_OK) return rc;
+    const size_t n = (size_t)fp.width * fp.height * 3;
+    HIP_TRY(hipSetDevice(s->device));
+    if ((rc = ensure_accum(s, n)) != PT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(s->d_accum, accum, n * sizeof(float), hipMemcpyHostToDevice, s->stream));
+    if (counters) HIP_TRY(hipMemsetAsync(s->d_counters, 0, sizeof(Counters), s->stream));
+    rc = render_impl(s, meta, frame0, nframes, frame_stride, max_depth, mode, true, s->d_accum,
+                     counters ? s->d_counters : nullptr, s->stream);
+    if (rc != PT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(accum, s->d_accum, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    if (counters) HIP_TRY(hipMemcpyAsync(counters, s->d_counters, sizeof(Counters), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return PT_OK;
+}
+
+int pt_frame_async(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float* d_radiance, void* stream) {
+    if (!s || !d_radiance) return fail(PT_ERR_INVALID, "null argument");
+    return render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_MEGAKERNEL, false, d_radiance, nullptr,
+                       static_cast<hipStream_t>(stream));
+}
+
+int pt_frame(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float* radiance) {
+    if (!s || !radiance || !meta) return fail(PT_ERR_INVALID, "null argument");
+    FrameParams fp;
+    int rc = make_params(meta, max_depth, fp);
+    if (rc != PT_OK) return rc;
+    const size_t n = (size_t)fp.width * fp.height * 3;
+    HIP_TRY(hipSetDevice(s->device));
+    if ((rc = ensure_accum(s, n)) != PT_OK) return rc;
+    rc = render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_MEGAKERNEL, false, s->d_accum, nullptr, s->stream);
+    if (rc != PT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(radiance, s->d_accum, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return PT_OK;
+}
+
+int pt_tonemap(const float* acc, size_t npix, uint32_t sample_runs, uint8_t* rgba) {
+    if (!acc || !rgba || sample_runs == 0) return fail(PT_ERR_INVALID, "null argument or zero sample_runs");
+    auto to_int32 = [](double v) -> int32_t {  // ECMAScript ToInt32
+        if (!std::isfinite(v)) return 0;
+        double m = std::fmod(std::trunc(v), 4294967296.0);
+        if (m < 0) m += 4294967296.0;
+        return (int32_t)(uint32_t)m;
+    };
+    auto u8 = [](int32_t v) -> uint8_t { return v < 0 ? 0 : (v > 255 ? 255 : (uint8_t)v); };
+    for (size_t i = 0; i < npix; ++i) {
+        const double r = (double)acc[3 * i] / sample_runs, g = (double)acc[3 * i + 1] / sample_runs,
+                     b = (double)acc[3 * i + 2] / sample_runs;
+        const double lum = (r + g + b) / 3.0;
+        const double f = std::pow(lum / (lum + 1.0), 0.01);
+        rgba[4 * i] = u8(to_int32(r * f * 255.0));
+        rgba[4 * i + 1] = u8(to_int32(g * f * 255.0));
+        rgba[4 * i + 2] = u8(to_int32(b * f * 255.0));
+        rgba[4 * i + 3] = 255;
+    }
+    return PT_OK;
+}
+
+int pt_selftest_math(int device, int fn, const float* a, const float* b, float* out, size_t n) {
+    if (!a || !b || !out || n == 0 || n > (1u << 28)) return fail(PT_ERR_INVALID, "bad argument");
+    if (fn < 0 || fn >= PT_MATH_COUNT_) return fail(PT_ERR_INVALID, "unknown math fn");
+    HIP_TRY(hipSetDevice(device));
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    HIP_TRY(hipMalloc(&da, n * 4));
+    HIP_TRY(hipMalloc(&db, n * 4));
+    HIP_TRY(hipMalloc(&dout, n * 4));
+    hipMemcpy(da, a, n * 4, hipMemcpyHostToDevice);
+    hipMemcpy(db, b, n * 4, hipMemcpyHostToDevice);
+    hipError_t e = launch_selftest_math(fn, da, db, dout, (int)n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
+    hipFree(da); hipFree(db); hipFree(dout);
+    if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
+    return PT_OK;
+}
+
+}  // extern "C"

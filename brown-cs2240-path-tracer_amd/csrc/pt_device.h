@@ -1,0 +1,213 @@
+// pt_device.h — device-side building blocks shared by the megakernel and the
+// wavefront kernels: ray/box and ray/triangle tests, BVH traversal with a
+// per-lane LDS stack, light sampling, hemisphere sampling, camera rays.
+// Every function cites the WGSL it restates; numerics follow pt_math.h.
+#pragma once
+#include "pt_layout.h"
+#include "pt_math.h"
+
+namespace pt {
+
+constexpr int kStackMax = 32;  // > max traversal stack of any accepted tree (host checks)
+
+struct Ray {
+    f3 o, d, inv;
+};
+
+struct Counters {
+    uint64_t samples, ext_queries, shadow_queries, nodes, tri_tests, box_tests;
+};
+
+// ray-bbox-intersection.wgsl:1-31 (Tavian's slab test; minNum/maxNum NaN handling)
+__device__ __forceinline__ float ray_box(const Ray& r, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
+    float tmin = -3.0e+38f, tmax = 3.0e+38f;
+    float t1 = (mnx - r.o.x) * r.inv.x, t2 = (mxx - r.o.x) * r.inv.x;
+    tmin = fmaxf(tmin, fminf(t1, t2));
+    tmax = fminf(tmax, fmaxf(t1, t2));
+    t1 = (mny - r.o.y) * r.inv.y; t2 = (mxy - r.o.y) * r.inv.y;
+    tmin = fmaxf(tmin, fminf(t1, t2));
+    tmax = fminf(tmax, fmaxf(t1, t2));
+    t1 = (mnz - r.o.z) * r.inv.z; t2 = (mxz - r.o.z) * r.inv.z;
+    tmin = fmaxf(tmin, fminf(t1, t2));
+    tmax = fminf(tmax, fmaxf(t1, t2));
+    return (tmax > fmaxf(tmin, 0.0f)) ? (tmin > 0.0f ? tmin : tmax) : -1.0f;
+}
+
+// ray-triangle-intersection.wgsl:1-42 restricted to what the traversal needs
+// (t); point and normal are rebuilt for the winning record only.
+__device__ __forceinline__ void test_leaf(const Tri* __restrict__ tris, int first, int cnt, const Ray& r, float& best_t,
+                                          int& best) {
+    const float eps = 1e-8f;
+    for (int i = first; i < first + cnt; ++i) {
+        const float4* tp = reinterpret_cast<const float4*>(tris + i);
+        float4 a = tp[0], b = tp[1], c = tp[2];
+        f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
+        f3 rce2 = cross(r.d, e2);
+        float det = dot(e1, rce2);
+        if (det > -eps && det < eps) continue;
+        float inv_det = 1.0f / det;
+        f3 s = r.o - v0;
+        float u = inv_det * dot(s, rce2);
+        if (u < 0.0f || u > 1.0f) continue;
+        f3 sce1 = cross(s, e1);
+        float v = inv_det * dot(r.d, sce1);
+        if (v < 0.0f || u + v > 1.0f) continue;
+        float t = inv_det * dot(e2, sce1);
+        if (t > eps && (best_t < 0.0f || t < best_t)) { best_t = t; best = i; }
+    }
+}
+
+// intersection-logic.wgsl:1-215.  The reference keeps -1 markers on a 64-entry
+// private stack; popping skips them, so the live entries behave exactly like
+// "pop node, push left then right (right on top)".  Here the right child is
+// taken directly and the left one parked on this lane's LDS stack
+// (stack[k * stride], lane-minor: conflict-free).  Same visit order, same
+// pruning with the box's exit distance, same strict-< closest hit.
+template <bool COUNT>
+__device__ __forceinline__ int trace(const SceneView& sc, const Ray& r, float& t_out, int32_t* stack, int stride,
+                                     Counters& cnt) {
+    float best_t = -1.0f;
+    int best = -1;
+    int node = 0, sp = 0;
+    const float4* __restrict__ nodes4 = reinterpret_cast<const float4*>(sc.nodes);
+    while (true) {
+        const float4* np = nodes4 + 4 * node;
+        float4 a = np[0], b = np[1], c = np[2];
+        int4 d = reinterpret_cast<const int4*>(np)[3];
+        if (COUNT) { cnt.nodes++; cnt.box_tests += 2; }
+        float ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
+        float rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
+        bool li = 0.0f < ld, ri = 0.0f < rd;
+        bool lleaf = d.z >= 0, rleaf = d.w >= 0;
+        if (li && lleaf) { test_leaf(sc.tris, d.x, d.z, r, best_t, best); if (COUNT) cnt.tri_tests += d.z; }
+        if (ri && rleaf) { test_leaf(sc.tris, d.y, d.w, r, best_t, best); if (COUNT) cnt.tri_tests += d.w; }
+        bool tl = li && !lleaf && !(best_t > 0.0f && ld > best_t);
+        bool tr = ri && !rleaf && !(best_t > 0.0f && rd > best_t);
+        if (tl && tr) {
+            stack[sp * stride] = d.x;
+            ++sp;
+            node = d.y;
+        } else if (tl) {
+            node = d.x;
+        } else if (tr) {
+            node = d.y;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = stack[sp * stride];
+        }
+    }
+    t_out = best_t;
+    return best;
+}
+
+struct Hit {
+    f3 p, n;
+    int mat;
+};
+
+// Intersection{point, normal} for the winning record (ray-triangle-intersection.wgsl:30-36)
+__device__ __forceinline__ Hit hit_data(const SceneView& sc, const Ray& r, int rec, float t) {
+    const float4* tp = reinterpret_cast<const float4*>(sc.tris + rec);
+    float4 a = tp[0], b = tp[1], c = tp[2];
+    Hit h;
+    h.p = madd(r.o, r.d, t);
+    h.n = normalize(cross(mk(b.x, b.y, b.z), mk(c.x, c.y, c.z)));
+    h.mat = __builtin_bit_cast(int, a.w);
+    return h;
+}
+
+struct Mat {
+    float Ns, illum;
+    f3 Kd, Ks, Ke;
+};
+__device__ __forceinline__ Mat load_mat(const SceneView& sc, int id) {
+    const float4* mp = reinterpret_cast<const float4*>(sc.mats + id);
+    float4 a = mp[0], b = mp[1], c = mp[2], e = mp[3];
+    Mat m;
+    m.Ns = a.x; m.illum = a.z;
+    m.Kd = mk(b.x, b.y, b.z); m.Ks = mk(c.x, c.y, c.z); m.Ke = mk(e.x, e.y, e.z);
+    return m;
+}
+
+// samplers.wgsl:70-80
+__device__ __forceinline__ f3 sample_triangle(f3 p0, f3 p1, f3 p2, uint32_t seed) {
+    float ux, uy;
+    hash2(seed, ux, uy);
+    float su0 = sqrtf(ux);
+    float bx = 1.0f - su0, by = uy * su0;
+    float bz = (1.0f - bx) - by;
+    return mk(fmaf(bz, p2.x, fmaf(by, p1.x, bx * p0.x)), fmaf(bz, p2.y, fmaf(by, p1.y, bx * p0.y)),
+              fmaf(bz, p2.z, fmaf(by, p1.z, bx * p0.z)));
+}
+
+// intersection-logic.wgsl:217-285: uniform emissive triangle, uniform point on it.
+// Returns the light direction; the MC weight is sc.inv_ntri.
+__device__ __forceinline__ f3 sample_area_lights(const SceneView& sc, f3 x, uint32_t seed) {
+    int k = (int)(hash1(seed * 7u + 11u) * sc.f_ntri);
+    const float4* lp = reinterpret_cast<const float4*>(sc.lights + k);
+    float4 a = lp[0], b = lp[1], c = lp[2];
+    f3 pt = sample_triangle(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), seed * 11u + 17u);
+    return normalize(pt - x);
+}
+
+// samplers.wgsl:15-46: cosine hemisphere around n (Duff et al. 2017 ONB)
+__device__ __forceinline__ f3 sample_hemisphere(f3 N, uint32_t seed, float& pdf) {
+    float xi1, xi2;
+    hash2(seed * 7u + 11u, xi1, xi2);
+    float phi = (2.0f * kPI) * xi1;
+    float theta = acos_p(sqrtf(xi2));
+    float sp, cp, st, ct;
+    sincos_p(phi, sp, cp);
+    sincos_p(theta, st, ct);
+    float nx = cp * st, ny = sp * st, nz = ct;
+    float s = N.z < 0.0f ? -1.0f : 1.0f;
+    float a = -1.0f / (s + N.z);
+    float b = (N.x * N.y) * a;
+    f3 T = mk(fmaf((s * N.x) * N.x, a, 1.0f), s * b, (-s) * N.x);
+    f3 B = mk(b, fmaf(N.y * N.y, a, s), -N.y);
+    pdf = ct / kPI;
+    return mk(fmaf(N.x, nz, fmaf(B.x, ny, T.x * nx)), fmaf(N.y, nz, fmaf(B.y, ny, T.y * nx)),
+              fmaf(N.z, nz, fmaf(B.z, ny, T.z * nx)));
+}
+
+// ray_with_epsilon, data-structs.wgsl:59-61 (w = 1 / 0 lanes are never read)
+__device__ __forceinline__ Ray ray_eps(f3 p, f3 d) {
+    Ray r;
+    r.o = mk(fmaf(0.001f, d.x, p.x), fmaf(0.001f, d.y, p.y), fmaf(0.001f, d.z, p.z));
+    r.d = d;
+    r.inv = rcp3(d);
+    return r;
+}
+
+// program-raymarch.wgsl:50-76: pixel seed chain, jittered pinhole ray, radiance seed.
+__device__ __forceinline__ Ray camera_ray(const FrameParams& fp, uint32_t x, uint32_t y, uint32_t t, uint32_t& seed_out) {
+    uint32_t index = x + y * fp.width;
+    uint32_t ts = index * 16787u + t;
+    ts = hash1u(ts);
+    ts = hash1u(ts);
+    float jx, jy;
+    hash2(ts, jx, jy);
+    float gx = (float)x + (jx - 0.5f), gy = (float)y + (jy - 0.5f);
+    float norm_x = fmaf(gx + 0.5f, fp.inv_w, -0.5f);
+    float norm_y = fmaf(((fp.H - 1.0f) - gy) + 0.5f, fp.inv_h, -0.5f);
+    float vhw = fp.view_half_h * fp.aspect;
+    float vx = vhw * norm_x, vy = fp.view_half_h * norm_y;
+    ts = hash1u(ts);
+    const float* M = fp.M;
+    float pz = -fp.focal;
+    float px = fmaf(M[12], 1.0f, fmaf(M[8], pz, fmaf(M[4], vy, M[0] * vx)));
+    float py = fmaf(M[13], 1.0f, fmaf(M[9], pz, fmaf(M[5], vy, M[1] * vx)));
+    float pzw = fmaf(M[14], 1.0f, fmaf(M[10], pz, fmaf(M[6], vy, M[2] * vx)));
+    float pw = fmaf(M[15], 1.0f, fmaf(M[11], pz, fmaf(M[7], vy, M[3] * vx)));
+    float dx = px - fp.cam[0], dy = py - fp.cam[1], dz = pzw - fp.cam[2], dw = pw - fp.cam[3];
+    float len = sqrtf(fmaf(dw, dw, fmaf(dz, dz, fmaf(dy, dy, dx * dx))));  // vec4 normalize
+    Ray r;
+    r.o = mk(fp.cam[0], fp.cam[1], fp.cam[2]);
+    r.d = mk(dx / len, dy / len, dz / len);
+    r.inv = rcp3(r.d);
+    seed_out = hash1u(ts + (index * 67u + t));
+    return r;
+}
+
+}  // namespace pt

@@ -1,0 +1,89 @@
+// pt_layout.h — device-resident scene layout (HBM), built once by pt_scene_create
+// from the reference's packed buffers (packer.ts:4-137 layouts).
+//
+// The reference walks a float-encoded pre-order tree (17-float nodes + inline
+// leaf payloads holding 1-based float vertex indices) and gathers 9 vertex
+// floats per triangle test.  Here the same tree is re-encoded for 16-byte
+// vector loads:
+//   nodes[]  64 B: both child AABBs + two child refs (one node = one traversal
+//            step of intersection-logic.wgsl:31-212; the root is node 0 = bvh[6])
+//   tris[]   48 B per leaf reference, leaves contiguous in traversal order:
+//            v0 | material id, e1 = v1 - v0, e2 = v2 - v0 (f32, exactly the values
+//            ray-triangle-intersection.wgsl:6-7 computes per test)
+//   mats[]   64 B: Ns Ni illum | Kd | Ks | Ke (program-raymarch.wgsl:87-102)
+//   lights[] 48 B: the Ntri emissive triangles in sample_area_lights' slot order,
+//            plus one extra entry k == Ntri for hash1 == 1.0 (the reference's
+//            out-of-range else-branch, resolved with Tint's clamped reads).
+#pragma once
+#include <stdint.h>
+
+namespace pt {
+
+struct alignas(16) Node {
+    float lmin[3];
+    float lmax[3];
+    float rmin[3];
+    float rmax[3];
+    int32_t lref, rref;  // internal child: node index; leaf child: first tri record
+    int32_t lcnt, rcnt;  // < 0: internal child; >= 0: leaf with that many triangles
+};
+static_assert(sizeof(Node) == 64, "node is 4 x 16 B");
+
+struct alignas(16) Tri {
+    float v0[3];
+    int32_t mat;
+    float e1[3];
+    int32_t pad0;
+    float e2[3];
+    int32_t pad1;
+};
+static_assert(sizeof(Tri) == 48, "tri record is 3 x 16 B");
+
+struct alignas(16) Material {
+    float Ns, Ni, illum, pad0;
+    float Kd[3], pad1;
+    float Ks[3], pad2;
+    float Ke[3], pad3;
+};
+static_assert(sizeof(Material) == 64, "material is 4 x 16 B");
+
+struct alignas(16) Light {
+    float p0[3], pad0;
+    float p1[3], pad1;
+    float p2[3], pad2;
+};
+static_assert(sizeof(Light) == 48, "light is 3 x 16 B");
+
+// Read-only scene view passed to kernels by value.
+struct SceneView {
+    const Node* nodes;
+    const Tri* tris;
+    const Material* mats;
+    const Light* lights;
+    int32_t n_nodes;
+    int32_t n_tris;
+    int32_t n_mats;
+    int32_t n_lights;   // Ntri (table holds n_lights + 1 entries)
+    float f_ntri;       // f32(Ntri)
+    float inv_ntri;     // 1.0 / f32(Ntri)
+    int32_t max_stack;  // deepest traversal stack the tree can produce
+    int32_t pad;
+};
+
+// Per-call camera/settings block derived from the reference's 48-float meta
+// (program-raymarch.wgsl:11-22, program-raymarch.ts:79-92).
+struct FrameParams {
+    float W, H;           // meta[0], meta[1]
+    float inv_w, inv_h;   // meta[8], meta[9]
+    float aspect;         // meta[10]
+    float focal;          // meta[2]
+    float view_half_h;    // 2 * focal * tan(vfov * 0.5), pinned tan, computed once on host
+    float rr_prob;        // meta[45]
+    float cam[4];         // meta[4..7]
+    float M[16];          // cam_to_world, meta[28..43], column-major
+    uint32_t width, height;  // u32(meta[0]), u32(meta[1])
+    int32_t direct_only;  // meta[46] > 0
+    int32_t max_depth;    // literal 16 in `while(depth <= 16)`, program-raymarch.wgsl:118
+};
+
+}  // namespace pt

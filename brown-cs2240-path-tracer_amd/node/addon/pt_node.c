@@ -1,0 +1,285 @@
+/*
+ * pt_node.c — N-API addon (N-API v8, Node >= 12.22) binding include/pt_hip.h for the Node
+ * host.  This is the thin layer between the reference-shaped JS API (node/lib/program-entry.js,
+ * replacing src/program-raymarch.ts:50-357) and libpt_hip.so.  Typed arrays are passed
+ * through without copies; render() runs as napi_async_work off the event loop and resolves a
+ * Promise (the reference's mapAsync().then chain, program-raymarch.ts:273).  Errors become JS
+ * Error objects carrying pt_last_error().
+ */
+#include <node_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/pt_hip.h"
+
+#define CHECK_NAPI(env, call)                                                  \
+    do {                                                                       \
+        if ((call) != napi_ok) {                                               \
+            napi_throw_error((env), NULL, "N-API call failed: " #call);        \
+            return NULL;                                                       \
+        }                                                                      \
+    } while (0)
+
+static napi_value throw_pt(napi_env env, int rc) {
+    char buf[512];
+    snprintf(buf, sizeof buf, "pt_hip error %d: %s", rc, pt_last_error());
+    napi_throw_error(env, NULL, buf);
+    return NULL;
+}
+
+static int get_f32(napi_env env, napi_value v, float** data, size_t* len) {
+    bool is_ta = false;
+    if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return 0;
+    napi_typedarray_type t;
+    void* p;
+    napi_value ab;
+    size_t off;
+    if (napi_get_typedarray_info(env, v, &t, len, &p, &ab, &off) != napi_ok || t != napi_float32_array) return 0;
+    *data = (float*)p;
+    return 1;
+}
+
+static int get_u8(napi_env env, napi_value v, uint8_t** data, size_t* len) {
+    bool is_ta = false;
+    if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return 0;
+    napi_typedarray_type t;
+    void* p;
+    napi_value ab;
+    size_t off;
+    if (napi_get_typedarray_info(env, v, &t, len, &p, &ab, &off) != napi_ok ||
+        (t != napi_uint8_array && t != napi_uint8_clamped_array))
+        return 0;
+    *data = (uint8_t*)p;
+    return 1;
+}
+
+static int get_i32(napi_env env, napi_value v, int32_t* out) { return napi_get_value_int32(env, v, out) == napi_ok; }
+static int get_u32(napi_env env, napi_value v, uint32_t* out) { return napi_get_value_uint32(env, v, out) == napi_ok; }
+
+static void scene_finalize(napi_env env, void* data, void* hint) {
+    (void)env; (void)hint;
+    pt_scene_destroy((pt_scene*)data);
+}
+
+static pt_scene* get_scene(napi_env env, napi_value v) {
+    void* p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
+    return (pt_scene*)p;
+}
+
+static napi_value counters_obj(napi_env env, const pt_counters* c) {
+    napi_value o, v;
+    napi_create_object(env, &o);
+    const char* names[6] = {"samples", "ext_queries", "shadow_queries", "nodes", "tri_tests", "box_tests"};
+    const uint64_t vals[6] = {c->samples, c->ext_queries, c->shadow_queries, c->nodes, c->tri_tests, c->box_tests};
+    for (int i = 0; i < 6; ++i) {
+        napi_create_double(env, (double)vals[i], &v);
+        napi_set_named_property(env, o, names[i], v);
+    }
+    return o;
+}
+
+/* abiVersion() -> number */
+static napi_value js_abi_version(napi_env env, napi_callback_info info) {
+    (void)info;
+    napi_value r;
+    CHECK_NAPI(env, napi_create_int32(env, pt_abi_version(), &r));
+    return r;
+}
+
+/* deviceCount() -> number */
+static napi_value js_device_count(napi_env env, napi_callback_info info) {
+    (void)info;
+    int n = 0;
+    int rc = pt_device_count(&n);
+    if (rc) return throw_pt(env, rc);
+    napi_value r;
+    CHECK_NAPI(env, napi_create_int32(env, n, &r));
+    return r;
+}
+
+/* sceneCreate(triangle_data: Float32Array, bvh_data: Float32Array, device: number) -> external */
+static napi_value js_scene_create(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    float *tri, *bvh;
+    size_t tl, bl;
+    int32_t dev = 0;
+    if (argc < 2 || !get_f32(env, argv[0], &tri, &tl) || !get_f32(env, argv[1], &bvh, &bl) ||
+        (argc > 2 && !get_i32(env, argv[2], &dev))) {
+        napi_throw_type_error(env, NULL, "sceneCreate(Float32Array triangle_data, Float32Array bvh_data, device?)");
+        return NULL;
+    }
+    pt_scene* s = NULL;
+    int rc = pt_scene_create(tri, tl, bvh, bl, dev, &s);
+    if (rc) return throw_pt(env, rc);
+    napi_value ext;
+    CHECK_NAPI(env, napi_create_external(env, s, scene_finalize, NULL, &ext));
+    return ext;
+}
+
+/* sceneInfo(scene) -> object */
+static napi_value js_scene_info(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
+    if (!s) { napi_throw_type_error(env, NULL, "sceneInfo(scene)"); return NULL; }
+    pt_scene_info si;
+    int rc = pt_scene_get_info(s, &si);
+    if (rc) return throw_pt(env, rc);
+    napi_value o, v;
+    napi_create_object(env, &o);
+#define SET(name) napi_create_double(env, (double)si.name, &v); napi_set_named_property(env, o, #name, v);
+    SET(nodes) SET(leaves) SET(leaf_refs) SET(max_leaf) SET(max_stack) SET(materials) SET(emissive_tris) SET(vertices)
+    SET(device_bytes)
+#undef SET
+    return o;
+}
+
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref refs[3]; /* scene, meta, accum kept alive while the worker runs */
+    pt_scene* scene;
+    float meta[48];
+    uint32_t frame0, nframes, stride;
+    int32_t max_depth, mode;
+    float* accum;
+    pt_counters counters;
+    int rc;
+    char err[512];
+} render_job;
+
+static void render_execute(napi_env env, void* data) {
+    (void)env;
+    render_job* j = (render_job*)data;
+    j->rc = pt_render(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->accum, &j->counters);
+    if (j->rc) snprintf(j->err, sizeof j->err, "pt_hip error %d: %s", j->rc, pt_last_error());
+}
+
+static void render_complete(napi_env env, napi_status status, void* data) {
+    render_job* j = (render_job*)data;
+    if (status == napi_ok && j->rc == 0) {
+        napi_resolve_deferred(env, j->deferred, counters_obj(env, &j->counters));
+    } else {
+        napi_value msg, e;
+        napi_create_string_utf8(env, j->rc ? j->err : "render cancelled", NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, NULL, msg, &e);
+        napi_reject_deferred(env, j->deferred, e);
+    }
+    for (int i = 0; i < 3; ++i) napi_delete_reference(env, j->refs[i]);
+    napi_delete_async_work(env, j->work);
+    free(j);
+}
+
+/* parse (scene, meta, frame0, nframes, stride, maxDepth, mode, accum) */
+static int parse_render_args(napi_env env, napi_callback_info info, render_job* j, napi_value argv[8]) {
+    size_t argc = 8;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 8) return 0;
+    float* meta;
+    size_t ml, al;
+    j->scene = get_scene(env, argv[0]);
+    if (!j->scene || !get_f32(env, argv[1], &meta, &ml) || ml < 48) return 0;
+    memcpy(j->meta, meta, sizeof j->meta);
+    if (!get_u32(env, argv[2], &j->frame0) || !get_u32(env, argv[3], &j->nframes) || !get_u32(env, argv[4], &j->stride) ||
+        !get_i32(env, argv[5], &j->max_depth) || !get_i32(env, argv[6], &j->mode) || !get_f32(env, argv[7], &j->accum, &al))
+        return 0;
+    if (al != (size_t)j->meta[0] * (size_t)j->meta[1] * 3) return 0;
+    return 1;
+}
+
+/* render(scene, meta, frame0, nframes, stride, maxDepth, mode, accum) -> Promise<counters> */
+static napi_value js_render(napi_env env, napi_callback_info info) {
+    napi_value argv[8];
+    render_job* j = (render_job*)calloc(1, sizeof(render_job));
+    if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
+    if (!parse_render_args(env, info, j, argv)) {
+        free(j);
+        napi_throw_type_error(env, NULL,
+                              "render(scene, Float32Array meta[48], frame0, nframes, stride, maxDepth, mode, "
+                              "Float32Array accum[W*H*3])");
+        return NULL;
+    }
+    napi_value promise, name;
+    CHECK_NAPI(env, napi_create_promise(env, &j->deferred, &promise));
+    napi_create_reference(env, argv[0], 1, &j->refs[0]);
+    napi_create_reference(env, argv[1], 1, &j->refs[1]);
+    napi_create_reference(env, argv[7], 1, &j->refs[2]);
+    napi_create_string_utf8(env, "pt_render", NAPI_AUTO_LENGTH, &name);
+    CHECK_NAPI(env, napi_create_async_work(env, NULL, name, render_execute, render_complete, j, &j->work));
+    CHECK_NAPI(env, napi_queue_async_work(env, j->work));
+    return promise;
+}
+
+/* renderSync(...same...) -> counters */
+static napi_value js_render_sync(napi_env env, napi_callback_info info) {
+    napi_value argv[8];
+    render_job j;
+    memset(&j, 0, sizeof j);
+    if (!parse_render_args(env, info, &j, argv)) {
+        napi_throw_type_error(env, NULL, "renderSync(scene, meta, frame0, nframes, stride, maxDepth, mode, accum)");
+        return NULL;
+    }
+    int rc = pt_render(j.scene, j.meta, j.frame0, j.nframes, j.stride, j.max_depth, j.mode, j.accum, &j.counters);
+    if (rc) return throw_pt(env, rc);
+    return counters_obj(env, &j.counters);
+}
+
+/* frame(scene, meta, t, maxDepth, out Float32Array[W*H*3]) */
+static napi_value js_frame(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    float *meta, *out;
+    size_t ml, ol;
+    uint32_t t;
+    int32_t md;
+    pt_scene* s = argc >= 5 ? get_scene(env, argv[0]) : NULL;
+    if (!s || !get_f32(env, argv[1], &meta, &ml) || ml < 48 || !get_u32(env, argv[2], &t) || !get_i32(env, argv[3], &md) ||
+        !get_f32(env, argv[4], &out, &ol) || ol != (size_t)meta[0] * (size_t)meta[1] * 3) {
+        napi_throw_type_error(env, NULL, "frame(scene, meta, t, maxDepth, Float32Array out[W*H*3])");
+        return NULL;
+    }
+    int rc = pt_frame(s, meta, t, md, out);
+    if (rc) return throw_pt(env, rc);
+    return NULL;
+}
+
+/* tonemap(accum Float32Array, sampleRuns, out Uint8Array[npix*4]) */
+static napi_value js_tonemap(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    float* acc;
+    uint8_t* out;
+    size_t al, ol;
+    uint32_t runs;
+    if (argc < 3 || !get_f32(env, argv[0], &acc, &al) || !get_u32(env, argv[1], &runs) || !get_u8(env, argv[2], &out, &ol) ||
+        ol != al / 3 * 4) {
+        napi_throw_type_error(env, NULL, "tonemap(Float32Array accum, sampleRuns, Uint8Array out)");
+        return NULL;
+    }
+    int rc = pt_tonemap(acc, al / 3, runs, out);
+    if (rc) return throw_pt(env, rc);
+    return NULL;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+    napi_property_descriptor props[] = {
+        {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_default, NULL},
+        {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_default, NULL},
+        {"sceneCreate", NULL, js_scene_create, NULL, NULL, NULL, napi_default, NULL},
+        {"sceneInfo", NULL, js_scene_info, NULL, NULL, NULL, napi_default, NULL},
+        {"render", NULL, js_render, NULL, NULL, NULL, napi_default, NULL},
+        {"renderSync", NULL, js_render_sync, NULL, NULL, NULL, napi_default, NULL},
+        {"frame", NULL, js_frame, NULL, NULL, NULL, napi_default, NULL},
+        {"tonemap", NULL, js_tonemap, NULL, NULL, NULL, napi_default, NULL},
+    };
+    napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

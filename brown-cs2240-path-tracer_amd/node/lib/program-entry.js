@@ -1,0 +1,61 @@
+'use strict';
+// programEntry counterpart (src/program-raymarch.ts:50-357) on the HIP core.
+//   * meta block: program-raymarch.ts:55-92 (48 f32, layout SURVEY.md §8a A2)
+//   * scene buffers: pt_scene_create replaces the storage buffers of :109-131
+//   * render_loop (:226-335): all spp frames in one device call (or `chunk`-sized calls
+//     reporting progress), t_k = k instead of the wall-clock ms, host accumulation moved
+//     onto the device; the display transform (:295-316) is `tonemap`.
+const { camera_matrices } = require('./geometry');
+const { load } = require('./addon');
+
+const MODE = { auto: 0, megakernel: 1, wavefront: 2 };
+
+/** program-raymarch.ts:55-92 */
+function make_meta(screenDimension, camera_data, scene_description, time_elapsed) {
+    const [W, H] = screenDimension;
+    const screen_dimension_inv = [1 / W, 1 / H];
+    const camera_position = camera_data.pos;
+    const camera_look = camera_data.focus.sub_v(camera_position).normalize();
+    const FOV = camera_data.heightangle;
+    const focal_length = 1;
+    const aspect_ratio = W / H;
+    const { world_to_cam, cam_to_world } = camera_matrices(camera_position, camera_look, camera_data.up);
+    const s = scene_description.Settings;
+    return new Float32Array([
+        W, H, focal_length, FOV * Math.PI / 180, ...camera_position.toArray(), 1,
+        ...screen_dimension_inv, aspect_ratio, time_elapsed || 0,
+        ...world_to_cam, ...cam_to_world,
+        s.samplesPerPixel, s.pathContinuationProb, s.directLightingOnly ? 1 : -1, 0,
+    ]);
+}
+
+/**
+ * programEntry(screenDimension, primitive_data, camera_data, scene_description, options?)
+ *   -> Promise<{accum: Float32Array(W*H*3), sample_runs, rgba: Uint8ClampedArray(W*H*4), counters, scene_info}>
+ * options: {device=0, maxDepth=16, mode='auto', frame0=0, chunk=spp, onFrames(done, total)}
+ * As in the reference only primitive_data[0] is rendered (program-raymarch.wgsl:31,33).
+ */
+async function programEntry(screenDimension, primitive_data, camera_data, scene_description, options) {
+    const o = Object.assign({ device: 0, maxDepth: 16, mode: 'auto', frame0: 0 }, options || {});
+    const pt = load();
+    const [W, H] = screenDimension;
+    const meta = make_meta(screenDimension, camera_data, scene_description, 0);
+    const scene = pt.sceneCreate(primitive_data[0].triangle_data, primitive_data[0].bvh_data, o.device);
+    const spp = scene_description.Settings.samplesPerPixel;
+    const chunk = Math.max(1, o.chunk || spp);
+    const accum = new Float32Array(W * H * 3);
+    const counters = { samples: 0, ext_queries: 0, shadow_queries: 0, nodes: 0, tri_tests: 0, box_tests: 0 };
+    const mode = typeof o.mode === 'number' ? o.mode : MODE[o.mode];
+    if (mode === undefined) throw Error(`unknown mode ${o.mode}`);
+    for (let done = 0; done < spp; done += chunk) {
+        const n = Math.min(chunk, spp - done);
+        const c = await pt.render(scene, meta, o.frame0 + done, n, 1, o.maxDepth, mode, accum);
+        for (const k of Object.keys(counters)) counters[k] += c[k];
+        if (o.onFrames) o.onFrames(done + n, spp);
+    }
+    const rgba = new Uint8ClampedArray(W * H * 4);
+    pt.tonemap(accum, spp, rgba);
+    return { accum, sample_runs: spp, rgba, counters, scene_info: pt.sceneInfo(scene) };
+}
+
+module.exports = { programEntry, make_meta, MODE };

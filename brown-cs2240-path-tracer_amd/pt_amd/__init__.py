@@ -1,0 +1,28 @@
+"""pt_amd — Python host binding of the MI355X path-tracing core (libpt_hip.so).
+
+Mirrors the reference's render-path interface (src/program-raymarch.ts:50-54,
+`programEntry(screenDimension, ctx, primitive_data, camera_data, scene_description)`)
+for Python callers: `Scene` wraps one uploaded `SceneObjectPacked`
+(triangle_data + bvh_data, src/ts-util/data-structs.ts:46-50), `Scene.render`
+is the render_loop of program-raymarch.ts:226-335 without per-frame readback,
+`tonemap` is its display transform (:295-316).
+
+The product path never falls back to CPU code: if libpt_hip.so is missing or
+no GPU is visible, calls raise `PtError`.
+"""
+from ._lib import (  # noqa: F401
+    MODE_AUTO,
+    MODE_MEGAKERNEL,
+    MODE_WAVEFRONT,
+    Counters,
+    PtError,
+    Scene,
+    SceneInfo,
+    abi_version,
+    device_count,
+    lib_path,
+    load_library,
+    selftest_math,
+    tonemap,
+)
+from .host import PackedScene, load_scene, program_entry  # noqa: F401

@@ -1,0 +1,183 @@
+"""ctypes binding of include/pt_hip.h (libpt_hip.so, built in-tree by csrc/Makefile)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_LIB_FILE = os.path.join(_PKG_ROOT, "lib", "libpt_hip.so")
+
+MODE_AUTO, MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1, 2
+MATH_FNS = ["sin", "cos", "tan", "acos", "log2", "exp2", "pow", "sqrt", "div", "hash1u", "hash1", "hash2x",
+            "hash2y", "min", "max"]
+
+_STATUS = {0: "PT_OK", -1: "PT_ERR_INVALID", -2: "PT_ERR_SCENE", -3: "PT_ERR_NOMEM", -4: "PT_ERR_HIP",
+           -5: "PT_ERR_NODEVICE"}
+
+
+class PtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("samples", "ext_queries", "shadow_queries", "nodes", "tri_tests", "box_tests")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class SceneInfo(ctypes.Structure):
+    _fields_ = [("nodes", ctypes.c_uint32), ("leaves", ctypes.c_uint32), ("leaf_refs", ctypes.c_uint32),
+                ("max_leaf", ctypes.c_uint32), ("max_stack", ctypes.c_uint32), ("materials", ctypes.c_uint32),
+                ("emissive_tris", ctypes.c_uint32), ("vertices", ctypes.c_uint32), ("device_bytes", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _LIB_FILE
+
+
+def load_library():
+    """Load libpt_hip.so; raise if it was not built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_FILE):
+        raise PtError(-4, f"{_LIB_FILE} not built (run __graft_entry__.build() or make -C csrc)")
+    L = ctypes.CDLL(_LIB_FILE)
+    p, i, u32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_size_t
+    L.pt_abi_version.restype = i
+    L.pt_last_error.restype = ctypes.c_char_p
+    L.pt_device_count.argtypes = [ctypes.POINTER(i)]
+    L.pt_scene_create.argtypes = [p, sz, p, sz, i, ctypes.POINTER(p)]
+    L.pt_scene_destroy.argtypes = [p]
+    L.pt_scene_destroy.restype = None
+    L.pt_scene_get_info.argtypes = [p, ctypes.POINTER(SceneInfo)]
+    L.pt_render.argtypes = [p, p, u32, u32, u32, i, i, p, p]
+    L.pt_render_async.argtypes = [p, p, u32, u32, u32, i, i, p, p, p]
+    L.pt_frame.argtypes = [p, p, u32, i, p]
+    L.pt_frame_async.argtypes = [p, p, u32, i, p, p]
+    L.pt_tonemap.argtypes = [p, sz, u32, p]
+    L.pt_selftest_math.argtypes = [i, i, p, p, p, sz]
+    for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math"):
+        getattr(L, fn).restype = i
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise PtError(rc, load_library().pt_last_error().decode(errors="replace"))
+
+
+def abi_version() -> int:
+    return int(load_library().pt_abi_version())
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(load_library().pt_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Scene:
+    """One `SceneObjectPacked` resident on one GPU (program-raymarch.ts:109-131)."""
+
+    def __init__(self, triangle_data, bvh_data, device: int = 0):
+        self._lib = load_library()
+        self.triangle_data = _f32(triangle_data)
+        self.bvh_data = _f32(bvh_data)
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(self._lib.pt_scene_create(_ptr(self.triangle_data), self.triangle_data.size, _ptr(self.bvh_data),
+                                         self.bvh_data.size, device, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def info(self) -> dict:
+        inf = SceneInfo()
+        _check(self._lib.pt_scene_get_info(self._h, ctypes.byref(inf)))
+        return inf.as_dict()
+
+    def render(self, meta, frame0: int, nframes: int, stride: int = 1, max_depth: int = -1, mode: int = MODE_AUTO,
+               accum: np.ndarray | None = None, counters: bool = False):
+        """Host-buffer render (blocking). Returns accum [H, W, 3] (and counters if requested)."""
+        meta = _f32(meta)
+        W, H = int(meta[0]), int(meta[1])
+        if accum is None:
+            accum = np.zeros((H, W, 3), np.float32)
+        if accum.dtype != np.float32 or not accum.flags.c_contiguous or accum.size != W * H * 3:
+            raise ValueError("accum must be a contiguous float32 array of H*W*3 elements")
+        c = Counters()
+        _check(self._lib.pt_render(self._h, _ptr(meta), frame0, nframes, stride, max_depth, mode, _ptr(accum),
+                                   ctypes.byref(c) if counters else None))
+        return (accum, c.as_dict()) if counters else accum
+
+    def render_async(self, meta, frame0: int, nframes: int, stride: int, max_depth: int, mode: int, d_accum_ptr: int,
+                     stream_ptr: int = 0, d_counters_ptr: int = 0):
+        """Device render into a caller-owned device buffer (e.g. a torch.cuda tensor's data_ptr())."""
+        meta = _f32(meta)
+        _check(self._lib.pt_render_async(self._h, _ptr(meta), frame0, nframes, stride, max_depth, mode,
+                                         ctypes.c_void_p(d_accum_ptr), ctypes.c_void_p(d_counters_ptr or None),
+                                         ctypes.c_void_p(stream_ptr or None)))
+
+    def frame(self, meta, t: int, max_depth: int = -1) -> np.ndarray:
+        """One reference dispatch: raw radiance [H, W, 3] for RNG salt t."""
+        meta = _f32(meta)
+        W, H = int(meta[0]), int(meta[1])
+        out = np.zeros((H, W, 3), np.float32)
+        _check(self._lib.pt_frame(self._h, _ptr(meta), t, max_depth, _ptr(out)))
+        return out
+
+
+def tonemap(accum, sample_runs: int) -> np.ndarray:
+    """program-raymarch.ts:295-316 display transform -> RGBA u8 [..., 4]."""
+    acc = _f32(accum)
+    npix = acc.size // 3
+    out = np.zeros(npix * 4, np.uint8)
+    _check(load_library().pt_tonemap(_ptr(acc), npix, sample_runs, _ptr(out)))
+    return out.reshape(acc.shape[:-1] + (4,)) if acc.ndim >= 2 else out
+
+
+def selftest_math(fn: str, a, b=None, device: int = 0) -> np.ndarray:
+    a = _f32(a).reshape(-1)
+    b = _f32(np.zeros_like(a) if b is None else b).reshape(-1)
+    out = np.zeros_like(a)
+    _check(load_library().pt_selftest_math(device, MATH_FNS.index(fn), _ptr(a), _ptr(b), _ptr(out), a.size))
+    return out

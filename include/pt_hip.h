@@ -1,0 +1,125 @@
+/*
+ * pt_hip.h — C ABI of the MI355X (gfx950) path-tracing core.
+ *
+ * Drop-in boundary for the reference's render path (Kauhentus/brown-cs2240-path-tracer):
+ * everything behind `programEntry(screenDimension, ctx, primitive_data, camera_data,
+ * scene_description)` (src/program-raymarch.ts:50-54) — the WebGPU device/buffer setup
+ * (:71-213), the per-frame dispatch + readback + host accumulation loop (:226-335) and the
+ * WGSL megakernel it dispatches (src/program-raymarch.wgsl:35-303 with
+ * the src/wgsl-util WGSL files) — is replaced by the calls below.  Inputs are the reference's own
+ * packed buffers, bit for bit: `SceneObjectPacked.triangle_data` / `.bvh_data`
+ * (src/ts-util/data-structs.ts:46-50, produced by src/packer.ts:4-137) and the 48-float
+ * meta block (src/program-raymarch.ts:79-92; layout SURVEY.md §8a A2).
+ *
+ * Conventions: plain pointers and sizes, no torch/HIP types in signatures (streams are
+ * `void*` = hipStream_t).  Every function returns PT_OK (0) or a negative pt_status; the
+ * message is available from pt_last_error() (thread-local).  Calls on one scene are not
+ * re-entrant; distinct scenes may be used from distinct threads.  Ownership: the library
+ * owns all device memory of a scene; the caller owns every buffer it passes in.
+ *
+ * RNG salts: the reference salts each dispatch with the wall-clock `time_elapsed` in ms
+ * (program-raymarch.ts:227,246 -> meta[11]); here frame k of a render is salted with
+ * t_k = u32(f32(k)) so results are reproducible.  meta[11] is ignored.
+ */
+#ifndef PT_HIP_H
+#define PT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+typedef enum {
+    PT_OK = 0,
+    PT_ERR_INVALID = -1,  /* bad argument (null pointer, zero size, bad meta) */
+    PT_ERR_SCENE = -2,    /* malformed packed buffers (see pt_last_error) */
+    PT_ERR_NOMEM = -3,    /* device or host allocation failed */
+    PT_ERR_HIP = -4,      /* HIP runtime error */
+    PT_ERR_NODEVICE = -5  /* no gfx950 device / bad device ordinal */
+} pt_status;
+
+typedef enum {
+    PT_MODE_AUTO = 0,       /* library picks the fastest path for the scene */
+    PT_MODE_MEGAKERNEL = 1, /* one lane per pixel, frames looped in-lane */
+    PT_MODE_WAVEFRONT = 2   /* SoA path/ray queues, per-bounce kernels, wave64 compaction */
+} pt_mode;
+
+/* Work counters (optional). A "sample" is one camera path with all its bounces
+ * and shadow rays; queries count closest-hit traversals. */
+typedef struct {
+    uint64_t samples;
+    uint64_t ext_queries;
+    uint64_t shadow_queries;
+    uint64_t nodes;      /* BVH nodes popped (each tests 2 child boxes) */
+    uint64_t tri_tests;
+    uint64_t box_tests;
+} pt_counters;
+
+typedef struct {
+    uint32_t nodes;        /* internal nodes (root included) */
+    uint32_t leaves;
+    uint32_t leaf_refs;    /* triangle references in leaves (duplicates included) */
+    uint32_t max_leaf;
+    uint32_t max_stack;    /* deepest traversal stack the tree can produce */
+    uint32_t materials;
+    uint32_t emissive_tris;/* Ntri of sample_area_lights */
+    uint32_t vertices;
+    uint64_t device_bytes; /* HBM held by the scene */
+} pt_scene_info;
+
+typedef struct pt_scene pt_scene;
+
+/* ABI version of the loaded library (== PT_ABI_VERSION when headers match). */
+int pt_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* pt_last_error(void);
+
+/* Number of visible HIP devices. */
+int pt_device_count(int* count_out);
+
+/* Upload a scene.  Replaces the storage-buffer creation of program-raymarch.ts:109-131
+ * (bindings 3 and 10).  Validates the packed layouts and re-encodes them for the device
+ * (brown-cs2240-path-tracer_amd/csrc/pt_layout.h).  device: HIP ordinal. */
+int pt_scene_create(const float* triangle_data, size_t triangle_len, const float* bvh_data, size_t bvh_len,
+                    int device, pt_scene** scene_out);
+void pt_scene_destroy(pt_scene* scene);
+int pt_scene_get_info(const pt_scene* scene, pt_scene_info* info_out);
+
+/* Render frames k = frame0 + i*frame_stride, i < nframes, each 1 spp per pixel, and add
+ * clamp(L) (v >= 0 ? v : 0, NaN -> 0) into accum in frame order — the render_loop of
+ * program-raymarch.ts:226-335 without the per-frame readback.  accum: host f32
+ * [H][W][3], in/out.  max_depth: the literal 16 of `while(depth <= 16)`
+ * (program-raymarch.wgsl:118); pass -1 for 16.  counters: nullable.  Blocking. */
+int pt_render(pt_scene* scene, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
+              int max_depth, int mode, float* accum, pt_counters* counters);
+
+/* Same on device memory, asynchronous on `stream` (hipStream_t; NULL = default stream).
+ * d_accum: device f32 [H][W][3] in/out.  d_counters: device pt_counters or NULL (added to). */
+int pt_render_async(pt_scene* scene, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
+                    int max_depth, int mode, float* d_accum, pt_counters* d_counters, void* stream);
+
+/* One reference dispatch: radiance[H][W][3] = radiance() of every pixel for RNG salt t
+ * (the resultMatrix of program-raymarch.wgsl:82-84, before host clamping). */
+int pt_frame(pt_scene* scene, const float meta[48], uint32_t t, int max_depth, float* radiance);
+int pt_frame_async(pt_scene* scene, const float meta[48], uint32_t t, int max_depth, float* d_radiance, void* stream);
+
+/* Display transform of program-raymarch.ts:295-316 on the host (JS double semantics):
+ * raw = acc/sample_runs, lum = mean(raw), out = raw * (lum/(lum+1))^0.01, u8 = ToInt32(out*255)
+ * clamped; rgba[i*4+3] = 255. */
+int pt_tonemap(const float* accum, size_t npix, uint32_t sample_runs, uint8_t* rgba_out);
+
+/* Numerics self-test: out[i] = f(a[i], b[i]) evaluated ON THE DEVICE with the core's
+ * pinned f32 math (fn ids: 0 sin, 1 cos, 2 tan, 3 acos, 4 log2, 5 exp2, 6 pow, 7 sqrt,
+ * 8 div, 9 hash1u, 10 hash1, 11 hash2.x, 12 hash2.y, 13 min, 14 max; hash inputs are the
+ * bit patterns of a[i]). */
+int pt_selftest_math(int device, int fn, const float* a, const float* b, float* out, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_HIP_H */

@@ -1,0 +1,180 @@
+"""GPU parity: the HIP core (through the C ABI) against the CPU oracle on identical inputs.
+
+Bar: bit-exact.  The numeric contract (pt_math.h / oracle/pt_oracle.c header) pins every
+implementation-defined WGSL operation, so per-pixel radiance, accumulators and work counters
+must match the oracle exactly, not within a tolerance.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import pt_amd
+
+pytestmark = pytest.mark.gpu
+
+RNG = np.random.default_rng(1234)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def same_bits(a, b):
+    """Bitwise equality, treating every NaN as equal to every NaN."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    both_nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all((bits(a) == bits(b)) | both_nan))
+
+
+def mismatch_report(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    bad = np.argwhere(~((bits(a) == bits(b)) | (np.isnan(a) & np.isnan(b))))
+    return f"{len(bad)} mismatches; first {bad[:5].tolist()}: gpu {a[tuple(bad[0])] if len(bad) else None} " \
+           f"oracle {b[tuple(bad[0])] if len(bad) else None}"
+
+
+# ---------------------------------------------------------------------------------------------
+# pinned math on device == oracle restatement
+# ---------------------------------------------------------------------------------------------
+def _inputs(fn, n=4096):
+    if fn in ("sin", "cos", "tan"):
+        x = np.concatenate([RNG.uniform(0, 2 * np.pi, n), RNG.uniform(-20, 20, n // 4), [0.0, -0.0, 0.785398, 1e-30]])
+    elif fn == "acos":
+        x = np.concatenate([RNG.uniform(0, 1, n), RNG.uniform(-1, 1, n // 4), [0.0, 0.5, 1.0, -1.0, -0.5]])
+    elif fn == "log2":
+        x = np.concatenate([RNG.uniform(0, 1, n), 10 ** RNG.uniform(-44, 30, n // 4), [1.0, 2.0, 0.0, 1e-45]])
+    elif fn == "exp2":
+        x = np.concatenate([RNG.uniform(-130, 130, n), RNG.uniform(-1, 1, n // 4), [0.0, -127.0, 127.0, -126.5]])
+    else:
+        x = RNG.uniform(0, 1, n)
+    return x.astype(np.float32)
+
+
+@pytest.mark.parametrize("fn", ["sin", "cos", "tan", "acos", "log2", "exp2"])
+def test_math_unary_bitexact(fn):
+    x = _inputs(fn)
+    gpu = pt_amd.selftest_math(fn, x)
+    ref = oracle.math_fn(fn, x)
+    assert same_bits(gpu, ref), mismatch_report(gpu, ref)
+
+
+def test_math_pow_bitexact():
+    x = np.concatenate([RNG.uniform(0, 1, 4096), [0.0, 1.0, 1e-3, 0.999]]).astype(np.float32)
+    y = np.concatenate([RNG.choice([5.0, 10.0, 40.0, 200.0, 1000.0], 4096), [40, 40, 40, 1000]]).astype(np.float32)
+    gpu = pt_amd.selftest_math("pow", x, y)
+    ref = np.array([oracle.lib().po_powf(float(a), float(b)) for a, b in zip(x, y)], np.float32)
+    assert same_bits(gpu, ref), mismatch_report(gpu, ref)
+
+
+def test_math_div_sqrt_correctly_rounded():
+    a = (RNG.standard_normal(8192) * 10 ** RNG.uniform(-30, 30, 8192)).astype(np.float32)
+    b = (RNG.standard_normal(8192) * 10 ** RNG.uniform(-30, 30, 8192)).astype(np.float32)
+    assert same_bits(pt_amd.selftest_math("div", a, b), a / b)
+    s = np.abs(a)
+    assert same_bits(pt_amd.selftest_math("sqrt", s), np.sqrt(s))
+
+
+def test_math_minmax_nan_handling():
+    nan = np.float32(np.nan)
+    a = np.array([nan, 1.0, nan, -0.0, 3.0], np.float32)
+    b = np.array([2.0, nan, nan, 0.0, -3.0], np.float32)
+    mn = pt_amd.selftest_math("min", a, b)
+    mx = pt_amd.selftest_math("max", a, b)
+    assert mn[0] == 2.0 and mn[1] == 1.0 and np.isnan(mn[2]) and mn[4] == -3.0
+    assert mx[0] == 2.0 and mx[1] == 1.0 and np.isnan(mx[2]) and mx[4] == 3.0
+
+
+def test_hash_bitexact():
+    n = np.concatenate([RNG.integers(0, 2**32, 20000, dtype=np.uint64), [0, 1, 2**31 - 1, 2**32 - 1]]).astype(np.uint32)
+    x = n.view(np.float32)
+    g1u = pt_amd.selftest_math("hash1u", x).view(np.uint32)
+    assert np.array_equal(g1u, np.array([oracle.hash1u(int(v)) for v in n], np.uint32))
+    g1 = pt_amd.selftest_math("hash1", x)
+    assert same_bits(g1, np.array([oracle.hash1(int(v)) for v in n], np.float32))
+    g2 = np.stack([pt_amd.selftest_math("hash2x", x), pt_amd.selftest_math("hash2y", x)], 1)
+    assert same_bits(g2, np.array([oracle.hash2(int(v)) for v in n], np.float32))
+
+
+# ---------------------------------------------------------------------------------------------
+# one reference dispatch (pt_frame) == oracle po_frame, per pixel, bit for bit
+# ---------------------------------------------------------------------------------------------
+FRAME_CASES = [
+    # scene, W, H, salts, max_depth
+    ("CornellBox", 48, 40, (0, 1, 977), 16),
+    ("CornellBox", 33, 17, (5,), 8),
+    ("CornellBox-Mirror", 40, 40, (0, 3), 16),
+    ("CornellBox-Glossy", 40, 32, (0, 11), 16),
+    ("CornellBox-Sphere", 40, 32, (0, 2), 16),
+    ("MedievalBoat", 24, 16, (0,), 16),
+]
+
+
+@pytest.mark.parametrize("scene,W,H,salts,depth", FRAME_CASES)
+def test_frame_bitexact(packed, scene, W, H, salts, depth):
+    p = packed[scene]
+    meta = p.meta_for(W, H)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        for t in salts:
+            gpu = s.frame(meta, t, depth)
+            ref, _ = oracle.frame(p.triangle_data, p.bvh_data, meta, t, depth)
+            assert same_bits(gpu, ref), f"{scene} t={t}: " + mismatch_report(gpu, ref)
+
+
+@pytest.mark.parametrize("rr,direct", [(0.9, False), (0.1, False), (0.9, True)])
+def test_frame_settings_bitexact(packed, rr, direct):
+    p = packed["CornellBox"]
+    meta = p.meta_for(40, 40, rr=rr, direct_only=direct)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        gpu = s.frame(meta, 42, 16)
+    ref, _ = oracle.frame(p.triangle_data, p.bvh_data, meta, 42, 16)
+    assert same_bits(gpu, ref), mismatch_report(gpu, ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# accumulation over frames (pt_render) == oracle po_render, and counters
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("scene,W,H,frame0,nframes,stride,depth", [
+    ("CornellBox", 64, 48, 0, 8, 1, 8),
+    ("CornellBox", 32, 32, 3, 5, 4, 16),
+    ("CornellBox-Glossy", 32, 32, 1, 4, 2, 16),
+    ("CornellBox-Sphere", 32, 32, 0, 4, 1, 16),
+])
+def test_render_accum_bitexact(packed, scene, W, H, frame0, nframes, stride, depth):
+    p = packed[scene]
+    meta = p.meta_for(W, H)
+    init = RNG.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        gpu, gc = s.render(meta, frame0, nframes, stride, depth, pt_amd.MODE_MEGAKERNEL, accum=init.copy(), counters=True)
+    ref, rc = oracle.render(p.triangle_data, p.bvh_data, meta, frame0, nframes, stride, depth, acc=init.copy())
+    assert same_bits(gpu, ref), mismatch_report(gpu, ref)
+    assert gc == rc, (gc, rc)
+
+
+def test_scene_info_matches_survey(packed):
+    with pt_amd.Scene(packed["CornellBox"].triangle_data, packed["CornellBox"].bvh_data) as s:
+        info = s.info
+    # 21 nodes / 11 leaves (10 internal), 164 leaf refs, max leaf 20, light = 2 triangles
+    assert info["nodes"] == 10 and info["leaves"] == 11 and info["leaf_refs"] == 164 and info["max_leaf"] == 20
+    assert info["emissive_tris"] == 2 and info["materials"] == 8 and info["vertices"] == 72
+
+
+def test_render_async_torch_stream(packed):
+    torch = pytest.importorskip("torch")
+    p = packed["CornellBox"]
+    meta = p.meta_for(64, 64)
+    acc = torch.zeros((64, 64, 3), dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.render_async(meta, 0, 4, 1, 8, pt_amd.MODE_MEGAKERNEL, acc.data_ptr(), st.cuda_stream)
+        st.synchronize()
+        host = s.render(meta, 0, 4, 1, 8, pt_amd.MODE_MEGAKERNEL)
+    assert same_bits(acc.cpu().numpy(), host)
+
+
+def test_invalid_scene_rejected():
+    tri = np.zeros(32, np.float32)
+    bvh = np.zeros(64, np.float32)
+    with pytest.raises(pt_amd.PtError) as e:
+        pt_amd.Scene(tri, bvh)
+    assert e.value.code == -2
