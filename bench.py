@@ -82,6 +82,7 @@ def main():
     import torch.distributed as dist
 
     import pt_amd
+    from pt_amd.shard import frames_for_rank, reduce_accum
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -96,23 +97,22 @@ def main():
     W, H = int(meta[0]), int(meta[1])
     mode = {"auto": pt_amd.MODE_AUTO, "megakernel": pt_amd.MODE_MEGAKERNEL, "wavefront": pt_amd.MODE_WAVEFRONT}[args.mode]
     scene = pt_amd.Scene(tri, bvh, device=local_rank)
-    # frames of this rank: k = rank, rank + world, ...
-    nframes = len(range(rank, args.spp, world))
+    # frames of this rank: k = rank, rank + world, ... (pt_amd/shard.py)
+    frame0, nframes, fstride = frames_for_rank(rank, world, args.spp)
     stream = torch.cuda.Stream(device=dev)
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
 
     def step():
         with torch.cuda.stream(stream):
             acc.zero_()
-            scene.render_async(meta, rank, nframes, world, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
-            if world > 1:
-                dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+            scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
+            reduce_accum(acc, dist)
 
     # work counters for the roofline's algorithmic bytes (separate pass, not timed)
     cnt = torch.zeros(6, dtype=torch.int64, device=dev)
     with torch.cuda.stream(stream):
         tmp = torch.zeros_like(acc)
-        scene.render_async(meta, rank, nframes, world, args.depth, mode, tmp.data_ptr(), stream.cuda_stream,
+        scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, tmp.data_ptr(), stream.cuda_stream,
                            d_counters_ptr=cnt.data_ptr())
     stream.synchronize()
     c = cnt.cpu().tolist()
@@ -133,10 +133,9 @@ def main():
         with torch.cuda.stream(stream):
             acc.zero_()
             ev0.record(stream)
-            scene.render_async(meta, rank, nframes, world, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
+            scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
             ev1.record(stream)
-            if world > 1:
-                dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+            reduce_accum(acc, dist)
         ev1.synchronize()
         kernel_ms.append(ev0.elapsed_time(ev1))
     stream.synchronize()

@@ -2,6 +2,7 @@
 // Host code only; kernels live in pt_kernels.hip.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -254,6 +255,10 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.f_ntri = (float)L.ntri;
     s->view.inv_ntri = 1.0f / (float)L.ntri;  // intersection-logic.wgsl:284
     s->view.max_stack = (int32_t)L.info.max_stack;
+    s->view.off_tris = (uint32_t)(o_tris - o_nodes);
+    s->view.off_mats = (uint32_t)(o_mats - o_nodes);
+    s->view.off_lights = (uint32_t)(o_lights - o_nodes);
+    s->view.span_bytes = (uint32_t)(o_lights + L.lights.size() * sizeof(Light) - o_nodes);
     s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);
     s->info = L.info;
     s->info.device_bytes = total;
@@ -303,6 +308,17 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
     return PT_OK;
 }
 
+// PT_MODE_* -> kernel.  PT_KERNEL=literal|regen|regen_lds overrides (A/B experiments).
+KernelKind kernel_kind(int mode) {
+    (void)mode;
+    if (const char* e = std::getenv("PT_KERNEL")) {
+        if (!std::strcmp(e, "literal")) return KernelKind::Literal;
+        if (!std::strcmp(e, "regen")) return KernelKind::Regen;
+        if (!std::strcmp(e, "regen_lds")) return KernelKind::RegenLds;
+    }
+    return KernelKind::Auto;
+}
+
 int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframes, uint32_t stride, int max_depth,
                 int mode, bool accum, float* d_out, Counters* d_cnt, hipStream_t stream) {
     FrameParams fp;
@@ -314,7 +330,8 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         return fail(PT_ERR_INVALID, "frame index >= 2^24 (t_k = u32(f32(k)) would round)");
     HIP_TRY(hipSetDevice(s->device));
     if (nframes == 0) return PT_OK;
-    HIP_TRY(launch_mega(s->view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt, stream));
+    HIP_TRY(launch_render(kernel_kind(mode), s->view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
+                          stream));
     return PT_OK;
 }
 

@@ -33,28 +33,25 @@ __device__ __forceinline__ float ray_box(const Ray& r, float mnx, float mny, flo
     return (tmax > fmaxf(tmin, 0.0f)) ? (tmin > 0.0f ? tmin : tmax) : -1.0f;
 }
 
-// ray-triangle-intersection.wgsl:1-42 restricted to what the traversal needs
-// (t); point and normal are rebuilt for the winning record only.
-__device__ __forceinline__ void test_leaf(const Tri* __restrict__ tris, int first, int cnt, const Ray& r, float& best_t,
-                                          int& best) {
+// ray-triangle-intersection.wgsl:1-42 restricted to what the traversal needs (t);
+// point and normal are rebuilt for the winning record only (hit_data).
+__device__ __forceinline__ void test_tri(const Tri* __restrict__ tris, int i, const Ray& r, float& best_t, int& best) {
     const float eps = 1e-8f;
-    for (int i = first; i < first + cnt; ++i) {
-        const float4* tp = reinterpret_cast<const float4*>(tris + i);
-        float4 a = tp[0], b = tp[1], c = tp[2];
-        f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
-        f3 rce2 = cross(r.d, e2);
-        float det = dot(e1, rce2);
-        if (det > -eps && det < eps) continue;
-        float inv_det = 1.0f / det;
-        f3 s = r.o - v0;
-        float u = inv_det * dot(s, rce2);
-        if (u < 0.0f || u > 1.0f) continue;
-        f3 sce1 = cross(s, e1);
-        float v = inv_det * dot(r.d, sce1);
-        if (v < 0.0f || u + v > 1.0f) continue;
-        float t = inv_det * dot(e2, sce1);
-        if (t > eps && (best_t < 0.0f || t < best_t)) { best_t = t; best = i; }
-    }
+    const float4* tp = reinterpret_cast<const float4*>(tris + i);
+    float4 a = tp[0], b = tp[1], c = tp[2];
+    f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
+    f3 rce2 = cross(r.d, e2);
+    float det = dot(e1, rce2);
+    if (det > -eps && det < eps) return;
+    float inv_det = 1.0f / det;
+    f3 s = r.o - v0;
+    float u = inv_det * dot(s, rce2);
+    if (u < 0.0f || u > 1.0f) return;
+    f3 sce1 = cross(s, e1);
+    float v = inv_det * dot(r.d, sce1);
+    if (v < 0.0f || u + v > 1.0f) return;
+    float t = inv_det * dot(e2, sce1);
+    if (t > eps && (best_t < 0.0f || t < best_t)) { best_t = t; best = i; }
 }
 
 // intersection-logic.wgsl:1-215.  The reference keeps -1 markers on a 64-entry
@@ -79,8 +76,11 @@ __device__ __forceinline__ int trace(const SceneView& sc, const Ray& r, float& t
         float rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
         bool li = 0.0f < ld, ri = 0.0f < rd;
         bool lleaf = d.z >= 0, rleaf = d.w >= 0;
-        if (li && lleaf) { test_leaf(sc.tris, d.x, d.z, r, best_t, best); if (COUNT) cnt.tri_tests += d.z; }
-        if (ri && rleaf) { test_leaf(sc.tris, d.y, d.w, r, best_t, best); if (COUNT) cnt.tri_tests += d.w; }
+        // leaf children are tested at once, left leaf first (intersection-logic.wgsl:47-176);
+        // one loop over both ranges keeps lanes with a left-only and a right-only leaf together
+        const int na = (li && lleaf) ? d.z : 0, nb = (ri && rleaf) ? d.w : 0;
+        for (int k = 0; k < na + nb; ++k) test_tri(sc.tris, k < na ? d.x + k : d.y + (k - na), r, best_t, best);
+        if (COUNT) cnt.tri_tests += na + nb;
         bool tl = li && !lleaf && !(best_t > 0.0f && ld > best_t);
         bool tr = ri && !rleaf && !(best_t > 0.0f && rd > best_t);
         if (tl && tr) {

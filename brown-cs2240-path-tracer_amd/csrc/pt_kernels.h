@@ -13,9 +13,17 @@ enum {
 namespace pt {
 
 constexpr int kMegaBlock = 256;
+// dynamic LDS a workgroup may use for traversal stacks + a staged scene copy
+constexpr size_t kLdsSceneBudget = 64 * 1024;
 
-hipError_t launch_mega(const SceneView& sc, const FrameParams& fp, uint32_t frame0, uint32_t nframes, uint32_t stride,
-                       bool accum, bool count, float* out, Counters* cnt, hipStream_t stream);
+enum class KernelKind { Auto, Literal, Regen, RegenLds };
+
+bool scene_fits_lds(const SceneView& sc);
+
+// Render (accum=true: frames frame0 + i*stride, i < nframes, added to out) or one dispatch
+// (accum=false: raw radiance of salt frame0 written to out).
+hipError_t launch_render(KernelKind kind, const SceneView& sc, const FrameParams& fp, uint32_t frame0, uint32_t nframes,
+                         uint32_t stride, bool accum, bool count, float* out, Counters* cnt, hipStream_t stream);
 
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);
 

@@ -67,7 +67,10 @@ struct SceneView {
     float f_ntri;       // f32(Ntri)
     float inv_ntri;     // 1.0 / f32(Ntri)
     int32_t max_stack;  // deepest traversal stack the tree can produce
-    int32_t pad;
+    // byte offsets of each section from `nodes` (one contiguous device allocation), and
+    // the span [nodes, end of lights) staged into LDS by kernels when it fits
+    uint32_t off_tris, off_mats, off_lights, span_bytes;
+    int32_t pad[3];
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

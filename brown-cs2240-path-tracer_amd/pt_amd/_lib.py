@@ -47,11 +47,26 @@ def lib_path() -> str:
     return _LIB_FILE
 
 
+def _bind_torch_hip_runtime():
+    """PyTorch-ROCm ships its own libamdhip64.so (SONAME libamdhip64.so.7, like /opt/rocm's).
+    Loading libpt_hip.so first would pull /opt/rocm's runtime and torch would then load a
+    second HIP/HSA runtime that finds no GPU.  Importing torch first makes libpt_hip.so bind to
+    the runtime already in the process, so device pointers and streams are shared with torch.
+    PT_AMD_NO_TORCH=1 skips this (standalone use on /opt/rocm's runtime)."""
+    if os.environ.get("PT_AMD_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_library():
     """Load libpt_hip.so; raise if it was not built (no silent fallback)."""
     global _lib
     if _lib is not None:
         return _lib
+    _bind_torch_hip_runtime()
     if not os.path.exists(_LIB_FILE):
         raise PtError(-4, f"{_LIB_FILE} not built (run __graft_entry__.build() or make -C csrc)")
     L = ctypes.CDLL(_LIB_FILE)

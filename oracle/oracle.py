@@ -127,5 +127,5 @@ def tonemap(acc, sample_runs: int):
 
 def math_fn(name: str, x):
     """Vectorised access to the pinned f32 transcendentals (po_sinf, po_acosf, ...)."""
-    fn = getattr(lib(), "po_" + name)
+    fn = getattr(lib(), "po_" + name + "f")
     return np.array([fn(float(v)) for v in np.asarray(x, np.float32)], np.float32)

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""A/B the render kernels (PT_KERNEL variants) on one workload, interleaved in one process.
+
+Usage: python scripts/perf_variants.py [--scene CornellBox] [--res 1024] [--spp 64] [--depth 8]
+       [--rounds 3] [--variants literal,regen,regen_lds]
+Prints one JSON line per variant: median/min kernel ms and Msamples/s.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "brown-cs2240-path-tracer_amd")
+sys.path.insert(0, PKG)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="CornellBox")
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="literal,regen,regen_lds")
+    args = ap.parse_args()
+    import torch
+
+    import pt_amd
+
+    H = args.height or args.res
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.run(["node", os.path.join(PKG, "node", "bin", "pt-pack.js"),
+                        os.path.join(ROOT, "scenes", "scene_assets", args.scene + ".xml"), td, "--width",
+                        str(args.res), "--height", str(H)], check=True)
+        tri = np.fromfile(os.path.join(td, "triangle_data.f32"), np.float32)
+        bvh = np.fromfile(os.path.join(td, "bvh_data.f32"), np.float32)
+        meta = np.fromfile(os.path.join(td, "meta.f32"), np.float32)
+    W, H = int(meta[0]), int(meta[1])
+    scene = pt_amd.Scene(tri, bvh)
+    st = torch.cuda.Stream()
+    acc = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    variants = args.variants.split(",")
+    times = {v: [] for v in variants}
+    ref = None
+    for r in range(args.rounds + 1):
+        for v in variants:
+            os.environ["PT_KERNEL"] = v
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(st):
+                acc.zero_()
+                e0.record(st)
+                scene.render_async(meta, 0, args.spp, 1, args.depth, 0, acc.data_ptr(), st.cuda_stream)
+                e1.record(st)
+            e1.synchronize()
+            if r > 0:
+                times[v].append(e0.elapsed_time(e1))
+            out = acc.cpu().numpy()
+            if ref is None:
+                ref = out.copy()
+            elif not np.array_equal(out.view(np.uint32), ref.view(np.uint32)):
+                print(json.dumps({"variant": v, "error": "result differs from first variant"}), flush=True)
+    n = W * H * args.spp
+    for v in variants:
+        t = np.array(times[v])
+        print(json.dumps({"scene": args.scene, "res": [W, H], "spp": args.spp, "depth": args.depth, "variant": v,
+                          "ms_median": round(float(np.median(t)), 3), "ms_min": round(float(t.min()), 3),
+                          "msamples_s": round(n / (np.median(t) * 1e-3) / 1e6, 1)}), flush=True)
+    scene.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -13,6 +13,17 @@ import pt_amd
 pytestmark = pytest.mark.gpu
 
 RNG = np.random.default_rng(1234)
+KERNELS = ["auto", "literal", "regen", "regen_lds"]
+
+
+@pytest.fixture(params=KERNELS)
+def kernel(request, monkeypatch):
+    """Every kernel variant must give the same bits (PT_KERNEL is read by the C ABI per call)."""
+    if request.param == "auto":
+        monkeypatch.delenv("PT_KERNEL", raising=False)
+    else:
+        monkeypatch.setenv("PT_KERNEL", request.param)
+    return request.param
 
 
 def bits(a):
@@ -111,18 +122,18 @@ FRAME_CASES = [
 
 
 @pytest.mark.parametrize("scene,W,H,salts,depth", FRAME_CASES)
-def test_frame_bitexact(packed, scene, W, H, salts, depth):
+def test_frame_bitexact(packed, kernel, scene, W, H, salts, depth):
     p = packed[scene]
     meta = p.meta_for(W, H)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         for t in salts:
             gpu = s.frame(meta, t, depth)
             ref, _ = oracle.frame(p.triangle_data, p.bvh_data, meta, t, depth)
-            assert same_bits(gpu, ref), f"{scene} t={t}: " + mismatch_report(gpu, ref)
+            assert same_bits(gpu, ref), f"{scene} t={t} kernel={kernel}: " + mismatch_report(gpu, ref)
 
 
 @pytest.mark.parametrize("rr,direct", [(0.9, False), (0.1, False), (0.9, True)])
-def test_frame_settings_bitexact(packed, rr, direct):
+def test_frame_settings_bitexact(packed, kernel, rr, direct):
     p = packed["CornellBox"]
     meta = p.meta_for(40, 40, rr=rr, direct_only=direct)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
@@ -140,7 +151,7 @@ def test_frame_settings_bitexact(packed, rr, direct):
     ("CornellBox-Glossy", 32, 32, 1, 4, 2, 16),
     ("CornellBox-Sphere", 32, 32, 0, 4, 1, 16),
 ])
-def test_render_accum_bitexact(packed, scene, W, H, frame0, nframes, stride, depth):
+def test_render_accum_bitexact(packed, kernel, scene, W, H, frame0, nframes, stride, depth):
     p = packed[scene]
     meta = p.meta_for(W, H)
     init = RNG.uniform(0, 1, (H, W, 3)).astype(np.float32)
