@@ -3,6 +3,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -197,6 +198,8 @@ struct pt_scene {
     float* d_accum = nullptr;  // scratch for the blocking host-buffer calls
     size_t accum_cap = 0;
     Counters* d_counters = nullptr;
+    void* d_wf = nullptr;  // wavefront path state, allocated on first use
+    WfBuffers wf{};
 };
 
 extern "C" {
@@ -271,6 +274,7 @@ void pt_scene_destroy(pt_scene* s) {
     hipSetDevice(s->device);
     if (s->stream) { hipStreamSynchronize(s->stream); hipStreamDestroy(s->stream); }
     if (s->d_accum) hipFree(s->d_accum);
+    if (s->d_wf) hipFree(s->d_wf);
     if (s->d_mem) hipFree(s->d_mem);
     delete s;
 }
@@ -308,15 +312,47 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
     return PT_OK;
 }
 
-// PT_MODE_* -> kernel.  PT_KERNEL=literal|regen|regen_lds overrides (A/B experiments).
-KernelKind kernel_kind(int mode) {
-    (void)mode;
+// PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
+// PT_TRAV=nested|flat.
+LaunchOpts launch_opts(int mode) {
+    LaunchOpts lo;
+    lo.wavefront = mode == PT_MODE_WAVEFRONT;
     if (const char* e = std::getenv("PT_KERNEL")) {
-        if (!std::strcmp(e, "literal")) return KernelKind::Literal;
-        if (!std::strcmp(e, "regen")) return KernelKind::Regen;
-        if (!std::strcmp(e, "regen_lds")) return KernelKind::RegenLds;
+        lo.literal = !std::strcmp(e, "literal");
+        if (!std::strcmp(e, "wavefront")) lo.wavefront = true;
+        if (!std::strcmp(e, "mega") || lo.literal) lo.wavefront = false;
     }
-    return KernelKind::Auto;
+    if (const char* e = std::getenv("PT_LDS")) lo.lds = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("PT_TRAV")) lo.flat = std::strcmp(e, "nested") != 0;
+    return lo;
+}
+
+// paths in flight per wavefront batch (~1.1 GB of SoA state at kWfBytesPerPath)
+constexpr uint64_t kWfTargetPaths = 8ull << 20;
+
+int ensure_wavefront(pt_scene* s, uint64_t paths) {
+    if (s->d_wf && s->wf.capacity >= paths) return PT_OK;
+    if (paths > 0x7fffffffull) return fail(PT_ERR_INVALID, "image too large for one wavefront batch");
+    if (s->d_wf) { hipStreamSynchronize(s->stream); hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; }
+    const size_t n = paths;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
+    const size_t o_r0 = take(16 * n), o_r1 = take(16 * n), o_hit = take(8 * n), o_s0 = take(16 * n), o_s1 = take(16 * n),
+                 o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(16 * n), o_rad = take(12 * n), o_q0 = take(4 * n),
+                 o_q1 = take(4 * n), o_ctl = take(4 * WF_CTL_WORDS);
+    if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
+    char* b = static_cast<char*>(s->d_wf);
+    WfBuffers& w = s->wf;
+    w.ray0 = reinterpret_cast<float4*>(b + o_r0); w.ray1 = reinterpret_cast<float4*>(b + o_r1);
+    w.hit = reinterpret_cast<int2*>(b + o_hit);
+    w.st0 = reinterpret_cast<float4*>(b + o_s0); w.st1 = reinterpret_cast<float4*>(b + o_s1);
+    w.sp0 = reinterpret_cast<float4*>(b + o_p0); w.sp1 = reinterpret_cast<float4*>(b + o_p1);
+    w.sp2 = reinterpret_cast<float4*>(b + o_p2);
+    w.rad = reinterpret_cast<float*>(b + o_rad);
+    w.q0 = reinterpret_cast<uint32_t*>(b + o_q0); w.q1 = reinterpret_cast<uint32_t*>(b + o_q1);
+    w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
+    w.capacity = (uint32_t)n;
+    return PT_OK;
 }
 
 int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframes, uint32_t stride, int max_depth,
@@ -330,8 +366,17 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         return fail(PT_ERR_INVALID, "frame index >= 2^24 (t_k = u32(f32(k)) would round)");
     HIP_TRY(hipSetDevice(s->device));
     if (nframes == 0) return PT_OK;
-    HIP_TRY(launch_render(kernel_kind(mode), s->view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
-                          stream));
+    const LaunchOpts lo = launch_opts(mode);
+    if (lo.wavefront) {
+        const uint64_t npix = (uint64_t)fp.width * fp.height;
+        const uint64_t want = std::max<uint64_t>(npix, std::min<uint64_t>(npix * (accum ? nframes : 1), kWfTargetPaths));
+        int rc2 = ensure_wavefront(s, want);
+        if (rc2 != PT_OK) return rc2;
+        HIP_TRY(launch_wavefront(lo, s->view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
+                                 stream));
+        return PT_OK;
+    }
+    HIP_TRY(launch_megakernel(lo, s->view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt, stream));
     return PT_OK;
 }
 
@@ -378,7 +423,7 @@ int pt_render(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nfram
 
 int pt_frame_async(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float* d_radiance, void* stream) {
     if (!s || !d_radiance) return fail(PT_ERR_INVALID, "null argument");
-    return render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_MEGAKERNEL, false, d_radiance, nullptr,
+    return render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_AUTO, false, d_radiance, nullptr,
                        static_cast<hipStream_t>(stream));
 }
 
@@ -390,7 +435,7 @@ int pt_frame(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float
     const size_t n = (size_t)fp.width * fp.height * 3;
     HIP_TRY(hipSetDevice(s->device));
     if ((rc = ensure_accum(s, n)) != PT_OK) return rc;
-    rc = render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_MEGAKERNEL, false, s->d_accum, nullptr, s->stream);
+    rc = render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_AUTO, false, s->d_accum, nullptr, s->stream);
     if (rc != PT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(radiance, s->d_accum, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));

@@ -16,14 +16,44 @@ constexpr int kMegaBlock = 256;
 // dynamic LDS a workgroup may use for traversal stacks + a staged scene copy
 constexpr size_t kLdsSceneBudget = 64 * 1024;
 
-enum class KernelKind { Auto, Literal, Regen, RegenLds };
+// Kernel selection (PT_KERNEL / PT_LDS / PT_TRAV environment overrides for A/B runs).
+struct LaunchOpts {
+    bool wavefront = false;  // wavefront pipeline (pt_wavefront.hip)
+    bool literal = false;  // k_mega: the reference's control flow
+    bool lds = true;       // stage the scene in LDS when it fits
+    bool flat = true;      // flattened wave-scheduled traversal (trav_step) vs nested loops
+};
 
 bool scene_fits_lds(const SceneView& sc);
 
-// Render (accum=true: frames frame0 + i*stride, i < nframes, added to out) or one dispatch
-// (accum=false: raw radiance of salt frame0 written to out).
-hipError_t launch_render(KernelKind kind, const SceneView& sc, const FrameParams& fp, uint32_t frame0, uint32_t nframes,
-                         uint32_t stride, bool accum, bool count, float* out, Counters* cnt, hipStream_t stream);
+// Wavefront path state (SoA, HBM), `capacity` paths; see pt_wavefront.hip.
+enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_HEAD = 2, WF_CTL_WORDS = 64 };
+struct WfBuffers {
+    float4* ray0;  // (o.xyz, d.x)
+    float4* ray1;  // (d.y, d.z, -, -)
+    int2* hit;     // (record, t bits)
+    float4* st0;   // (L.xyz, beta.x)
+    float4* st1;   // (beta.y, beta.z, seed bits, depth | spec << 16)
+    float4* sp0;   // (shading point, material id)
+    float4* sp1;   // (normal, -)
+    float4* sp2;   // (incoming direction, -)
+    float* rad;    // [capacity][3] radiance of finished paths
+    uint32_t* q0;  // path queues (ping-pong)
+    uint32_t* q1;
+    uint32_t* ctl; // queue counts + trace head
+    uint32_t capacity;
+};
+constexpr size_t kWfBytesPerPath = 16 * 7 + 8 + 12 + 4 * 2;
+
+hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
+                            uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
+                            Counters* cnt, hipStream_t stream);
+
+// Megakernel render (accum=true: frames frame0 + i*stride, i < nframes, added to out) or one
+// dispatch (accum=false: raw radiance of salt frame0 written to out).
+hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
+                             uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
+                             hipStream_t stream);
 
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);
 

@@ -19,6 +19,23 @@ PKG = os.path.join(ROOT, "brown-cs2240-path-tracer_amd")
 sys.path.insert(0, PKG)
 
 
+VARIANTS = {
+    "auto": {},
+    "literal": {"PT_KERNEL": "literal"},
+    "mega_nested": {"PT_KERNEL": "mega", "PT_TRAV": "nested"},
+    "mega_flat_global": {"PT_KERNEL": "mega", "PT_LDS": "0"},
+    "mega_flat_lds": {"PT_KERNEL": "mega"},
+    "wavefront_global": {"PT_KERNEL": "wavefront", "PT_LDS": "0"},
+    "wavefront_lds": {"PT_KERNEL": "wavefront"},
+}
+
+
+def set_variant(v):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+        os.environ.pop(k, None)
+    os.environ.update(VARIANTS[v])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="CornellBox")
@@ -27,7 +44,7 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="literal,regen,regen_lds")
+    ap.add_argument("--variants", default="mega_flat_lds,wavefront_lds")
     args = ap.parse_args()
     import torch
 
@@ -50,7 +67,7 @@ def main():
     ref = None
     for r in range(args.rounds + 1):
         for v in variants:
-            os.environ["PT_KERNEL"] = v
+            set_variant(v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             with torch.cuda.stream(st):
                 acc.zero_()

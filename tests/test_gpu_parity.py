@@ -13,16 +13,25 @@ import pt_amd
 pytestmark = pytest.mark.gpu
 
 RNG = np.random.default_rng(1234)
-KERNELS = ["auto", "literal", "regen", "regen_lds"]
+# kernel variants (environment read by the C ABI on every call)
+KERNELS = {
+    "auto": {},
+    "literal": {"PT_KERNEL": "literal"},
+    "mega_nested": {"PT_KERNEL": "mega", "PT_TRAV": "nested"},
+    "mega_flat_global": {"PT_KERNEL": "mega", "PT_LDS": "0"},
+    "mega_flat_lds": {"PT_KERNEL": "mega"},
+    "wavefront_global": {"PT_KERNEL": "wavefront", "PT_LDS": "0"},
+    "wavefront_lds": {"PT_KERNEL": "wavefront"},
+}
 
 
-@pytest.fixture(params=KERNELS)
+@pytest.fixture(params=list(KERNELS))
 def kernel(request, monkeypatch):
-    """Every kernel variant must give the same bits (PT_KERNEL is read by the C ABI per call)."""
-    if request.param == "auto":
-        monkeypatch.delenv("PT_KERNEL", raising=False)
-    else:
-        monkeypatch.setenv("PT_KERNEL", request.param)
+    """Every kernel variant must give the same bits."""
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in KERNELS[request.param].items():
+        monkeypatch.setenv(k, v)
     return request.param
 
 
