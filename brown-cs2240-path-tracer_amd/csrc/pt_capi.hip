@@ -337,19 +337,18 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     const size_t n = paths;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
-    const size_t o_r0 = take(16 * n), o_r1 = take(16 * n), o_hit = take(8 * n), o_s0 = take(16 * n), o_s1 = take(16 * n),
-                 o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(16 * n), o_rad = take(12 * n), o_q0 = take(4 * n),
-                 o_q1 = take(4 * n), o_ctl = take(4 * WF_CTL_WORDS);
+    const size_t o_q0 = take(32 * n), o_q1 = take(32 * n), o_hit = take(8 * n), o_s0 = take(16 * n),
+                 o_s1 = take(16 * n), o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(16 * n), o_rad = take(12 * n),
+                 o_ctl = take(4 * WF_CTL_WORDS);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
     char* b = static_cast<char*>(s->d_wf);
     WfBuffers& w = s->wf;
-    w.ray0 = reinterpret_cast<float4*>(b + o_r0); w.ray1 = reinterpret_cast<float4*>(b + o_r1);
-    w.hit = reinterpret_cast<int2*>(b + o_hit);
+    w.rq0 = reinterpret_cast<float4*>(b + o_q0); w.rq1 = reinterpret_cast<float4*>(b + o_q1);
+    w.hitq = reinterpret_cast<int2*>(b + o_hit);
     w.st0 = reinterpret_cast<float4*>(b + o_s0); w.st1 = reinterpret_cast<float4*>(b + o_s1);
     w.sp0 = reinterpret_cast<float4*>(b + o_p0); w.sp1 = reinterpret_cast<float4*>(b + o_p1);
     w.sp2 = reinterpret_cast<float4*>(b + o_p2);
     w.rad = reinterpret_cast<float*>(b + o_rad);
-    w.q0 = reinterpret_cast<uint32_t*>(b + o_q0); w.q1 = reinterpret_cast<uint32_t*>(b + o_q1);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
     w.capacity = (uint32_t)n;
     return PT_OK;

@@ -27,23 +27,23 @@ struct LaunchOpts {
 bool scene_fits_lds(const SceneView& sc);
 
 // Wavefront path state (SoA, HBM), `capacity` paths; see pt_wavefront.hip.
-enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_HEAD = 2, WF_CTL_WORDS = 64 };
+enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_CTL_WORDS = 64 };
 struct WfBuffers {
-    float4* ray0;  // (o.xyz, d.x)
-    float4* ray1;  // (d.y, d.z, -, -)
-    int2* hit;     // (record, t bits)
-    float4* st0;   // (L.xyz, beta.x)
-    float4* st1;   // (beta.y, beta.z, seed bits, depth | spec << 16)
-    float4* sp0;   // (shading point, material id)
-    float4* sp1;   // (normal, -)
-    float4* sp2;   // (incoming direction, -)
-    float* rad;    // [capacity][3] radiance of finished paths
-    uint32_t* q0;  // path queues (ping-pong)
-    uint32_t* q1;
-    uint32_t* ctl; // queue counts + trace head
+    // ray queues (dense, compacted each iteration; ping-pong): entry i = 2 float4
+    // (o.xyz, d.x), (d.y, d.z, path index bits, 0)
+    float4* rq0;
+    float4* rq1;
+    int2* hitq;    // per queue entry: (leaf record, t bits)
+    float4* st0;   // per path: (L.xyz, beta.x)
+    float4* st1;   // per path: (beta.y, beta.z, seed bits, depth | spec << 16)
+    float4* sp0;   // per path: (shading point, material id)
+    float4* sp1;   // per path: (normal, -)
+    float4* sp2;   // per path: (incoming direction, -)
+    float* rad;    // per path: radiance when it ended [capacity][3]
+    uint32_t* ctl; // queue counts
     uint32_t capacity;
 };
-constexpr size_t kWfBytesPerPath = 16 * 7 + 8 + 12 + 4 * 2;
+constexpr size_t kWfBytesPerPath = 32 * 2 + 8 + 16 * 5 + 12;
 
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

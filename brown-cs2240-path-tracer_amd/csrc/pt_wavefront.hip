@@ -1,19 +1,21 @@
 // pt_wavefront.hip — wavefront path tracer for gfx950 (the north-star design).
 //
-// A batch of P = F*W*H paths (F frames of the image) lives in HBM as SoA float4 arrays.
-// Each iteration runs two kernels over the queue of live paths:
-//   k_wf_trace   persistent waves with dynamic ray fetch: a wave pulls 16..64 path indices
-//                at a time from the queue with ONE atomic (wave-aggregated), walks every
-//                lane's ray through the BVH with the flattened, ballot-scheduled traversal
-//                (trav_step, per-lane stack in LDS, scene in LDS when it fits) and refills
-//                lanes as their rays finish, so no lane idles behind a long traversal;
+// A batch of P = F*W*H paths (F frames of the image) lives in HBM as SoA float4 arrays
+// indexed by path; the rays still to be traced live in a DENSE queue (32 B per ray, the
+// path index in the record) that is compacted every iteration.  Each iteration runs:
+//   k_wf_trace   closest-hit traversal of the queue.  Persistent waves, each owning a
+//                contiguous chunk of the queue (no atomics); every lane keeps one ray in
+//                flight and one prefetched, and swaps in the next ray the moment its
+//                traversal ends, so lanes never idle behind a long traversal and a refill
+//                never waits on memory.  Traversal is the flattened, ballot-scheduled
+//                trav_step (per-lane stack in LDS, scene in LDS when it fits).
 //   k_wf_shade   the path logic after that traversal (path_after_ext / path_after_shadow,
-//                pt_path.h) and compaction of the survivors into the next queue with
+//                pt_path.h) and compaction of the surviving rays into the next queue with
 //                __ballot + mbcnt (one atomicAdd per wave).
-// All paths of a batch start together, so every queue holds only extension rays or only
-// shadow rays and the two alternate.  k_wf_generate creates the camera paths; k_wf_accum
-// adds the finished radiance of the batch into the accumulator in frame order, which keeps
-// the result bit-identical to the reference's host accumulation.
+// All paths of a batch start together, so a queue holds only extension rays or only
+// shadow rays and the two alternate.  k_wf_generate writes the camera rays; k_wf_accum adds
+// the batch's finished radiance into the accumulator in frame order, which keeps the result
+// bit-identical to the reference's host accumulation.
 #include "pt_kernels.h"
 #include "pt_path.h"
 
@@ -28,16 +30,16 @@ __device__ __forceinline__ uint32_t rank_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ void store_ray(const WfBuffers& wb, uint32_t p, const Ray& r) {
-    wb.ray0[p] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    wb.ray1[p] = make_float4(r.d.y, r.d.z, 0.0f, 0.0f);
+__device__ __forceinline__ void store_ray(float4* q, uint32_t i, const Ray& r, uint32_t p) {
+    q[2 * (size_t)i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    q[2 * (size_t)i + 1] = make_float4(r.d.y, r.d.z, __builtin_bit_cast(float, p), 0.0f);
 }
-__device__ __forceinline__ Ray load_ray(const WfBuffers& wb, uint32_t p) {
-    float4 a = wb.ray0[p], b = wb.ray1[p];
+__device__ __forceinline__ Ray unpack_ray(float4 a, float4 b, uint32_t& p) {
     Ray r;
     r.o = mk(a.x, a.y, a.z);
     r.d = mk(a.w, b.x, b.y);
     r.inv = rcp3(r.d);
+    p = __builtin_bit_cast(uint32_t, b.z);
     return r;
 }
 __device__ __forceinline__ void store_state(const WfBuffers& wb, uint32_t p, const PathState& ps) {
@@ -82,7 +84,6 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
     if (p == 0) {
         wb.ctl[WF_COUNT0] = P;
         wb.ctl[WF_COUNT1] = 0;
-        wb.ctl[WF_HEAD] = 0;
     }
     Counters c = {};
     if (p < P) {
@@ -91,9 +92,8 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
         const uint32_t t = raw_salt ? frame0 : (uint32_t)(float)(frame0 + (fbase + f) * stride);
         PathState ps;
         Ray r = path_begin(fp, x, y, t, ps);
-        store_ray(wb, p, r);
+        store_ray(wb.rq0, p, r, p);
         store_state(wb, p, ps);
-        wb.q0[p] = p;
         if (COUNT) { c.samples++; c.ext_queries++; }
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -104,41 +104,56 @@ __global__ __launch_bounds__(256) void k_wf_trace(SceneView sc, WfBuffers wb, in
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
+    const uint32_t count = wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64), w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t per = (count + nwaves - 1) / nwaves;
+    const uint32_t begin = min(w * per, count), end = min(begin + per, count);
     if (LDS) stage_scene_lds(sc, smem + (uint32_t)sc.max_stack * blockDim.x * 4u);
-    const uint32_t* queue = in_q ? wb.q1 : wb.q0;
-    const uint32_t count = __hip_atomic_load(&wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (begin >= end) return;  // wave-uniform
+    const float4* q = in_q ? wb.rq1 : wb.rq0;
+    const uint32_t lane = lane_id();
     Counters c = {};
-    bool has = false, drained = count == 0;
-    uint32_t p = 0;
+    // current ray
+    uint32_t cur = begin;
+    uint32_t idx = cur + lane, p = 0;
+    bool has = idx < end;
     Ray r;
     r.o = r.d = r.inv = mk(0.0f, 0.0f, 0.0f);
+    if (has) r = unpack_ray(q[2 * (size_t)idx], q[2 * (size_t)idx + 1], p);
+    cur = min(cur + 64, end);
     TravState s;
-    trav_init(s, false);
+    trav_init(s, has);
+    // prefetched ray (loads stay in flight until the lane swaps it in)
+    uint32_t pidx = cur + lane;
+    bool pf = pidx < end;
+    float4 pa = make_float4(0, 0, 0, 0), pb = pa;
+    if (pf) { pa = q[2 * (size_t)pidx]; pb = q[2 * (size_t)pidx + 1]; }
+    cur = min(cur + 64, end);
     while (true) {
-        const uint64_t empty = __ballot(!has);
-        const uint32_t n_empty = (uint32_t)__popcll(empty);
-        if (!drained && (n_empty >= 16 || n_empty == 64)) {
-            uint32_t base = 0;
-            if (lane_id() == 0) base = atomicAdd(&wb.ctl[WF_HEAD], n_empty);
-            base = __shfl(base, 0, 64);
-            if (base + n_empty >= count) drained = true;
-            if (!has) {
-                const uint32_t idx = base + rank_below(empty);
-                if (idx < count) {
-                    p = queue[idx];
-                    r = load_ray(wb, p);
-                    trav_init(s, true);
-                    has = true;
-                }
-            }
-        }
-        if (!trav_step<COUNT>(sc, r, s, stack, blockDim.x, c)) {
-            if (drained) break;
-            continue;
-        }
+        if (!trav_step<COUNT>(sc, r, s, stack, blockDim.x, c) && !__any(pf)) break;
         if (has && s.done) {
-            wb.hit[p] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
+            wb.hitq[idx] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;
+        }
+        if (!has && pf) {  // swap in the prefetched ray
+            r = unpack_ray(pa, pb, p);
+            idx = pidx;
+            trav_init(s, true);
+            has = true;
+            pf = false;
+        }
+        if (cur < end) {  // refill the prefetch slots that were consumed
+            const uint64_t need = __ballot(!pf);
+            if (need) {
+                const uint32_t j = cur + rank_below(need);
+                if (!pf && j < end) {
+                    pidx = j;
+                    pa = q[2 * (size_t)j];
+                    pb = q[2 * (size_t)j + 1];
+                    pf = true;
+                }
+                cur = min(cur + (uint32_t)__popcll(need), end);
+            }
         }
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -147,51 +162,47 @@ __global__ __launch_bounds__(256) void k_wf_trace(SceneView sc, WfBuffers wb, in
 template <bool EXT, bool COUNT>
 __global__ __launch_bounds__(256) void k_wf_shade(SceneView sc, FrameParams fp, WfBuffers wb, int in_q,
                                                   Counters* cnt_out) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[WF_HEAD] = 0;  // for the next trace
-    const uint32_t* queue = in_q ? wb.q1 : wb.q0;
-    uint32_t* out_q = in_q ? wb.q0 : wb.q1;
-    uint32_t* out_count = &wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1];
     const uint32_t count = wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
-    const uint32_t waves = gridDim.x * (blockDim.x / 64), wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x * blockDim.x >= count) return;  // whole block past the queue
+    const float4* q = in_q ? wb.rq1 : wb.rq0;
+    float4* out_q = in_q ? wb.rq0 : wb.rq1;
+    uint32_t* out_count = &wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1];
     Counters c = {};
-    for (uint32_t chunk = wave; chunk * 64 < count; chunk += waves) {
-        const uint32_t i = chunk * 64 + lane_id();
-        bool more = false;
-        uint32_t p = 0;
-        if (i < count) {
-            p = queue[i];
-            PathState ps;
-            load_state(wb, p, ps);
-            Ray r = load_ray(wb, p);
-            const int2 h = wb.hit[p];
-            const float t = __builtin_bit_cast(float, h.y);
-            if (EXT) {
-                more = path_after_ext(sc, h.x, t, r, ps);
-                if (more) {
-                    store_shading_point(wb, p, ps);
-                    if (COUNT) c.shadow_queries++;
-                }
-            } else {
-                load_shading_point(wb, p, ps);
-                more = path_after_shadow(sc, fp, h.x, t, r, ps);
-                if (more && COUNT) c.ext_queries++;
-            }
+    bool more = false;
+    uint32_t p = 0;
+    Ray r;
+    if (i < count) {
+        r = unpack_ray(q[2 * (size_t)i], q[2 * (size_t)i + 1], p);
+        const int2 h = wb.hitq[i];
+        const float t = __builtin_bit_cast(float, h.y);
+        PathState ps;
+        load_state(wb, p, ps);
+        if (EXT) {
+            more = path_after_ext(sc, h.x, t, r, ps);
             if (more) {
-                store_ray(wb, p, r);
-                store_state(wb, p, ps);
-            } else {
-                float* o = wb.rad + 3 * (size_t)p;
-                o[0] = ps.L.x; o[1] = ps.L.y; o[2] = ps.L.z;
+                store_shading_point(wb, p, ps);
+                if (COUNT) c.shadow_queries++;
             }
+        } else {
+            load_shading_point(wb, p, ps);
+            more = path_after_shadow(sc, fp, h.x, t, r, ps);
+            if (more && COUNT) c.ext_queries++;
         }
-        // compaction of the survivors: one atomic per wave, lane offsets from mbcnt
-        const uint64_t keep = __ballot(more);
-        if (keep) {
-            uint32_t base = 0;
-            if (lane_id() == 0) base = atomicAdd(out_count, (uint32_t)__popcll(keep));
-            base = __shfl(base, 0, 64);
-            if (more) out_q[base + rank_below(keep)] = p;
+        store_state(wb, p, ps);
+        if (!more) {
+            float* o = wb.rad + 3 * (size_t)p;
+            o[0] = ps.L.x; o[1] = ps.L.y; o[2] = ps.L.z;
         }
+    }
+    // compaction of the surviving rays: one atomic per wave, lane offsets from mbcnt
+    const uint64_t keep = __ballot(more);
+    if (keep) {
+        uint32_t base = 0;
+        const uint32_t leader = (uint32_t)__builtin_ctzll(keep);
+        if (lane_id() == leader) base = atomicAdd(out_count, (uint32_t)__popcll(keep));
+        base = __shfl(base, (int)leader, 64);
+        if (more) store_ray(out_q, base + rank_below(keep), r, p);
     }
     if (COUNT) flush_counters(c, cnt_out);
 }
@@ -238,14 +249,11 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     const uint32_t F = std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
     const size_t lds = (size_t)sc.max_stack * 256 * 4 + (LDS ? sc.span_bytes : 0);
     const int tblocks = trace_blocks<LDS, COUNT>(lds);
-    int dev = 0, cus = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int sblocks = cus * 8;
     const int iters = 2 * (fp.max_depth + 1);
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         const uint32_t P = Fb * npix;
+        const int sblocks = (int)((P + 255) / 256);
         hipLaunchKernelGGL((k_wf_generate<COUNT>), dim3((P + 255) / 256), dim3(256), 0, stream, fp, wb, frame0, stride, fb,
                            P, !accum, cnt);
         int in_q = 0;
