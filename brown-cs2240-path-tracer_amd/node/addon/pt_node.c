@@ -269,14 +269,14 @@ static napi_value js_tonemap(napi_env env, napi_callback_info info) {
 
 static napi_value init(napi_env env, napi_value exports) {
     napi_property_descriptor props[] = {
-        {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_default, NULL},
-        {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_default, NULL},
-        {"sceneCreate", NULL, js_scene_create, NULL, NULL, NULL, napi_default, NULL},
-        {"sceneInfo", NULL, js_scene_info, NULL, NULL, NULL, napi_default, NULL},
-        {"render", NULL, js_render, NULL, NULL, NULL, napi_default, NULL},
-        {"renderSync", NULL, js_render_sync, NULL, NULL, NULL, napi_default, NULL},
-        {"frame", NULL, js_frame, NULL, NULL, NULL, napi_default, NULL},
-        {"tonemap", NULL, js_tonemap, NULL, NULL, NULL, napi_default, NULL},
+        {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"sceneCreate", NULL, js_scene_create, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"sceneInfo", NULL, js_scene_info, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"render", NULL, js_render, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"renderSync", NULL, js_render_sync, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"frame", NULL, js_frame, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"tonemap", NULL, js_tonemap, NULL, NULL, NULL, napi_enumerable, NULL},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

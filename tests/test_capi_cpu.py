@@ -1,0 +1,74 @@
+"""C ABI checks that need no GPU: the library loads, exports every symbol include/pt_hip.h
+declares, reports errors the documented way, and its host-side tone map matches the oracle."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import pt_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pt_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pt_[a-z_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for f in ("pt_scene_create", "pt_scene_destroy", "pt_render", "pt_render_async", "pt_frame", "pt_tonemap",
+              "pt_last_error"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(pt_amd.lib_path())
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", pt_amd.lib_path()], capture_output=True, text=True).stdout
+    for f in declared_functions():
+        assert re.search(rf"\bT {f}\b", out), f
+
+
+def test_kernels_built_for_gfx950():
+    """The fat binary embedded in libpt_hip.so carries gfx950 code objects only."""
+    data = open(pt_amd.lib_path(), "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data
+    assert b"gfx942" not in data and b"gfx90a" not in data
+
+
+def test_abi_version():
+    assert pt_amd.abi_version() == 1
+
+
+def test_errors_without_gpu():
+    if pt_amd.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(pt_amd.PtError) as e:
+        pt_amd.Scene(np.zeros(64, np.float32), np.zeros(64, np.float32))
+    assert e.value.code == -5  # PT_ERR_NODEVICE
+    assert "device" in str(e.value)
+
+
+def test_invalid_arguments():
+    lib = pt_amd.load_library()
+    assert lib.pt_scene_create(None, 0, None, 0, 0, None) == -1
+    assert b"null" in lib.pt_last_error()
+    assert lib.pt_tonemap(None, 0, 1, None) == -1
+
+
+def test_tonemap_matches_oracle():
+    rng = np.random.default_rng(5)
+    acc = (rng.exponential(2.0, (37, 41, 3)) * rng.integers(1, 64)).astype(np.float32)
+    acc[0, 0] = [np.nan, -1.0, 1e12]
+    for runs in (1, 7, 50):
+        got = pt_amd.tonemap(acc, runs).reshape(-1)
+        want = oracle.tonemap(acc, runs)
+        assert np.array_equal(got, want)

@@ -79,8 +79,12 @@ def test_ray_bbox_quirks():
     # miss and behind
     assert oracle.ray_bbox([5, 5, 5], [1, 0, 0], [-1, -1, -1], [1, 1, 1]) == -1.0
     assert oracle.ray_bbox([0, 0, 5], [0, 0, 1], [-1, -1, -1], [1, 1, 1]) == -1.0
-    # axis-parallel ray (d_inv = inf) on a slab plane: 0*inf = NaN handled by minNum/maxNum
-    assert oracle.ray_bbox([1, 0, -5], [0, 0, 1], [-1, -1, -1], [1, 1, 1]) == pytest.approx(4.0)
+    # axis-parallel ray (d_inv = +inf) lying ON a slab plane: (max - p) * inf = 0 * inf = NaN;
+    # minNum/maxNum drop the NaN, the other slab bound is +-inf, so tmax = -inf and the box is
+    # MISSED on both planes (Tavian's form treats the boundary as outside)
+    assert oracle.ray_bbox([1, 0, -5], [0, 0, 1], [-1, -1, -1], [1, 1, 1]) == -1.0
+    assert oracle.ray_bbox([-1, 0, -5], [0, 0, 1], [-1, -1, -1], [1, 1, 1]) == -1.0
+    assert oracle.ray_bbox([0.5, 0, -5], [0, 0, 1], [-1, -1, -1], [1, 1, 1]) == pytest.approx(4.0)
 
 
 def _cornell():
