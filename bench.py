@@ -41,27 +41,45 @@ def pack_scene(scene: str, out_dir: str, W: int, H: int, spp: int):
 
 
 def cpu_baseline(tri, bvh, meta, depth, target_s=12.0):
-    """C oracle on the host cores over a bounded sample of the same workload."""
+    """C oracle on the host cores over a bounded sample of the same workload (~target_s of CPU work)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (cpu_baseline leg only)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     W, H = int(meta[0]), int(meta[1])
-    # calibrate on 1/16 of the rows, one frame
     rows = max(1, H // 16)
     y0 = (H - rows) // 2
     t = time.perf_counter()
     oracle.render(tri, bvh, meta, 0, 1, 1, depth, y0=y0, y1=y0 + rows, nthreads=threads)
-    dt = time.perf_counter() - t
-    per_row = dt / rows
-    n_rows = int(min(H, max(8, target_s / max(per_row, 1e-9))))
+    per_frame = (time.perf_counter() - t) * H / rows  # one full frame
+    if per_frame >= target_s:  # a band of central rows, one frame
+        n_rows, nframes = max(8, int(H * target_s / per_frame)), 1
+    else:  # whole frames
+        n_rows, nframes = H, max(1, int(target_s / per_frame))
     y0 = (H - n_rows) // 2
     t = time.perf_counter()
-    _, c = oracle.render(tri, bvh, meta, 0, 1, 1, depth, y0=y0, y1=y0 + n_rows, nthreads=threads)
+    _, c = oracle.render(tri, bvh, meta, 0, nframes, 1, depth, y0=y0, y1=y0 + n_rows, nthreads=threads)
     dt = time.perf_counter() - t
     return {"value": round(c["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/pt_oracle.c (CPU restatement of the reference WGSL; no CPU WebGPU adapter exists here), "
-                      f"{W}x{n_rows} central rows of the {W}x{H} frame 0, depth {depth}, {threads} OpenMP threads, "
-                      f"{c['samples']} samples in {dt:.2f} s"}
+            "sample": f"oracle/pt_oracle.c (CPU restatement of the reference WGSL; no CPU WebGPU adapter exists "
+                      f"here), {W}x{n_rows} rows x {nframes} frames of the same workload (depth {depth}), "
+                      f"{threads} OpenMP threads, {c['samples']} samples in {dt:.2f} s"}
+
+
+def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world: int):
+    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC passes
+    (scripts/collect_traffic.sh -> profiles/traffic.json), when they match this configuration."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    key = f"{W}x{H}x{spp}x{depth}x{world}"
+    cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix)}
+    timed = [k for k in cands if k.endswith("false>")]  # COUNT=false: the timed (uncounted) instance
+    for k in timed or list(cands):
+        return cands[k]["hbm_bytes_per_launch"]
+    return None
 
 
 def main():
@@ -156,6 +174,8 @@ def main():
     achieved = b_alg / (k_ms * 1e-3) / 1e9
 
     if rank == 0:
+        kernel = "k_wf_trace" if args.mode == "wavefront" else "k_regen"
+        traffic = load_traffic(kernel, W, H, args.spp, args.depth, world)
         out = {
             "metric": "Msamples/s (paths/s) CornellBox 1024^2 depth 8",
             "value": round(value, 3),
@@ -174,8 +194,8 @@ def main():
                                                                         if world > 1 else ""),
                        "mode": args.mode, "samples_per_step": total_samples},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_mega", "kernel_ms": round(k_ms, 3),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": kernel, "kernel_ms": round(k_ms, 3),
                          "bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
                          "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3)},
         }
