@@ -1,11 +1,11 @@
 #!/bin/bash
 # Round-end style GPU session: parity tests, smoke, bench, rocprofv3 kernel trace of the bench,
-# PMC traffic.  Copies the summaries into profiles/<tag>_*.  Stops at the first crash/timeout.
+# PMC traffic.  Writes the summaries to gpurun_out/profiles/<tag>_* (copy into profiles/).  Stops at the first crash/timeout.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 TAG=${1:-r01}
-mkdir -p gpurun_out profiles
+mkdir -p gpurun_out/profiles
 timeout -k 10 900 python -m pytest tests -m gpu -q -rA -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|global" gpurun_out/pytest_gpu.log | tail -15
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
@@ -15,11 +15,11 @@ timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep "^{" gpurun_out/bench.log; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/bench_kt -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_kt.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
-cp gpurun_out/bench_kt/run_kernel_stats.csv profiles/${TAG}_bench_kernel_stats.csv
-grep "^{" gpurun_out/bench_kt.log > profiles/${TAG}_bench_under_rocprof.json || true
+cp gpurun_out/bench_kt/run_kernel_stats.csv gpurun_out/profiles/${TAG}_bench_kernel_stats.csv
+grep "^{" gpurun_out/bench_kt.log > gpurun_out/profiles/${TAG}_bench_under_rocprof.json || true
 timeout -k 10 900 bash scripts/collect_traffic.sh
 rc=$?; echo "traffic rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench2.log 2>&1
 rc=$?; echo "bench2 rc=$rc"; grep "^{" gpurun_out/bench2.log
-cp gpurun_out/bench.log profiles/${TAG}_bench.log
+cp gpurun_out/bench.log gpurun_out/profiles/${TAG}_bench.log
 exit $rc
