@@ -176,12 +176,102 @@ __device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, Tra
     return true;
 }
 
+// Branch-free triangle test with the exact arithmetic of test_tri: every quantity of the
+// reference's early-out chain is computed and the chain becomes one predicate (the values
+// skipped by an early return never reach `hit`, so the result is identical).
+__device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, const Ray& r, float& t_out) {
+    const float eps = 1e-8f;
+    const float4* tp = reinterpret_cast<const float4*>(tris + i);
+    float4 a = tp[0], b = tp[1], c = tp[2];
+    f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
+    f3 rce2 = cross(r.d, e2);
+    float det = dot(e1, rce2);
+    float inv_det = 1.0f / det;
+    f3 s = r.o - v0;
+    float u = inv_det * dot(s, rce2);
+    f3 sce1 = cross(s, e1);
+    float v = inv_det * dot(r.d, sce1);
+    float t = inv_det * dot(e2, sce1);
+    t_out = t;
+    const bool ok_det = !(det > -eps && det < eps);
+    const bool ok_u = !(u < 0.0f || u > 1.0f);
+    const bool ok_v = !(v < 0.0f || u + v > 1.0f);
+    return ok_det & ok_u & ok_v & (t > eps);
+}
+
+// trav_step with every per-lane branch replaced by selects (the scalar unit is shared by
+// the CU's four SIMDs and the exec-mask bookkeeping of divergent branches was ~0.7 SALU
+// per VALU instruction).  All lanes run the chosen unit on a valid record; lanes for which
+// the unit is not meant keep their state.  The push/pop decision stores unconditionally
+// into stack[sp], the free slot just above the lane's stack top, and reads stack[sp-1].
 template <bool COUNT>
-__device__ __forceinline__ int trace_flat(const SceneView& sc, const Ray& r, float& t_out, int32_t* stack, int stride,
-                                          Counters& cnt, bool active = true) {
+__device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r, TravState& s, int32_t* stack,
+                                               int stride, Counters& cnt) {
+    const bool is_leaf = !s.done && s.in_leaf;
+    const bool is_node = !s.done && !s.in_leaf;
+    const uint64_t want_leaf = __ballot(is_leaf);
+    const uint64_t want_node = __ballot(is_node);
+    if ((want_leaf | want_node) == 0) return false;
+    bool decide;
+    if (__popcll(want_leaf) >= __popcll(want_node)) {  // wave-uniform
+        const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+        float t;
+        const bool hit = tri_hit(sc.tris, is_leaf ? idx : 0, r, t);
+        const bool take = is_leaf & hit & ((s.best_t < 0.0f) | (t < s.best_t));
+        s.best_t = take ? t : s.best_t;
+        s.best = take ? idx : s.best;
+        if (COUNT) cnt.tri_tests += is_leaf ? 1 : 0;
+        s.k += is_leaf ? 1 : 0;
+        decide = is_leaf & (s.k == s.nt);
+        s.in_leaf = s.in_leaf & !decide;
+    } else {
+        const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * (is_node ? s.node : 0);
+        float4 a = np[0], b = np[1], c = np[2];
+        int4 d = reinterpret_cast<const int4*>(np)[3];
+        if (COUNT) { cnt.nodes += is_node ? 1 : 0; cnt.box_tests += is_node ? 2 : 0; }
+        const float ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
+        const float rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
+        const bool li = 0.0f < ld, ri = 0.0f < rd;
+        const bool lleaf = d.z >= 0, rleaf = d.w >= 0;
+        const int na = (li & lleaf) ? d.z : 0;
+        const int nt = na + ((ri & rleaf) ? d.w : 0);
+        if (is_node) {  // plain moves; the compiler turns these into selects
+            s.ld = ld; s.rd = rd; s.na = na; s.nt = nt;
+            s.la = d.x; s.lb = d.y; s.lc = d.x; s.rc = d.y; s.k = 0;
+            s.lint = li & !lleaf;
+            s.rint = ri & !rleaf;
+        }
+        decide = is_node & (nt == 0);
+        s.in_leaf = is_node ? (nt > 0) : s.in_leaf;
+    }
+    const bool tl = decide & s.lint & !((s.best_t > 0.0f) & (s.ld > s.best_t));
+    const bool tr = decide & s.rint & !((s.best_t > 0.0f) & (s.rd > s.best_t));
+    const bool push = tl & tr;
+    const bool pop = decide & !tl & !tr;
+    stack[s.sp * stride] = s.lc;  // slot above the top: free unless this is a push
+    const int top = stack[(s.sp > 0 ? s.sp - 1 : 0) * stride];
+    s.node = tr ? s.rc : (tl ? s.lc : (pop ? top : s.node));
+    s.done = s.done | (pop & (s.sp == 0));
+    s.sp += push ? 1 : ((pop & (s.sp > 0)) ? -1 : 0);
+    return true;
+}
+
+// Traversal flavours (LaunchOpts.trav): 0 nested loops (trace), 1 flattened with per-lane
+// branches (trav_step), 2 flattened and predicated (trav_step_pred, default).
+template <int TRAV, bool COUNT>
+__device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, TravState& s, int32_t* stack, int stride,
+                                             Counters& cnt) {
+    if (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
+    return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);
+}
+
+template <int TRAV, bool COUNT>
+__device__ __forceinline__ int trace_any(const SceneView& sc, const Ray& r, float& t_out, int32_t* stack, int stride,
+                                         Counters& cnt) {
+    if (TRAV == 0) return trace<COUNT>(sc, r, t_out, stack, stride, cnt);
     TravState s;
-    trav_init(s, active);
-    while (trav_step<COUNT>(sc, r, s, stack, stride, cnt)) {
+    trav_init(s, true);
+    while (trav_advance<TRAV, COUNT>(sc, r, s, stack, stride, cnt)) {
     }
     t_out = s.best_t;
     return s.best;

@@ -21,7 +21,7 @@ struct LaunchOpts {
     bool wavefront = false;  // wavefront pipeline (pt_wavefront.hip)
     bool literal = false;  // k_mega: the reference's control flow
     bool lds = true;       // stage the scene in LDS when it fits
-    bool flat = true;      // flattened wave-scheduled traversal (trav_step) vs nested loops
+    int trav = 2;          // traversal: 0 nested loops, 1 flattened (trav_step), 2 flattened+predicated
 };
 
 bool scene_fits_lds(const SceneView& sc);

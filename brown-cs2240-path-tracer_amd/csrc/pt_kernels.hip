@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kMegaBlock) void k_mega(SceneView sc, FrameParams f
 // ---------------------------------------------------------------------------------------
 // Megakernel: path regeneration, one traversal site, optional LDS scene, flat traversal
 // ---------------------------------------------------------------------------------------
-template <bool LDS, bool FLAT, bool ACCUM, bool COUNT>
+template <bool LDS, int TRAV, bool ACCUM, bool COUNT>
 __global__ __launch_bounds__(kMegaBlock) void k_regen(SceneView sc, FrameParams fp, uint32_t frame0, uint32_t nframes,
                                                      uint32_t stride, float* __restrict__ out, Counters* cnt_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -119,8 +119,7 @@ __global__ __launch_bounds__(kMegaBlock) void k_regen(SceneView sc, FrameParams 
             if (COUNT) { c.samples++; c.ext_queries++; }
         }
         float t;
-        const int rec = FLAT ? trace_flat<COUNT>(sc, ray, t, stack, kMegaBlock, c)
-                             : trace<COUNT>(sc, ray, t, stack, kMegaBlock, c);
+        const int rec = trace_any<TRAV, COUNT>(sc, ray, t, stack, kMegaBlock, c);
         bool more;
         if (phase == kExt) {
             more = path_after_ext(sc, rec, t, ray, ps);
@@ -172,24 +171,24 @@ bool scene_fits_lds(const SceneView& sc) {
     return (size_t)sc.max_stack * kMegaBlock * 4 + sc.span_bytes <= kLdsSceneBudget;
 }
 
-template <bool LDS, bool FLAT, bool ACCUM, bool COUNT>
+template <bool LDS, int TRAV, bool ACCUM, bool COUNT>
 static void launch_regen_t(const SceneView& sc, const FrameParams& fp, uint32_t frame0, uint32_t nframes, uint32_t stride,
                            float* out, Counters* cnt, hipStream_t stream) {
     dim3 grid((fp.width + 15) / 16, (fp.height + 15) / 16), block(kMegaBlock);
     size_t lds = (size_t)sc.max_stack * kMegaBlock * 4 + (LDS ? sc.span_bytes : 0);
-    hipLaunchKernelGGL((k_regen<LDS, FLAT, ACCUM, COUNT>), grid, block, lds, stream, sc, fp, frame0, nframes, stride, out,
+    hipLaunchKernelGGL((k_regen<LDS, TRAV, ACCUM, COUNT>), grid, block, lds, stream, sc, fp, frame0, nframes, stride, out,
                        cnt);
 }
 
-template <bool LDS, bool FLAT>
+template <bool LDS, int TRAV>
 static void launch_regen_a(const SceneView& sc, const FrameParams& fp, uint32_t frame0, uint32_t nframes, uint32_t stride,
                            bool accum, bool count, float* out, Counters* cnt, hipStream_t stream) {
     if (accum) {
-        if (count) launch_regen_t<LDS, FLAT, true, true>(sc, fp, frame0, nframes, stride, out, cnt, stream);
-        else launch_regen_t<LDS, FLAT, true, false>(sc, fp, frame0, nframes, stride, out, cnt, stream);
+        if (count) launch_regen_t<LDS, TRAV, true, true>(sc, fp, frame0, nframes, stride, out, cnt, stream);
+        else launch_regen_t<LDS, TRAV, true, false>(sc, fp, frame0, nframes, stride, out, cnt, stream);
     } else {
-        if (count) launch_regen_t<LDS, FLAT, false, true>(sc, fp, frame0, nframes, stride, out, cnt, stream);
-        else launch_regen_t<LDS, FLAT, false, false>(sc, fp, frame0, nframes, stride, out, cnt, stream);
+        if (count) launch_regen_t<LDS, TRAV, false, true>(sc, fp, frame0, nframes, stride, out, cnt, stream);
+        else launch_regen_t<LDS, TRAV, false, false>(sc, fp, frame0, nframes, stride, out, cnt, stream);
     }
 }
 
@@ -206,13 +205,13 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
         return hipGetLastError();
     }
     const bool lds = lo.lds && scene_fits_lds(sc);
+#define RA(L, T) launch_regen_a<L, T>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream)
     if (lds) {
-        if (lo.flat) launch_regen_a<true, true>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream);
-        else launch_regen_a<true, false>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream);
+        if (lo.trav == 0) RA(true, 0); else if (lo.trav == 1) RA(true, 1); else RA(true, 2);
     } else {
-        if (lo.flat) launch_regen_a<false, true>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream);
-        else launch_regen_a<false, false>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream);
+        if (lo.trav == 0) RA(false, 0); else if (lo.trav == 1) RA(false, 1); else RA(false, 2);
     }
+#undef RA
     return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@
 #include "pt_path.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pt {
 
@@ -99,8 +100,8 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
     if (COUNT) flush_counters(c, cnt_out);
 }
 
-template <bool LDS, bool COUNT>
-__global__ __launch_bounds__(256) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
+template <bool LDS, int TRAV, bool COUNT>
+__global__ __launch_bounds__(256) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out, int dbg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
@@ -130,9 +131,9 @@ __global__ __launch_bounds__(256) void k_wf_trace(SceneView sc, WfBuffers wb, in
     if (pf) { pa = q[2 * (size_t)pidx]; pb = q[2 * (size_t)pidx + 1]; }
     cur = min(cur + 64, end);
     while (true) {
-        if (!trav_step<COUNT>(sc, r, s, stack, blockDim.x, c) && !__any(pf)) break;
+        if (!trav_advance<TRAV, COUNT>(sc, r, s, stack, blockDim.x, c) && !__any(pf)) break;
         if (has && s.done) {
-            wb.hitq[idx] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
+            if (!(dbg & 1)) wb.hitq[idx] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));  // dbg&1: timing only
             has = false;
         }
         if (!has && pf) {  // swap in the prefetched ray
@@ -225,31 +226,33 @@ __global__ __launch_bounds__(256) void k_wf_accum(const float* __restrict__ rad,
 // ---------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------
-template <bool LDS, bool COUNT>
+template <bool LDS, int TRAV, bool COUNT>
 static int trace_blocks(size_t lds_bytes) {
-    static int cached[2][2] = {{0, 0}, {0, 0}};
-    static size_t cached_lds[2][2] = {{0, 0}, {0, 0}};
-    int& b = cached[LDS][COUNT];
-    if (b == 0 || cached_lds[LDS][COUNT] != lds_bytes) {
+    static int cached = 0;
+    static size_t cached_lds = 0;
+    int& b = cached;
+    if (b == 0 || cached_lds != lds_bytes) {
         int per_cu = 0, dev = 0, cus = 0;
         hipGetDevice(&dev);
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_wf_trace<LDS, COUNT>, 256, lds_bytes);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_wf_trace<LDS, TRAV, COUNT>, 256, lds_bytes);
         b = std::max(1, per_cu) * std::max(1, cus);
-        cached_lds[LDS][COUNT] = lds_bytes;
+        cached_lds = lds_bytes;
     }
     return b;
 }
 
-template <bool LDS, bool COUNT>
+template <bool LDS, int TRAV, bool COUNT>
 static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const WfBuffers& wb, uint32_t frame0,
                               uint32_t nframes, uint32_t stride, bool accum, float* out, Counters* cnt,
                               hipStream_t stream) {
     const uint32_t npix = fp.width * fp.height;
     const uint32_t F = std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
     const size_t lds = (size_t)sc.max_stack * 256 * 4 + (LDS ? sc.span_bytes : 0);
-    const int tblocks = trace_blocks<LDS, COUNT>(lds);
+    const int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
     const int iters = 2 * (fp.max_depth + 1);
+    const char* dbg_env = std::getenv("PT_WF_DEBUG");  // timing experiments only (wrong results)
+    const int dbg = dbg_env ? std::atoi(dbg_env) : 0;
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         const uint32_t P = Fb * npix;
@@ -258,7 +261,7 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                            P, !accum, cnt);
         int in_q = 0;
         for (int it = 0; it < iters; ++it) {
-            hipLaunchKernelGGL((k_wf_trace<LDS, COUNT>), dim3(tblocks), dim3(256), lds, stream, sc, wb, in_q, cnt);
+            hipLaunchKernelGGL((k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(256), lds, stream, sc, wb, in_q, cnt, dbg);
             if ((it & 1) == 0)
                 hipLaunchKernelGGL((k_wf_shade<true, COUNT>), dim3(sblocks), dim3(256), 0, stream, sc, fp, wb, in_q, cnt);
             else
@@ -275,10 +278,15 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
                             Counters* cnt, hipStream_t stream) {
     if (!accum) { nframes = 1; stride = 1; }
     const bool lds = lo.lds && scene_fits_lds(sc);
-    if (lds) return count ? wf_render_t<true, true>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream)
-                          : wf_render_t<true, false>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream);
-    return count ? wf_render_t<false, true>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream)
-                 : wf_render_t<false, false>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream);
+    const int trav = lo.trav == 1 ? 1 : 2;  // the wavefront always uses a flattened traversal
+#define WF(L, T, C) return wf_render_t<L, T, C>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream)
+    if (lds) {
+        if (trav == 1) { if (count) WF(true, 1, true); else WF(true, 1, false); }
+        if (count) WF(true, 2, true); else WF(true, 2, false);
+    }
+    if (trav == 1) { if (count) WF(false, 1, true); else WF(false, 1, false); }
+    if (count) WF(false, 2, true); else WF(false, 2, false);
+#undef WF
 }
 
 }  // namespace pt
