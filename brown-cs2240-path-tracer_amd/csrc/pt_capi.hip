@@ -313,7 +313,7 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 }
 
 // PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
-// PT_TRAV=nested|flat1|pred.
+// PT_TRAV=nested|flat1|pred|lean.
 LaunchOpts launch_opts(int mode) {
     LaunchOpts lo;
     lo.wavefront = mode == PT_MODE_WAVEFRONT;
@@ -323,7 +323,7 @@ LaunchOpts launch_opts(int mode) {
         if (!std::strcmp(e, "mega") || lo.literal) lo.wavefront = false;
     }
     if (const char* e = std::getenv("PT_LDS")) lo.lds = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : (!std::strcmp(e, "flat1") ? 1 : 2);
+    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : 3;
     return lo;
 }
 

@@ -256,20 +256,94 @@ __device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r
     return true;
 }
 
+// trav_step with its per-lane state laid out for the compiler: loop-carried flags live
+// in one VGPR bitfield (a bool carried around the loop becomes an SGPR lane mask that
+// needs an s_andn2/s_and/s_or merge at every join; a VGPR written under exec needs none),
+// the triangle test is branch-free (its three early-outs can only skip work when all 64
+// lanes reject at the same step, which practically never happens), each unit is one exec
+// region and the push/pop decision is straight-line (stack[sp] is the free slot above the
+// top: max_stack = max depth + 1, pt_capi.hip).  Same units, same order, same arithmetic.
+enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8 };
+struct TravLean {
+    int node, sp, k, na, nt, la, lb, fl, best;
+    float ld, rd, best_t;
+};
+__device__ __forceinline__ void trav_init(TravLean& s, bool active) {
+    s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1;
+    s.fl = active ? 0 : TF_DONE;
+    s.ld = 0.0f; s.rd = 0.0f; s.best_t = -1.0f;
+}
+__device__ __forceinline__ bool trav_finished(const TravLean& s) { return (s.fl & TF_DONE) != 0; }
+__device__ __forceinline__ bool trav_finished(const TravState& s) { return s.done; }
+
+template <bool COUNT>
+__device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
+                                               int stride, Counters& cnt) {
+    const int state = s.fl & (TF_LEAF | TF_DONE);
+    const uint64_t want_leaf = __ballot(state == TF_LEAF);
+    const uint64_t want_node = __ballot(state == 0);
+    if ((want_leaf | want_node) == 0) return false;
+    bool decide = false;
+    if (__popcll(want_leaf) >= __popcll(want_node)) {  // wave-uniform
+        if (state == TF_LEAF) {
+            const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+            float t;
+            const bool take = tri_hit(sc.tris, idx, r, t) & ((s.best_t < 0.0f) | (t < s.best_t));
+            s.best_t = take ? t : s.best_t;
+            s.best = take ? idx : s.best;
+            if (COUNT) cnt.tri_tests++;
+            s.k += 1;
+            decide = s.k == s.nt;
+            s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
+        }
+    } else if (state == 0) {
+        const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * s.node;
+        float4 a = np[0], b = np[1], c = np[2];
+        int4 d = reinterpret_cast<const int4*>(np)[3];
+        if (COUNT) { cnt.nodes++; cnt.box_tests += 2; }
+        s.ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
+        s.rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
+        const bool li = 0.0f < s.ld, ri = 0.0f < s.rd;
+        const bool lleaf = d.z >= 0, rleaf = d.w >= 0;
+        s.na = (li & lleaf) ? d.z : 0;
+        s.nt = s.na + ((ri & rleaf) ? d.w : 0);
+        s.la = d.x; s.lb = d.y; s.k = 0;
+        s.fl = ((li & !lleaf) ? TF_LINT : 0) | ((ri & !rleaf) ? TF_RINT : 0) | (s.nt > 0 ? TF_LEAF : 0);
+        decide = s.nt == 0;
+    }
+    if (decide) {
+        const bool tl = (s.fl & TF_LINT) && !((s.best_t > 0.0f) & (s.ld > s.best_t));
+        const bool tr = (s.fl & TF_RINT) && !((s.best_t > 0.0f) & (s.rd > s.best_t));
+        const bool pop = !tl & !tr;
+        stack[s.sp * stride] = s.la;  // a push keeps it, anything else leaves the slot free
+        const int top = stack[max(s.sp - 1, 0) * stride];
+        s.node = tr ? s.lb : (tl ? s.la : top);
+        s.fl |= (pop & (s.sp == 0)) ? TF_DONE : 0;
+        s.sp += (tl & tr) ? 1 : (pop ? -1 : 0);  // sp < 0 only once done
+    }
+    return true;
+}
+
 // Traversal flavours (LaunchOpts.trav): 0 nested loops (trace), 1 flattened with per-lane
-// branches (trav_step), 2 flattened and predicated (trav_step_pred, default).
+// branches (trav_step), 2 flattened and predicated (trav_step_pred), 3 lean (trav_step_lean).
+template <int TRAV>
+struct TravSel { using type = TravState; };
+template <>
+struct TravSel<3> { using type = TravLean; };
+
 template <int TRAV, bool COUNT>
-__device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, TravState& s, int32_t* stack, int stride,
-                                             Counters& cnt) {
-    if (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
-    return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);
+__device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
+                                             int32_t* stack, int stride, Counters& cnt) {
+    if constexpr (TRAV == 3) return trav_step_lean<COUNT>(sc, r, s, stack, stride, cnt);
+    else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
+    else return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);
 }
 
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ int trace_any(const SceneView& sc, const Ray& r, float& t_out, int32_t* stack, int stride,
                                          Counters& cnt) {
     if (TRAV == 0) return trace<COUNT>(sc, r, t_out, stack, stride, cnt);
-    TravState s;
+    typename TravSel<TRAV>::type s;
     trav_init(s, true);
     while (trav_advance<TRAV, COUNT>(sc, r, s, stack, stride, cnt)) {
     }

@@ -21,7 +21,7 @@ struct LaunchOpts {
     bool wavefront = false;  // wavefront pipeline (pt_wavefront.hip)
     bool literal = false;  // k_mega: the reference's control flow
     bool lds = true;       // stage the scene in LDS when it fits
-    int trav = 2;          // traversal: 0 nested loops, 1 flattened (trav_step), 2 flattened+predicated
+    int trav = 3;          // traversal: 0 nested loops, 1 flattened (trav_step), 2 flattened+predicated, 3 lean
 };
 
 bool scene_fits_lds(const SceneView& sc);

@@ -20,7 +20,6 @@
 #include "pt_path.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace pt {
 
@@ -100,61 +99,82 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
     if (COUNT) flush_counters(c, cnt_out);
 }
 
+// Per-wave LDS staging for k_wf_trace: the current window of 64 queued rays and a ring of
+// hit records.  Keeping both in LDS takes every global load and store out of the traversal
+// loop: on gfx9 loads and stores share the wave's in-order vmcnt, so a per-lane global store
+// (or prefetch) in the loop makes the next use of any loaded register wait for it.
+constexpr uint32_t kWinRays = 32;
+constexpr uint32_t kHitRing = 128;  // entries; power of two, multiple of kWinRays
+constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8;
+constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
+
 template <bool LDS, int TRAV, bool COUNT>
-__global__ __launch_bounds__(256) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out, int dbg) {
+__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
+    char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
+    char* stage = stage_base + (threadIdx.x / 64u) * kStageBytes;
+    float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
+    int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [kHitRing]
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     const uint32_t count = wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64), w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t per = (count + nwaves - 1) / nwaves;
     const uint32_t begin = min(w * per, count), end = min(begin + per, count);
-    if (LDS) stage_scene_lds(sc, smem + (uint32_t)sc.max_stack * blockDim.x * 4u);
+    if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * kStageBytes);
     if (begin >= end) return;  // wave-uniform
     const float4* q = in_q ? wb.rq1 : wb.rq0;
     const uint32_t lane = lane_id();
     Counters c = {};
-    // current ray
-    uint32_t cur = begin;
-    uint32_t idx = cur + lane, p = 0;
-    bool has = idx < end;
+    // window [ws, we) sits in LDS; the following window [ns, ne) is in flight in registers
+    uint32_t ws = begin, we = min(begin + kWinRays, end);
+    // lanes 0..31 carry the rays of a window, lanes 32..63 the second halves of each record
+    const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
+    if (ws + wl < we) wray[2 * wl + half] = q[2 * (size_t)(ws + wl) + half];
+    uint32_t ns = we, ne = min(we + kWinRays, end);
+    float4 na = make_float4(0, 0, 0, 0);
+    if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
+    uint32_t cur = ws;      // next queue entry to hand out
+    uint32_t flushed = ws;  // entries below this are in wb.hitq
+    uint32_t idx = 0, p = 0;
+    bool has = false;
     Ray r;
     r.o = r.d = r.inv = mk(0.0f, 0.0f, 0.0f);
-    if (has) r = unpack_ray(q[2 * (size_t)idx], q[2 * (size_t)idx + 1], p);
-    cur = min(cur + 64, end);
-    TravState s;
-    trav_init(s, has);
-    // prefetched ray (loads stay in flight until the lane swaps it in)
-    uint32_t pidx = cur + lane;
-    bool pf = pidx < end;
-    float4 pa = make_float4(0, 0, 0, 0), pb = pa;
-    if (pf) { pa = q[2 * (size_t)pidx]; pb = q[2 * (size_t)pidx + 1]; }
-    cur = min(cur + 64, end);
+    typename TravSel<TRAV>::type s;
+    trav_init(s, false);
     while (true) {
-        if (!trav_advance<TRAV, COUNT>(sc, r, s, stack, blockDim.x, c) && !__any(pf)) break;
-        if (has && s.done) {
-            if (!(dbg & 1)) wb.hitq[idx] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));  // dbg&1: timing only
+        // hand the next entries to idle lanes (wave-uniform control)
+        const uint64_t need = __ballot(!has);
+        if (need && cur < end) {
+            if (cur == we && ne - flushed <= kHitRing) {  // next window, if the hit ring has room
+                if (ns + wl < ne) wray[2 * wl + half] = na;
+                ws = ns; we = ne; ns = we; ne = min(we + kWinRays, end);
+                if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
+            }
+            if (cur < we) {
+                const uint32_t j = cur + rank_below(need);
+                if (!has && j < we) {
+                    r = unpack_ray(wray[2 * (j - ws)], wray[2 * (j - ws) + 1], p);
+                    idx = j;
+                    trav_init(s, true);
+                    has = true;
+                }
+                cur = min(cur + (uint32_t)__popcll(need), we);
+            }
+        }
+        if (!__any(has)) break;  // nothing in flight and nothing left to hand out
+        trav_advance<TRAV, COUNT>(sc, r, s, stack, blockDim.x, c);
+        if (has && trav_finished(s)) {
+            ring[(idx - begin) & (kHitRing - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;
         }
-        if (!has && pf) {  // swap in the prefetched ray
-            r = unpack_ray(pa, pb, p);
-            idx = pidx;
-            trav_init(s, true);
-            has = true;
-            pf = false;
-        }
-        if (cur < end) {  // refill the prefetch slots that were consumed
-            const uint64_t need = __ballot(!pf);
-            if (need) {
-                const uint32_t j = cur + rank_below(need);
-                if (!pf && j < end) {
-                    pidx = j;
-                    pa = q[2 * (size_t)j];
-                    pb = q[2 * (size_t)j + 1];
-                    pf = true;
-                }
-                cur = min(cur + (uint32_t)__popcll(need), end);
-            }
+        // write back every fully traced window: coalesced, once per 64 entries
+        while (true) {
+            const uint32_t fe = min(flushed + kWinRays, end);
+            if (fe > cur || flushed >= end || __any(has && idx < fe)) break;
+            const uint32_t e = flushed + lane;  // fe - flushed <= 32: the upper half of the wave idles
+            if (e < fe) wb.hitq[e] = ring[(e - begin) & (kHitRing - 1)];
+            flushed = fe;
         }
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -235,7 +255,8 @@ static int trace_blocks(size_t lds_bytes) {
         int per_cu = 0, dev = 0, cus = 0;
         hipGetDevice(&dev);
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_wf_trace<LDS, TRAV, COUNT>, 256, lds_bytes);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_wf_trace<LDS, TRAV, COUNT>, kTraceBlock,
+                                                     lds_bytes);
         b = std::max(1, per_cu) * std::max(1, cus);
         cached_lds = lds_bytes;
     }
@@ -248,11 +269,9 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                               hipStream_t stream) {
     const uint32_t npix = fp.width * fp.height;
     const uint32_t F = std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
-    const size_t lds = (size_t)sc.max_stack * 256 * 4 + (LDS ? sc.span_bytes : 0);
+    const size_t lds = (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * kStageBytes + (LDS ? sc.span_bytes : 0);
     const int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
     const int iters = 2 * (fp.max_depth + 1);
-    const char* dbg_env = std::getenv("PT_WF_DEBUG");  // timing experiments only (wrong results)
-    const int dbg = dbg_env ? std::atoi(dbg_env) : 0;
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         const uint32_t P = Fb * npix;
@@ -261,7 +280,7 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                            P, !accum, cnt);
         int in_q = 0;
         for (int it = 0; it < iters; ++it) {
-            hipLaunchKernelGGL((k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(256), lds, stream, sc, wb, in_q, cnt, dbg);
+            hipLaunchKernelGGL((k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, stream, sc, wb, in_q, cnt);
             if ((it & 1) == 0)
                 hipLaunchKernelGGL((k_wf_shade<true, COUNT>), dim3(sblocks), dim3(256), 0, stream, sc, fp, wb, in_q, cnt);
             else
@@ -278,13 +297,15 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
                             Counters* cnt, hipStream_t stream) {
     if (!accum) { nframes = 1; stride = 1; }
     const bool lds = lo.lds && scene_fits_lds(sc);
-    const int trav = lo.trav == 1 ? 1 : 2;  // the wavefront always uses a flattened traversal
+    const int trav = lo.trav == 0 ? 1 : lo.trav;  // the wavefront always uses a flattened traversal
 #define WF(L, T, C) return wf_render_t<L, T, C>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream)
     if (lds) {
         if (trav == 1) { if (count) WF(true, 1, true); else WF(true, 1, false); }
+        if (trav == 3) { if (count) WF(true, 3, true); else WF(true, 3, false); }
         if (count) WF(true, 2, true); else WF(true, 2, false);
     }
     if (trav == 1) { if (count) WF(false, 1, true); else WF(false, 1, false); }
+    if (trav == 3) { if (count) WF(false, 3, true); else WF(false, 3, false); }
     if (count) WF(false, 2, true); else WF(false, 2, false);
 #undef WF
 }

@@ -23,18 +23,21 @@ VARIANTS = {
     "auto": {},
     "literal": {"PT_KERNEL": "literal"},
     "mega_nested": {"PT_KERNEL": "mega", "PT_TRAV": "nested"},
-    "mega_flat_global": {"PT_KERNEL": "mega", "PT_LDS": "0"},
-    "mega_flat_lds": {"PT_KERNEL": "mega"},
-    "wavefront_global": {"PT_KERNEL": "wavefront", "PT_LDS": "0"},
-    "wavefront_lds": {"PT_KERNEL": "wavefront"},
-    "mega_flat1_lds": {"PT_KERNEL": "mega", "PT_TRAV": "flat1"},
-    "wavefront_flat1_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1"},
-    "wavefront_nostore": {"PT_KERNEL": "wavefront", "PT_WF_DEBUG": "1"},
+    "mega_flat_global": {"PT_KERNEL": "mega", "PT_TRAV": "flat1", "PT_LDS": "0"},
+    "mega_flat_lds": {"PT_KERNEL": "mega", "PT_TRAV": "flat1"},
+    "mega_pred_lds": {"PT_KERNEL": "mega", "PT_TRAV": "pred"},
+    "mega_lean_lds": {"PT_KERNEL": "mega", "PT_TRAV": "lean"},
+    "mega_lean_global": {"PT_KERNEL": "mega", "PT_TRAV": "lean", "PT_LDS": "0"},
+    "wavefront_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1", "PT_LDS": "0"},
+    "wavefront_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1"},
+    "wavefront_pred_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "pred"},
+    "wavefront_lean_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean"},
+    "wavefront_lean_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean", "PT_LDS": "0"},
 }
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_WF_DEBUG"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 
@@ -83,7 +86,7 @@ def main():
             out = acc.cpu().numpy()
             if ref is None:
                 ref = out.copy()
-            elif "nostore" not in v and not np.array_equal(out.view(np.uint32), ref.view(np.uint32)):
+            elif not np.array_equal(out.view(np.uint32), ref.view(np.uint32)):
                 print(json.dumps({"variant": v, "error": "result differs from first variant"}), flush=True)
     n = W * H * args.spp
     for v in variants:

@@ -18,10 +18,16 @@ KERNELS = {
     "auto": {},
     "literal": {"PT_KERNEL": "literal"},
     "mega_nested": {"PT_KERNEL": "mega", "PT_TRAV": "nested"},
-    "mega_flat_global": {"PT_KERNEL": "mega", "PT_LDS": "0"},
-    "mega_flat_lds": {"PT_KERNEL": "mega"},
-    "wavefront_global": {"PT_KERNEL": "wavefront", "PT_LDS": "0"},
-    "wavefront_lds": {"PT_KERNEL": "wavefront"},
+    "mega_flat_global": {"PT_KERNEL": "mega", "PT_TRAV": "flat1", "PT_LDS": "0"},
+    "mega_flat_lds": {"PT_KERNEL": "mega", "PT_TRAV": "flat1"},
+    "mega_pred_lds": {"PT_KERNEL": "mega", "PT_TRAV": "pred"},
+    "mega_lean_lds": {"PT_KERNEL": "mega", "PT_TRAV": "lean"},
+    "mega_lean_global": {"PT_KERNEL": "mega", "PT_TRAV": "lean", "PT_LDS": "0"},
+    "wavefront_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1", "PT_LDS": "0"},
+    "wavefront_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1"},
+    "wavefront_pred_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "pred"},
+    "wavefront_lean_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean"},
+    "wavefront_lean_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean", "PT_LDS": "0"},
 }
 
 
