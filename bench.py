@@ -9,9 +9,14 @@ work is fixed as N grows.  The scene is packed by the product's Node host
 (node/bin/pt-pack.js) before timing; scene upload is outside the timed region.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` for the
-render kernel (algorithmic bytes per launch from the GPU's own work counters, SURVEY.md §8d:
-B_alg = 48*Q + 96*Q_ext + 24 bytes per sample, over the kernel's HIP-event duration) and
-`cpu_baseline` (the C oracle, oracle/pt_oracle.c, on the host cores, rank 0 at N=1 only).
+dominant kernel (the one with the most HIP-event time in the timed region, recorded by the
+library around every launch on the render stream: pt_profile_enable/pt_profile_read).
+Its algorithmic bytes per launch follow SURVEY.md §8d from the GPU's own work counters:
+k_wf_trace (wavefront) moves 48 B per ray query (32 B ray read + 16 B hit write), so a launch
+carries 48*Q / launches; the megakernel k_regen carries the whole path model
+B_alg = 48*Q + 96*Q_ext + 24 B per sample in one launch.  `pipeline` gives B_alg over the
+whole render.  `cpu_baseline` is the C oracle (oracle/pt_oracle.c) on the host cores, rank 0
+at N=1 only.
 """
 import argparse
 import json
@@ -145,7 +150,8 @@ def main():
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    kernel_ms = []
+    render_ms = []
+    scene.profile_enable(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         with torch.cuda.stream(stream):
@@ -155,12 +161,14 @@ def main():
             ev1.record(stream)
             reduce_accum(acc, dist)
         ev1.synchronize()
-        kernel_ms.append(ev0.elapsed_time(ev1))
+        render_ms.append(ev0.elapsed_time(ev1))
     stream.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    prof = scene.profile_read()
+    scene.profile_enable(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -169,13 +177,20 @@ def main():
     total_samples = W * H * args.spp
     ms_per_step = elapsed / args.steps * 1e3
     value = total_samples / (elapsed / args.steps) / 1e6
-    k_ms = float(np.mean(kernel_ms))
-    b_alg = (48.0 * (q_ext + q_sh) + 96.0 * q_ext + 24.0 * samples_c)  # bytes per launch
-    achieved = b_alg / (k_ms * 1e-3) / 1e9
+    r_ms = float(np.mean(render_ms))
+    b_alg = (48.0 * (q_ext + q_sh) + 96.0 * q_ext + 24.0 * samples_c)  # bytes per render
+    kernel = max(prof, key=lambda k: prof[k]["total_ms"])
+    launches_per_render = prof[kernel]["launches"] / args.steps
+    k_ms = prof[kernel]["avg_ms"]
+    if kernel == "k_wf_trace":
+        bytes_per_launch = 48.0 * (q_ext + q_sh) / launches_per_render
+    else:  # the megakernel: the whole path model in one launch
+        bytes_per_launch = b_alg / launches_per_render
+    achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
+    pipeline = b_alg / (r_ms * 1e-3) / 1e9
 
     if rank == 0:
-        kernel = "k_wf_trace" if args.mode == "wavefront" else "k_regen"
-        traffic = load_traffic(kernel, W, H, args.spp, args.depth, world)
+        traffic = load_traffic(kernel + "<", W, H, args.spp, args.depth, world)
         out = {
             "metric": "Msamples/s (paths/s) CornellBox 1024^2 depth 8",
             "value": round(value, 3),
@@ -195,9 +210,12 @@ def main():
                        "mode": args.mode, "samples_per_step": total_samples},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": kernel, "kernel_ms": round(k_ms, 3),
-                         "bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
-                         "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3)},
+                         "kernel": kernel, "kernel_avg_ms": round(k_ms, 4),
+                         "launches_per_step": launches_per_render, "bytes_per_launch": round(bytes_per_launch),
+                         "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3),
+                         "pipeline": {"bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
+                                      "achieved": round(pipeline, 2), "frac": round(pipeline / HBM_PEAK_GBS, 4)},
+                         "kernels_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()}},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(tri, bvh, meta, args.depth)

@@ -200,11 +200,84 @@ struct pt_scene {
     Counters* d_counters = nullptr;
     void* d_wf = nullptr;  // wavefront path state, allocated on first use
     WfBuffers wf{};
+    bool prof_on = false;  // pt_profile_enable
+    KernelProfiler prof;
 };
+
+namespace pt {
+thread_local KernelProfiler* t_prof = nullptr;
+
+hipEvent_t KernelProfiler::take() {
+    hipEvent_t e = nullptr;
+    if (!pool.empty()) {
+        e = pool.back();
+        pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        e = nullptr;
+    }
+    return e;
+}
+void KernelProfiler::start(int kid, hipStream_t st) {
+    Rec r{kid, take(), take()};
+    if (r.a) hipEventRecord(r.a, st);
+    recs.push_back(r);
+}
+void KernelProfiler::stop(hipStream_t st) {
+    if (!recs.empty() && recs.back().b) hipEventRecord(recs.back().b, st);
+}
+void KernelProfiler::reset() {
+    for (auto& r : recs) {
+        if (r.a) pool.push_back(r.a);
+        if (r.b) pool.push_back(r.b);
+    }
+    recs.clear();
+}
+void KernelProfiler::destroy() {
+    reset();
+    for (auto e : pool) hipEventDestroy(e);
+    pool.clear();
+}
+}  // namespace pt
 
 extern "C" {
 
 int pt_abi_version(void) { return PT_ABI_VERSION; }
+
+int pt_profile_enable(pt_scene* s, int enable) {
+    if (!s) return fail(PT_ERR_INVALID, "null scene");
+    HIP_TRY(hipSetDevice(s->device));
+    s->prof.reset();
+    s->prof_on = enable != 0;
+    return PT_OK;
+}
+
+int pt_profile_read(pt_scene* s, pt_kernel_time* out, int max_entries, int* n_out) {
+    if (!s || !n_out || (max_entries > 0 && !out)) return fail(PT_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(s->device));
+    pt_kernel_time acc[KID_COUNT] = {};
+    for (const auto& r : s->prof.recs) {
+        if (!r.a || !r.b) return fail(PT_ERR_HIP, "profiling event could not be created");
+        HIP_TRY(hipEventSynchronize(r.b));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+        pt_kernel_time& k = acc[r.kid];
+        k.min_ms = k.launches ? std::min(k.min_ms, (double)ms) : (double)ms;
+        k.max_ms = k.launches ? std::max(k.max_ms, (double)ms) : (double)ms;
+        k.total_ms += ms;
+        k.launches++;
+    }
+    int n = 0;
+    for (int k = 0; k < KID_COUNT; ++k) {
+        if (!acc[k].launches) continue;
+        if (n < max_entries) {
+            out[n] = acc[k];
+            std::snprintf(out[n].name, sizeof(out[n].name), "%s", kernel_name(k));
+        }
+        ++n;
+    }
+    *n_out = std::min(n, std::max(max_entries, 0));
+    return PT_OK;
+}
 
 const char* pt_last_error(void) { return g_err.c_str(); }
 
@@ -276,6 +349,7 @@ void pt_scene_destroy(pt_scene* s) {
     if (s->d_accum) hipFree(s->d_accum);
     if (s->d_wf) hipFree(s->d_wf);
     if (s->d_mem) hipFree(s->d_mem);
+    s->prof.destroy();
     delete s;
 }
 
@@ -314,9 +388,13 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 
 // PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
 // PT_TRAV=nested|flat1|pred|lean.
-LaunchOpts launch_opts(int mode) {
+// AUTO picks the wavefront pipeline once a call has this many paths: below it the fixed
+// cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.
+constexpr uint64_t kWfAutoMinPaths = 1ull << 20;
+
+LaunchOpts launch_opts(int mode, uint64_t paths) {
     LaunchOpts lo;
-    lo.wavefront = mode == PT_MODE_WAVEFRONT;
+    lo.wavefront = mode == PT_MODE_WAVEFRONT || (mode == PT_MODE_AUTO && paths >= kWfAutoMinPaths);
     if (const char* e = std::getenv("PT_KERNEL")) {
         lo.literal = !std::strcmp(e, "literal");
         if (!std::strcmp(e, "wavefront")) lo.wavefront = true;
@@ -337,17 +415,19 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     const size_t n = paths;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
-    const size_t o_q0 = take(32 * n), o_q1 = take(32 * n), o_hit = take(8 * n), o_s0 = take(16 * n),
-                 o_s1 = take(16 * n), o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(16 * n), o_rad = take(12 * n),
-                 o_ctl = take(4 * WF_CTL_WORDS);
+    size_t oq[8];
+    for (auto& o : oq) o = take(16 * n);
+    const size_t o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(8 * n), o_hit = take(8 * n),
+                 o_rad = take(12 * n), o_ctl = take(4 * WF_CTL_WORDS);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
     char* b = static_cast<char*>(s->d_wf);
+    auto f4 = [&](size_t o) { return reinterpret_cast<float4*>(b + o); };
     WfBuffers& w = s->wf;
-    w.rq0 = reinterpret_cast<float4*>(b + o_q0); w.rq1 = reinterpret_cast<float4*>(b + o_q1);
+    w.ext = WfQueue{f4(oq[0]), f4(oq[1]), f4(oq[2]), f4(oq[3])};
+    w.shd = WfQueue{f4(oq[4]), f4(oq[5]), f4(oq[6]), f4(oq[7])};
+    w.sp0 = f4(o_p0); w.sp1 = f4(o_p1);
+    w.sp2 = reinterpret_cast<float2*>(b + o_p2);
     w.hitq = reinterpret_cast<int2*>(b + o_hit);
-    w.st0 = reinterpret_cast<float4*>(b + o_s0); w.st1 = reinterpret_cast<float4*>(b + o_s1);
-    w.sp0 = reinterpret_cast<float4*>(b + o_p0); w.sp1 = reinterpret_cast<float4*>(b + o_p1);
-    w.sp2 = reinterpret_cast<float4*>(b + o_p2);
     w.rad = reinterpret_cast<float*>(b + o_rad);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
     w.capacity = (uint32_t)n;
@@ -365,9 +445,13 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         return fail(PT_ERR_INVALID, "frame index >= 2^24 (t_k = u32(f32(k)) would round)");
     HIP_TRY(hipSetDevice(s->device));
     if (nframes == 0) return PT_OK;
-    const LaunchOpts lo = launch_opts(mode);
+    const uint64_t npix = (uint64_t)fp.width * fp.height;
+    const LaunchOpts lo = launch_opts(mode, npix * (accum ? nframes : 1));
+    struct ProfScope {  // attach the scene's profiler to this thread for the launches below
+        explicit ProfScope(KernelProfiler* p) { t_prof = p; }
+        ~ProfScope() { t_prof = nullptr; }
+    } prof_scope(s->prof_on ? &s->prof : nullptr);
     if (lo.wavefront) {
-        const uint64_t npix = (uint64_t)fp.width * fp.height;
         const uint64_t want = std::max<uint64_t>(npix, std::min<uint64_t>(npix * (accum ? nframes : 1), kWfTargetPaths));
         int rc2 = ensure_wavefront(s, want);
         if (rc2 != PT_OK) return rc2;

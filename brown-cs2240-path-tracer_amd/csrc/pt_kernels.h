@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "pt_device.h"
 
 // ids for k_selftest_math (also used by pt_selftest_math in the C-ABI)
@@ -11,6 +13,34 @@ enum {
 };
 
 namespace pt {
+
+// Kernel timing (pt_profile_enable / pt_profile_read): while a profiler is attached to the
+// calling thread, every launch is bracketed by two HIP events on its stream.
+enum KernelId : int {
+    KID_MEGA = 0, KID_REGEN, KID_WF_GENERATE, KID_WF_TRACE, KID_WF_SHADE_EXT, KID_WF_SHADE_SHADOW, KID_WF_ACCUM, KID_COUNT
+};
+inline const char* kernel_name(int k) {
+    static const char* const n[KID_COUNT] = {"k_mega",     "k_regen",         "k_wf_generate",     "k_wf_trace",
+                                             "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum"};
+    return (k >= 0 && k < KID_COUNT) ? n[k] : "?";
+}
+struct KernelProfiler {
+    struct Rec { int kid; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t take();
+    void start(int kid, hipStream_t s);
+    void stop(hipStream_t s);
+    void reset();    // records' events go back to the pool
+    void destroy();  // frees every event
+};
+extern thread_local KernelProfiler* t_prof;
+#define PT_LAUNCH(KID, STREAM, ...)                                  \
+    do {                                                             \
+        if (::pt::t_prof) ::pt::t_prof->start((KID), (STREAM));      \
+        hipLaunchKernelGGL(__VA_ARGS__);                             \
+        if (::pt::t_prof) ::pt::t_prof->stop(STREAM);                \
+    } while (0)
 
 constexpr int kMegaBlock = 256;
 // dynamic LDS a workgroup may use for traversal stacks + a staged scene copy
@@ -26,24 +56,29 @@ struct LaunchOpts {
 
 bool scene_fits_lds(const SceneView& sc);
 
-// Wavefront path state (SoA, HBM), `capacity` paths; see pt_wavefront.hip.
+// Wavefront path state (HBM), `capacity` entries per queue; see pt_wavefront.hip.  Every
+// path's state travels with its ray: queue entry i holds the ray AND the path state, and
+// a shade kernel writes the surviving path to its compacted slot of the other queue, so no
+// kernel gathers by path index.  Iterations alternate extension / shadow queues.
 enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_CTL_WORDS = 64 };
+struct WfQueue {
+    float4* q0;  // (o.xyz, d.x)
+    float4* q1;  // (d.y, d.z, path index bits, depth | spec << 16)
+    float4* q2;  // (L.xyz, seed bits)
+    float4* q3;  // (beta.xyz, -)
+};
 struct WfBuffers {
-    // ray queues (dense, compacted each iteration; ping-pong): entry i = 2 float4
-    // (o.xyz, d.x), (d.y, d.z, path index bits, 0)
-    float4* rq0;
-    float4* rq1;
+    WfQueue ext;   // extension rays (queue 0)
+    WfQueue shd;   // shadow rays (queue 1) ...
+    float4* sp0;   // ... and their shading points: (hp.xyz, material id)
+    float4* sp1;   // (hn.xyz, wi.x)
+    float2* sp2;   // (wi.y, wi.z)
     int2* hitq;    // per queue entry: (leaf record, t bits)
-    float4* st0;   // per path: (L.xyz, beta.x)
-    float4* st1;   // per path: (beta.y, beta.z, seed bits, depth | spec << 16)
-    float4* sp0;   // per path: (shading point, material id)
-    float4* sp1;   // per path: (normal, -)
-    float4* sp2;   // per path: (incoming direction, -)
     float* rad;    // per path: radiance when it ended [capacity][3]
     uint32_t* ctl; // queue counts
     uint32_t capacity;
 };
-constexpr size_t kWfBytesPerPath = 32 * 2 + 8 + 16 * 5 + 12;
+constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

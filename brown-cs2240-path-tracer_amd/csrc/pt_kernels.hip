@@ -176,7 +176,7 @@ static void launch_regen_t(const SceneView& sc, const FrameParams& fp, uint32_t 
                            float* out, Counters* cnt, hipStream_t stream) {
     dim3 grid((fp.width + 15) / 16, (fp.height + 15) / 16), block(kMegaBlock);
     size_t lds = (size_t)sc.max_stack * kMegaBlock * 4 + (LDS ? sc.span_bytes : 0);
-    hipLaunchKernelGGL((k_regen<LDS, TRAV, ACCUM, COUNT>), grid, block, lds, stream, sc, fp, frame0, nframes, stride, out,
+    PT_LAUNCH(KID_REGEN, stream, (k_regen<LDS, TRAV, ACCUM, COUNT>), grid, block, lds, stream, sc, fp, frame0, nframes, stride, out,
                        cnt);
 }
 
@@ -198,7 +198,7 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
     if (!accum) { nframes = 1; stride = 1; }
     if (lo.literal) {
         dim3 grid((fp.width + 15) / 16, (fp.height + 15) / 16), block(kMegaBlock);
-#define LIT(A, C) hipLaunchKernelGGL((k_mega<A, C>), grid, block, 0, stream, sc, fp, frame0, nframes, stride, out, cnt)
+#define LIT(A, C) PT_LAUNCH(KID_MEGA, stream, (k_mega<A, C>), grid, block, 0, stream, sc, fp, frame0, nframes, stride, out, cnt)
         if (accum) { if (count) LIT(true, true); else LIT(true, false); }
         else { if (count) LIT(false, true); else LIT(false, false); }
 #undef LIT

@@ -1,16 +1,20 @@
 // pt_wavefront.hip — wavefront path tracer for gfx950 (the north-star design).
 //
-// A batch of P = F*W*H paths (F frames of the image) lives in HBM as SoA float4 arrays
-// indexed by path; the rays still to be traced live in a DENSE queue (32 B per ray, the
-// path index in the record) that is compacted every iteration.  Each iteration runs:
+// A batch of P = F*W*H paths (F frames of the image) lives in HBM as DENSE queues of
+// entries that carry the ray AND the path state (WfQueue, pt_kernels.h: 64 B per entry,
+// +40 B of shading point in the shadow queue).  Survivors are compacted into the other
+// queue every iteration, so every kernel streams its queue coalesced and nothing is
+// gathered by path index (the radiance of a finished path is the only scatter).  Each
+// iteration runs:
 //   k_wf_trace   closest-hit traversal of the queue.  Persistent waves, each owning a
-//                contiguous chunk of the queue (no atomics); every lane keeps one ray in
-//                flight and one prefetched, and swaps in the next ray the moment its
-//                traversal ends, so lanes never idle behind a long traversal and a refill
-//                never waits on memory.  Traversal is the flattened, ballot-scheduled
-//                trav_step (per-lane stack in LDS, scene in LDS when it fits).
+//                contiguous chunk of the queue (no atomics).  Rays arrive in LDS windows of
+//                32 records (the next window in flight in registers) and hits leave through
+//                an LDS ring written back one coalesced window at a time, so the traversal
+//                loop issues no global memory operation; a lane takes its next ray the
+//                moment its traversal ends.  Traversal is trav_step_lean (per-lane stack in
+//                LDS, scene in LDS when it fits).
 //   k_wf_shade   the path logic after that traversal (path_after_ext / path_after_shadow,
-//                pt_path.h) and compaction of the surviving rays into the next queue with
+//                pt_path.h) and compaction of the surviving paths into the next queue with
 //                __ballot + mbcnt (one atomicAdd per wave).
 // All paths of a batch start together, so a queue holds only extension rays or only
 // shadow rays and the two alternate.  k_wf_generate writes the camera rays; k_wf_accum adds
@@ -30,9 +34,12 @@ __device__ __forceinline__ uint32_t rank_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ void store_ray(float4* q, uint32_t i, const Ray& r, uint32_t p) {
-    q[2 * (size_t)i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    q[2 * (size_t)i + 1] = make_float4(r.d.y, r.d.z, __builtin_bit_cast(float, p), 0.0f);
+__device__ __forceinline__ uint32_t pack_dspec(const PathState& ps) {
+    return (uint32_t)ps.depth | (ps.spec ? 0x10000u : 0u);
+}
+__device__ __forceinline__ void unpack_dspec(uint32_t dw, PathState& ps) {
+    ps.depth = (int)(dw & 0xffffu);
+    ps.spec = (dw & 0x10000u) != 0;
 }
 __device__ __forceinline__ Ray unpack_ray(float4 a, float4 b, uint32_t& p) {
     Ray r;
@@ -42,31 +49,33 @@ __device__ __forceinline__ Ray unpack_ray(float4 a, float4 b, uint32_t& p) {
     p = __builtin_bit_cast(uint32_t, b.z);
     return r;
 }
-__device__ __forceinline__ void store_state(const WfBuffers& wb, uint32_t p, const PathState& ps) {
-    wb.st0[p] = make_float4(ps.L.x, ps.L.y, ps.L.z, ps.beta.x);
-    wb.st1[p] = make_float4(ps.beta.y, ps.beta.z, __builtin_bit_cast(float, ps.seed),
-                            __builtin_bit_cast(float, (uint32_t)ps.depth | (ps.spec ? 0x10000u : 0u)));
+// queue entry i <- (ray, path index, path state)
+__device__ __forceinline__ void store_entry(const WfQueue& Q, uint32_t i, const Ray& r, uint32_t p, const PathState& ps) {
+    Q.q0[i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    Q.q1[i] = make_float4(r.d.y, r.d.z, __builtin_bit_cast(float, p), __builtin_bit_cast(float, pack_dspec(ps)));
+    Q.q2[i] = make_float4(ps.L.x, ps.L.y, ps.L.z, __builtin_bit_cast(float, ps.seed));
+    Q.q3[i] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
 }
-__device__ __forceinline__ void load_state(const WfBuffers& wb, uint32_t p, PathState& ps) {
-    float4 a = wb.st0[p], b = wb.st1[p];
-    ps.L = mk(a.x, a.y, a.z);
-    ps.beta = mk(a.w, b.x, b.y);
-    ps.seed = __builtin_bit_cast(uint32_t, b.z);
-    const uint32_t dw = __builtin_bit_cast(uint32_t, b.w);
-    ps.depth = (int)(dw & 0xffffu);
-    ps.spec = (dw & 0x10000u) != 0;
+__device__ __forceinline__ Ray load_entry(const WfQueue& Q, uint32_t i, uint32_t& p, PathState& ps) {
+    const float4 a = Q.q0[i], b = Q.q1[i], c = Q.q2[i], d = Q.q3[i];
+    unpack_dspec(__builtin_bit_cast(uint32_t, b.w), ps);
+    ps.L = mk(c.x, c.y, c.z);
+    ps.seed = __builtin_bit_cast(uint32_t, c.w);
+    ps.beta = mk(d.x, d.y, d.z);
+    return unpack_ray(a, b, p);
 }
-__device__ __forceinline__ void store_shading_point(const WfBuffers& wb, uint32_t p, const PathState& ps) {
-    wb.sp0[p] = make_float4(ps.hp.x, ps.hp.y, ps.hp.z, __builtin_bit_cast(float, ps.mat_id));
-    wb.sp1[p] = make_float4(ps.hn.x, ps.hn.y, ps.hn.z, 0.0f);
-    wb.sp2[p] = make_float4(ps.wi.x, ps.wi.y, ps.wi.z, 0.0f);
+__device__ __forceinline__ void store_shading_point(const WfBuffers& wb, uint32_t i, const PathState& ps) {
+    wb.sp0[i] = make_float4(ps.hp.x, ps.hp.y, ps.hp.z, __builtin_bit_cast(float, ps.mat_id));
+    wb.sp1[i] = make_float4(ps.hn.x, ps.hn.y, ps.hn.z, ps.wi.x);
+    wb.sp2[i] = make_float2(ps.wi.y, ps.wi.z);
 }
-__device__ __forceinline__ void load_shading_point(const WfBuffers& wb, uint32_t p, PathState& ps) {
-    float4 a = wb.sp0[p], b = wb.sp1[p], c = wb.sp2[p];
+__device__ __forceinline__ void load_shading_point(const WfBuffers& wb, uint32_t i, PathState& ps) {
+    const float4 a = wb.sp0[i], b = wb.sp1[i];
+    const float2 c = wb.sp2[i];
     ps.hp = mk(a.x, a.y, a.z);
     ps.mat_id = __builtin_bit_cast(int, a.w);
     ps.hn = mk(b.x, b.y, b.z);
-    ps.wi = mk(c.x, c.y, c.z);
+    ps.wi = mk(b.w, c.x, c.y);
 }
 
 // pixel of path p (row-major within its frame)
@@ -92,8 +101,7 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
         const uint32_t t = raw_salt ? frame0 : (uint32_t)(float)(frame0 + (fbase + f) * stride);
         PathState ps;
         Ray r = path_begin(fp, x, y, t, ps);
-        store_ray(wb.rq0, p, r, p);
-        store_state(wb, p, ps);
+        store_entry(wb.ext, p, r, p, ps);
         if (COUNT) { c.samples++; c.ext_queries++; }
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -123,17 +131,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     const uint32_t begin = min(w * per, count), end = min(begin + per, count);
     if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * kStageBytes);
     if (begin >= end) return;  // wave-uniform
-    const float4* q = in_q ? wb.rq1 : wb.rq0;
+    // lanes 0..31 load the first halves (q0) of a window's records, lanes 32..63 the second (q1)
     const uint32_t lane = lane_id();
+    const float4* qh = (lane < kWinRays) ? (in_q ? wb.shd.q0 : wb.ext.q0) : (in_q ? wb.shd.q1 : wb.ext.q1);
     Counters c = {};
     // window [ws, we) sits in LDS; the following window [ns, ne) is in flight in registers
     uint32_t ws = begin, we = min(begin + kWinRays, end);
-    // lanes 0..31 carry the rays of a window, lanes 32..63 the second halves of each record
     const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
-    if (ws + wl < we) wray[2 * wl + half] = q[2 * (size_t)(ws + wl) + half];
+    if (ws + wl < we) wray[2 * wl + half] = qh[ws + wl];
     uint32_t ns = we, ne = min(we + kWinRays, end);
     float4 na = make_float4(0, 0, 0, 0);
-    if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
+    if (ns + wl < ne) na = qh[ns + wl];
     uint32_t cur = ws;      // next queue entry to hand out
     uint32_t flushed = ws;  // entries below this are in wb.hitq
     uint32_t idx = 0, p = 0;
@@ -149,7 +157,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
             if (cur == we && ne - flushed <= kHitRing) {  // next window, if the hit ring has room
                 if (ns + wl < ne) wray[2 * wl + half] = na;
                 ws = ns; we = ne; ns = we; ne = min(we + kWinRays, end);
-                if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
+                if (ns + wl < ne) na = qh[ns + wl];
             }
             if (cur < we) {
                 const uint32_t j = cur + rank_below(need);
@@ -180,50 +188,67 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     if (COUNT) flush_counters(c, cnt_out);
 }
 
+// Shade blocks are 1024 threads so that compaction takes one atomicAdd per 1024 entries: all
+// atomics on the queue counter serialise at one memory channel, and one per wave (131k per
+// 8M-path batch) cost more than the shading itself.
+constexpr uint32_t kShadeBlock = 1024;
+
 template <bool EXT, bool COUNT>
-__global__ __launch_bounds__(256) void k_wf_shade(SceneView sc, FrameParams fp, WfBuffers wb, int in_q,
-                                                  Counters* cnt_out) {
-    const uint32_t count = wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
+__global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneView sc, FrameParams fp, WfBuffers wb, Counters* cnt_out) {
+    // EXT: extension queue -> shadow queue; else shadow queue -> extension queue
+    const uint32_t count = wb.ctl[EXT ? WF_COUNT0 : WF_COUNT1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x * blockDim.x >= count) return;  // whole block past the queue
-    const float4* q = in_q ? wb.rq1 : wb.rq0;
-    float4* out_q = in_q ? wb.rq0 : wb.rq1;
-    uint32_t* out_count = &wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1];
+    const WfQueue& in = EXT ? wb.ext : wb.shd;
+    const WfQueue& out = EXT ? wb.shd : wb.ext;
+    uint32_t* out_count = &wb.ctl[EXT ? WF_COUNT1 : WF_COUNT0];
     Counters c = {};
     bool more = false;
     uint32_t p = 0;
     Ray r;
+    PathState ps;
     if (i < count) {
-        r = unpack_ray(q[2 * (size_t)i], q[2 * (size_t)i + 1], p);
+        r = load_entry(in, i, p, ps);
         const int2 h = wb.hitq[i];
         const float t = __builtin_bit_cast(float, h.y);
-        PathState ps;
-        load_state(wb, p, ps);
         if (EXT) {
             more = path_after_ext(sc, h.x, t, r, ps);
-            if (more) {
-                store_shading_point(wb, p, ps);
-                if (COUNT) c.shadow_queries++;
-            }
+            if (more && COUNT) c.shadow_queries++;
         } else {
-            load_shading_point(wb, p, ps);
+            load_shading_point(wb, i, ps);
             more = path_after_shadow(sc, fp, h.x, t, r, ps);
             if (more && COUNT) c.ext_queries++;
         }
-        store_state(wb, p, ps);
         if (!more) {
             float* o = wb.rad + 3 * (size_t)p;
             o[0] = ps.L.x; o[1] = ps.L.y; o[2] = ps.L.z;
         }
     }
-    // compaction of the surviving rays: one atomic per wave, lane offsets from mbcnt
+    // compaction of the surviving paths: wave counts -> LDS prefix -> one atomicAdd per block
+    __shared__ uint32_t s_cnt[kShadeBlock / 64];
     const uint64_t keep = __ballot(more);
-    if (keep) {
+    const uint32_t wv = threadIdx.x / 64;
+    if (lane_id() == 0) s_cnt[wv] = (uint32_t)__popcll(keep);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t n = threadIdx.x < kShadeBlock / 64 ? s_cnt[threadIdx.x] : 0u;
+        uint32_t incl = n;  // inclusive scan of the wave counts
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(incl, off, 64);
+            if (lane_id() >= (uint32_t)off) incl += v;
+        }
+        const uint32_t total = __shfl(incl, 63, 64);
         uint32_t base = 0;
-        const uint32_t leader = (uint32_t)__builtin_ctzll(keep);
-        if (lane_id() == leader) base = atomicAdd(out_count, (uint32_t)__popcll(keep));
-        base = __shfl(base, (int)leader, 64);
-        if (more) store_ray(out_q, base + rank_below(keep), r, p);
+        if (threadIdx.x == 0 && total) base = atomicAdd(out_count, total);
+        base = __shfl(base, 0, 64);
+        if (threadIdx.x < kShadeBlock / 64) s_cnt[threadIdx.x] = base + incl - n;
+    }
+    __syncthreads();
+    if (more) {
+        const uint32_t j = s_cnt[wv] + rank_below(keep);
+        store_entry(out, j, r, p, ps);
+        if (EXT) store_shading_point(wb, j, ps);
     }
     if (COUNT) flush_counters(c, cnt_out);
 }
@@ -275,19 +300,19 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         const uint32_t P = Fb * npix;
-        const int sblocks = (int)((P + 255) / 256);
-        hipLaunchKernelGGL((k_wf_generate<COUNT>), dim3((P + 255) / 256), dim3(256), 0, stream, fp, wb, frame0, stride, fb,
+        const int sblocks = (int)((P + kShadeBlock - 1) / kShadeBlock);
+        PT_LAUNCH(KID_WF_GENERATE, stream, (k_wf_generate<COUNT>), dim3((P + 255) / 256), dim3(256), 0, stream, fp, wb, frame0, stride, fb,
                            P, !accum, cnt);
         int in_q = 0;
         for (int it = 0; it < iters; ++it) {
-            hipLaunchKernelGGL((k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, stream, sc, wb, in_q, cnt);
+            PT_LAUNCH(KID_WF_TRACE, stream, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, stream, sc, wb, in_q, cnt);
             if ((it & 1) == 0)
-                hipLaunchKernelGGL((k_wf_shade<true, COUNT>), dim3(sblocks), dim3(256), 0, stream, sc, fp, wb, in_q, cnt);
+                PT_LAUNCH(KID_WF_SHADE_EXT, stream, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, stream, sc, fp, wb, cnt);
             else
-                hipLaunchKernelGGL((k_wf_shade<false, COUNT>), dim3(sblocks), dim3(256), 0, stream, sc, fp, wb, in_q, cnt);
+                PT_LAUNCH(KID_WF_SHADE_SHADOW, stream, (k_wf_shade<false, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, stream, sc, fp, wb, cnt);
             in_q ^= 1;
         }
-        hipLaunchKernelGGL(k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix, Fb, accum);
+        PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix, Fb, accum);
     }
     return hipGetLastError();
 }

@@ -40,6 +40,11 @@ class SceneInfo(ctypes.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
+class KernelTime(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_uint64), ("total_ms", ctypes.c_double),
+                ("min_ms", ctypes.c_double), ("max_ms", ctypes.c_double)]
+
+
 _lib = None
 
 
@@ -84,8 +89,10 @@ def load_library():
     L.pt_frame_async.argtypes = [p, p, u32, i, p, p]
     L.pt_tonemap.argtypes = [p, sz, u32, p]
     L.pt_selftest_math.argtypes = [i, i, p, p, p, sz]
+    L.pt_profile_enable.argtypes = [p, i]
+    L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math"):
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read"):
         getattr(L, fn).restype = i
     _lib = L
     return L
@@ -171,6 +178,21 @@ class Scene:
         _check(self._lib.pt_render_async(self._h, _ptr(meta), frame0, nframes, stride, max_depth, mode,
                                          ctypes.c_void_p(d_accum_ptr), ctypes.c_void_p(d_counters_ptr or None),
                                          ctypes.c_void_p(stream_ptr or None)))
+
+    def profile_enable(self, enable: bool = True):
+        """Bracket every kernel launch of this scene with HIP events (discards earlier records)."""
+        _check(self._lib.pt_profile_enable(self._h, 1 if enable else 0))
+
+    def profile_read(self) -> dict:
+        """{kernel name: {"launches", "total_ms", "avg_ms", "min_ms", "max_ms"}} since profile_enable()."""
+        buf = (KernelTime * 16)()
+        n = ctypes.c_int(0)
+        _check(self._lib.pt_profile_read(self._h, buf, 16, ctypes.byref(n)))
+        out = {}
+        for k in buf[: n.value]:
+            out[k.name.decode()] = {"launches": int(k.launches), "total_ms": k.total_ms,
+                                    "avg_ms": k.total_ms / max(1, k.launches), "min_ms": k.min_ms, "max_ms": k.max_ms}
+        return out
 
     def frame(self, meta, t: int, max_depth: int = -1) -> np.ndarray:
         """One reference dispatch: raw radiance [H, W, 3] for RNG salt t."""

@@ -43,7 +43,7 @@ typedef enum {
 } pt_status;
 
 typedef enum {
-    PT_MODE_AUTO = 0,       /* library picks the fastest path for the scene */
+    PT_MODE_AUTO = 0,       /* wavefront when a call has >= 2^20 paths (W*H*nframes), else megakernel */
     PT_MODE_MEGAKERNEL = 1, /* one lane per pixel, frames looped in-lane */
     PT_MODE_WAVEFRONT = 2   /* SoA path/ray queues, per-bounce kernels, wave64 compaction */
 } pt_mode;
@@ -72,6 +72,15 @@ typedef struct {
 } pt_scene_info;
 
 typedef struct pt_scene pt_scene;
+
+/* Per-kernel launch timing (pt_profile_read). */
+typedef struct {
+    char name[32];     /* "k_regen", "k_wf_trace", "k_wf_shade_ext", ... */
+    uint64_t launches;
+    double total_ms;   /* sum over launches of the HIP-event time around each launch */
+    double min_ms;
+    double max_ms;
+} pt_kernel_time;
 
 /* ABI version of the loaded library (== PT_ABI_VERSION when headers match). */
 int pt_abi_version(void);
@@ -112,6 +121,14 @@ int pt_frame_async(pt_scene* scene, const float meta[48], uint32_t t, int max_de
  * raw = acc/sample_runs, lum = mean(raw), out = raw * (lum/(lum+1))^0.01, u8 = ToInt32(out*255)
  * clamped; rgba[i*4+3] = 255. */
 int pt_tonemap(const float* accum, size_t npix, uint32_t sample_runs, uint8_t* rgba_out);
+
+/* Kernel timing (no counterpart in the reference, which has no GPU timing): while enabled,
+ * every kernel the scene launches is bracketed by two HIP events on the launch stream (no
+ * synchronisation, a few microseconds per launch).  enable != 0 also discards earlier
+ * records.  pt_profile_read waits for the recorded events and writes per-kernel totals
+ * (at most max_entries; *n_out = entries written). */
+int pt_profile_enable(pt_scene* scene, int enable);
+int pt_profile_read(pt_scene* scene, pt_kernel_time* out, int max_entries, int* n_out);
 
 /* Numerics self-test: out[i] = f(a[i], b[i]) evaluated ON THE DEVICE with the core's
  * pinned f32 math (fn ids: 0 sin, 1 cos, 2 tan, 3 acos, 4 log2, 5 exp2, 6 pow, 7 sqrt,

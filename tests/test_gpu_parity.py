@@ -204,3 +204,59 @@ def test_invalid_scene_rejected():
     with pytest.raises(pt_amd.PtError) as e:
         pt_amd.Scene(tri, bvh)
     assert e.value.code == -2
+
+
+# ---------------------------------------------------------------------------------------------
+# kernel timing (pt_profile_*) and the AUTO policy (megakernel below 2^20 paths per call)
+# ---------------------------------------------------------------------------------------------
+def test_profile_records_every_launch(packed, monkeypatch):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+        monkeypatch.delenv(k, raising=False)
+    p = packed["CornellBox"]
+    meta = p.meta_for(64, 64)
+    depth = 8
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        s.render(meta, 0, 4, 1, depth, pt_amd.MODE_MEGAKERNEL)
+        mega = s.profile_read()
+        s.profile_enable(True)
+        s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
+        wf = s.profile_read()
+        s.profile_enable(False)
+        s.render(meta, 0, 1, 1, depth, pt_amd.MODE_WAVEFRONT)
+        assert s.profile_read() == {}
+    assert set(mega) == {"k_regen"} and mega["k_regen"]["launches"] == 1
+    assert set(wf) == {"k_wf_generate", "k_wf_trace", "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum"}
+    assert wf["k_wf_trace"]["launches"] == 2 * (depth + 1)  # one batch: 4 frames of 64^2 fit
+    assert wf["k_wf_shade_ext"]["launches"] == wf["k_wf_shade_shadow"]["launches"] == depth + 1
+    for v in list(mega.values()) + list(wf.values()):
+        assert 0.0 < v["min_ms"] <= v["avg_ms"] <= v["max_ms"] and v["total_ms"] > 0.0
+
+
+def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+        monkeypatch.delenv(k, raising=False)
+    p = packed["CornellBox"]
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        s.render(p.meta_for(64, 64), 0, 2, 1, 2, pt_amd.MODE_AUTO)
+        small = s.profile_read()
+        s.profile_enable(True)
+        s.render(p.meta_for(512, 512), 0, 4, 1, 2, pt_amd.MODE_AUTO)  # 2^20 paths
+        large = s.profile_read()
+        s.profile_enable(False)
+    assert "k_regen" in small and "k_wf_trace" not in small
+    assert "k_wf_trace" in large and "k_regen" not in large
+
+
+def test_auto_large_render_matches_megakernel(packed, monkeypatch):
+    """At the AUTO switch point the wavefront result equals the megakernel's bit for bit
+    (both equal the oracle on the smaller cases above)."""
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+        monkeypatch.delenv(k, raising=False)
+    p = packed["CornellBox"]
+    meta = p.meta_for(512, 512)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        a = s.render(meta, 0, 4, 1, 8, pt_amd.MODE_AUTO)
+        m = s.render(meta, 0, 4, 1, 8, pt_amd.MODE_MEGAKERNEL)
+    assert same_bits(a, m), mismatch_report(a, m)
