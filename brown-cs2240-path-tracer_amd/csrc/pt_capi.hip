@@ -387,7 +387,7 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 }
 
 // PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
-// PT_TRAV=nested|flat1|pred|lean.
+// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8.
 // AUTO picks the wavefront pipeline once a call has this many paths: below it the fixed
 // cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.
 constexpr uint64_t kWfAutoMinPaths = 1ull << 20;
@@ -401,7 +401,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
         if (!std::strcmp(e, "mega") || lo.literal) lo.wavefront = false;
     }
     if (const char* e = std::getenv("PT_LDS")) lo.lds = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : 3;
+    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : -1;
     return lo;
 }
 
@@ -415,16 +415,16 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     const size_t n = paths;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
-    size_t oq[8];
-    for (auto& o : oq) o = take(16 * n);
+    size_t oq[6];
+    for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * n);
     const size_t o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(8 * n), o_hit = take(8 * n),
                  o_rad = take(12 * n), o_ctl = take(4 * WF_CTL_WORDS);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
     char* b = static_cast<char*>(s->d_wf);
     auto f4 = [&](size_t o) { return reinterpret_cast<float4*>(b + o); };
     WfBuffers& w = s->wf;
-    w.ext = WfQueue{f4(oq[0]), f4(oq[1]), f4(oq[2]), f4(oq[3])};
-    w.shd = WfQueue{f4(oq[4]), f4(oq[5]), f4(oq[6]), f4(oq[7])};
+    w.ext = WfQueue{f4(oq[0]), f4(oq[1]), f4(oq[2])};
+    w.shd = WfQueue{f4(oq[3]), f4(oq[4]), f4(oq[5])};
     w.sp0 = f4(o_p0); w.sp1 = f4(o_p1);
     w.sp2 = reinterpret_cast<float2*>(b + o_p2);
     w.hitq = reinterpret_cast<int2*>(b + o_hit);

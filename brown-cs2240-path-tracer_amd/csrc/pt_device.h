@@ -276,7 +276,10 @@ __device__ __forceinline__ void trav_init(TravLean& s, bool active) {
 __device__ __forceinline__ bool trav_finished(const TravLean& s) { return (s.fl & TF_DONE) != 0; }
 __device__ __forceinline__ bool trav_finished(const TravState& s) { return s.done; }
 
-template <bool COUNT>
+// K = triangle tests per leaf turn: a lane with at least two triangles of its leaf pair left
+// runs two in sequence (same order, each against the closest t so far), which halves the
+// per-iteration overhead (scheduling ballots, decision, loop control) per test.
+template <int K, bool COUNT>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
                                                int stride, Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE);
@@ -286,13 +289,18 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     bool decide = false;
     if (__popcll(want_leaf) >= __popcll(want_node)) {  // wave-uniform
         if (state == TF_LEAF) {
-            const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
-            float t;
-            const bool take = tri_hit(sc.tris, idx, r, t) & ((s.best_t < 0.0f) | (t < s.best_t));
-            s.best_t = take ? t : s.best_t;
-            s.best = take ? idx : s.best;
-            if (COUNT) cnt.tri_tests++;
-            s.k += 1;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const bool live = j == 0 || s.k < s.nt;  // the first test always is
+                const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+                float t;
+                const bool take = tri_hit(sc.tris, live ? idx : s.la, r, t) & live &
+                                  ((s.best_t < 0.0f) | (t < s.best_t));
+                s.best_t = take ? t : s.best_t;
+                s.best = take ? idx : s.best;
+                if (COUNT) cnt.tri_tests += live ? 1 : 0;
+                s.k += live ? 1 : 0;
+            }
             decide = s.k == s.nt;
             s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
         }
@@ -325,16 +333,26 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
 }
 
 // Traversal flavours (LaunchOpts.trav): 0 nested loops (trace), 1 flattened with per-lane
-// branches (trav_step), 2 flattened and predicated (trav_step_pred), 3 lean (trav_step_lean).
+// branches (trav_step), 2 flattened and predicated (trav_step_pred), 3 lean (trav_step_lean),
+// 4 lean with two triangle tests per leaf turn, 5 with four, 6 with eight.
 template <int TRAV>
 struct TravSel { using type = TravState; };
 template <>
 struct TravSel<3> { using type = TravLean; };
+template <>
+struct TravSel<4> { using type = TravLean; };
+template <>
+struct TravSel<5> { using type = TravLean; };
+template <>
+struct TravSel<6> { using type = TravLean; };
 
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
                                              int32_t* stack, int stride, Counters& cnt) {
-    if constexpr (TRAV == 3) return trav_step_lean<COUNT>(sc, r, s, stack, stride, cnt);
+    if constexpr (TRAV == 3) return trav_step_lean<1, COUNT>(sc, r, s, stack, stride, cnt);
+    else if constexpr (TRAV == 4) return trav_step_lean<2, COUNT>(sc, r, s, stack, stride, cnt);
+    else if constexpr (TRAV == 5) return trav_step_lean<4, COUNT>(sc, r, s, stack, stride, cnt);
+    else if constexpr (TRAV == 6) return trav_step_lean<8, COUNT>(sc, r, s, stack, stride, cnt);
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
     else return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);
 }

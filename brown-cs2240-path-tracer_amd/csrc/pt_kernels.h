@@ -51,7 +51,7 @@ struct LaunchOpts {
     bool wavefront = false;  // wavefront pipeline (pt_wavefront.hip)
     bool literal = false;  // k_mega: the reference's control flow
     bool lds = true;       // stage the scene in LDS when it fits
-    int trav = 3;          // traversal: 0 nested loops, 1 flattened (trav_step), 2 flattened+predicated, 3 lean
+    int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -62,10 +62,9 @@ bool scene_fits_lds(const SceneView& sc);
 // kernel gathers by path index.  Iterations alternate extension / shadow queues.
 enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_CTL_WORDS = 64 };
 struct WfQueue {
-    float4* q0;  // (o.xyz, d.x)
-    float4* q1;  // (d.y, d.z, path index bits, depth | spec << 16)
-    float4* q2;  // (L.xyz, seed bits)
-    float4* q3;  // (beta.xyz, -)
+    float4* ray;  // [i][2]: (o.xyz, d.x), (d.y, d.z, path index bits, depth | spec << 16)
+    float4* q2;   // (L.xyz, seed bits)
+    float4* q3;   // (beta.xyz, -)
 };
 struct WfBuffers {
     WfQueue ext;   // extension rays (queue 0)

@@ -205,11 +205,14 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
         return hipGetLastError();
     }
     const bool lds = lo.lds && scene_fits_lds(sc);
+    // lean by default: the megakernel keeps the path state live across traversal, so the
+    // multi-test leaf turns (lean2+) cost it occupancy (measured slower)
+    const int trav = lo.trav < 0 ? 3 : lo.trav;
 #define RA(L, T) launch_regen_a<L, T>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream)
     if (lds) {
-        if (lo.trav == 0) RA(true, 0); else if (lo.trav == 1) RA(true, 1); else if (lo.trav == 3) RA(true, 3); else RA(true, 2);
+        if (trav == 0) RA(true, 0); else if (trav == 1) RA(true, 1); else if (trav == 3) RA(true, 3); else if (trav >= 4) RA(true, 4); else RA(true, 2);
     } else {
-        if (lo.trav == 0) RA(false, 0); else if (lo.trav == 1) RA(false, 1); else if (lo.trav == 3) RA(false, 3); else RA(false, 2);
+        if (trav == 0) RA(false, 0); else if (trav == 1) RA(false, 1); else if (trav == 3) RA(false, 3); else if (trav >= 4) RA(false, 4); else RA(false, 2);
     }
 #undef RA
     return hipGetLastError();

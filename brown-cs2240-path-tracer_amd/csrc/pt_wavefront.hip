@@ -51,13 +51,13 @@ __device__ __forceinline__ Ray unpack_ray(float4 a, float4 b, uint32_t& p) {
 }
 // queue entry i <- (ray, path index, path state)
 __device__ __forceinline__ void store_entry(const WfQueue& Q, uint32_t i, const Ray& r, uint32_t p, const PathState& ps) {
-    Q.q0[i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
-    Q.q1[i] = make_float4(r.d.y, r.d.z, __builtin_bit_cast(float, p), __builtin_bit_cast(float, pack_dspec(ps)));
+    Q.ray[2 * (size_t)i] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+    Q.ray[2 * (size_t)i + 1] = make_float4(r.d.y, r.d.z, __builtin_bit_cast(float, p), __builtin_bit_cast(float, pack_dspec(ps)));
     Q.q2[i] = make_float4(ps.L.x, ps.L.y, ps.L.z, __builtin_bit_cast(float, ps.seed));
     Q.q3[i] = make_float4(ps.beta.x, ps.beta.y, ps.beta.z, 0.0f);
 }
 __device__ __forceinline__ Ray load_entry(const WfQueue& Q, uint32_t i, uint32_t& p, PathState& ps) {
-    const float4 a = Q.q0[i], b = Q.q1[i], c = Q.q2[i], d = Q.q3[i];
+    const float4 a = Q.ray[2 * (size_t)i], b = Q.ray[2 * (size_t)i + 1], c = Q.q2[i], d = Q.q3[i];
     unpack_dspec(__builtin_bit_cast(uint32_t, b.w), ps);
     ps.L = mk(c.x, c.y, c.z);
     ps.seed = __builtin_bit_cast(uint32_t, c.w);
@@ -117,7 +117,7 @@ constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8;
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 
 template <bool LDS, int TRAV, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(TRAV == 6 ? 5 : (TRAV >= 4 ? 6 : 1), 8))) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
@@ -131,17 +131,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     const uint32_t begin = min(w * per, count), end = min(begin + per, count);
     if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * kStageBytes);
     if (begin >= end) return;  // wave-uniform
-    // lanes 0..31 load the first halves (q0) of a window's records, lanes 32..63 the second (q1)
+    // lanes 0..31 load the first halves of a window's ray records, lanes 32..63 the second
     const uint32_t lane = lane_id();
-    const float4* qh = (lane < kWinRays) ? (in_q ? wb.shd.q0 : wb.ext.q0) : (in_q ? wb.shd.q1 : wb.ext.q1);
+    const float4* q = in_q ? wb.shd.ray : wb.ext.ray;
     Counters c = {};
     // window [ws, we) sits in LDS; the following window [ns, ne) is in flight in registers
     uint32_t ws = begin, we = min(begin + kWinRays, end);
     const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
-    if (ws + wl < we) wray[2 * wl + half] = qh[ws + wl];
+    if (ws + wl < we) wray[2 * wl + half] = q[2 * (size_t)(ws + wl) + half];
     uint32_t ns = we, ne = min(we + kWinRays, end);
     float4 na = make_float4(0, 0, 0, 0);
-    if (ns + wl < ne) na = qh[ns + wl];
+    if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
     uint32_t cur = ws;      // next queue entry to hand out
     uint32_t flushed = ws;  // entries below this are in wb.hitq
     uint32_t idx = 0, p = 0;
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
             if (cur == we && ne - flushed <= kHitRing) {  // next window, if the hit ring has room
                 if (ns + wl < ne) wray[2 * wl + half] = na;
                 ws = ns; we = ne; ns = we; ne = min(we + kWinRays, end);
-                if (ns + wl < ne) na = qh[ns + wl];
+                if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
             }
             if (cur < we) {
                 const uint32_t j = cur + rank_below(need);
@@ -322,15 +322,22 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
                             Counters* cnt, hipStream_t stream) {
     if (!accum) { nframes = 1; stride = 1; }
     const bool lds = lo.lds && scene_fits_lds(sc);
-    const int trav = lo.trav == 0 ? 1 : lo.trav;  // the wavefront always uses a flattened traversal
+    // lean4 by default (measured best on gfx950); the wavefront always uses a flattened traversal
+    const int trav = lo.trav < 0 ? 5 : (lo.trav == 0 ? 1 : lo.trav);
 #define WF(L, T, C) return wf_render_t<L, T, C>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream)
     if (lds) {
         if (trav == 1) { if (count) WF(true, 1, true); else WF(true, 1, false); }
         if (trav == 3) { if (count) WF(true, 3, true); else WF(true, 3, false); }
+        if (trav == 4) { if (count) WF(true, 4, true); else WF(true, 4, false); }
+        if (trav == 5) { if (count) WF(true, 5, true); else WF(true, 5, false); }
+        if (trav == 6) { if (count) WF(true, 6, true); else WF(true, 6, false); }
         if (count) WF(true, 2, true); else WF(true, 2, false);
     }
     if (trav == 1) { if (count) WF(false, 1, true); else WF(false, 1, false); }
     if (trav == 3) { if (count) WF(false, 3, true); else WF(false, 3, false); }
+    if (trav == 4) { if (count) WF(false, 4, true); else WF(false, 4, false); }
+    if (trav == 5) { if (count) WF(false, 5, true); else WF(false, 5, false); }
+    if (trav == 6) { if (count) WF(false, 6, true); else WF(false, 6, false); }
     if (count) WF(false, 2, true); else WF(false, 2, false);
 #undef WF
 }

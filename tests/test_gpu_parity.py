@@ -28,6 +28,9 @@ KERNELS = {
     "wavefront_pred_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "pred"},
     "wavefront_lean_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean"},
     "wavefront_lean_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean", "PT_LDS": "0"},
+    "wavefront_lean2_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean2"},
+    "wavefront_lean4_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4"},
+    "mega_lean2_lds": {"PT_KERNEL": "mega", "PT_TRAV": "lean2"},
 }
 
 
