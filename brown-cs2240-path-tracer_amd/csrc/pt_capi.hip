@@ -55,6 +55,7 @@ struct HostLayout {
     std::vector<Light> lights;
     pt_scene_info info{};
     int32_t ntri = 0;
+    bool fast_rcp = false;  // SceneView::fast_rcp
 };
 
 // Re-encode packer.ts layouts into pt_layout.h.
@@ -151,6 +152,17 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
         L.nodes[(size_t)it.node] = nd;
     }
     L.info.nodes = (uint32_t)L.nodes.size();
+    // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
+    // a reflection/refraction of unit vectors; non-finite ones give no hit on either path)
+    double emax = 0.0;
+    bool finite = true;
+    for (const Tri& t : L.tris) {
+        const double a = std::sqrt((double)t.e1[0] * t.e1[0] + (double)t.e1[1] * t.e1[1] + (double)t.e1[2] * t.e1[2]);
+        const double b = std::sqrt((double)t.e2[0] * t.e2[0] + (double)t.e2[1] * t.e2[1] + (double)t.e2[2] * t.e2[2]);
+        finite = finite && std::isfinite(a) && std::isfinite(b);
+        emax = std::max(emax, a * b);
+    }
+    L.fast_rcp = finite && emax < std::ldexp(1.0, 124);
     // The device stack parks at most one left child per internal ancestor.
     L.info.max_stack = max_depth + 1;
     if (L.info.max_stack >= (uint32_t)kStackMax) return fail(PT_ERR_SCENE, "BVH deeper than the device traversal stack");
@@ -331,6 +343,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.f_ntri = (float)L.ntri;
     s->view.inv_ntri = 1.0f / (float)L.ntri;  // intersection-logic.wgsl:284
     s->view.max_stack = (int32_t)L.info.max_stack;
+    s->view.fast_rcp = L.fast_rcp ? 1 : 0;
     s->view.off_tris = (uint32_t)(o_tris - o_nodes);
     s->view.off_mats = (uint32_t)(o_mats - o_nodes);
     s->view.off_lights = (uint32_t)(o_lights - o_nodes);
@@ -387,7 +400,7 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 }
 
 // PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
-// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8.
+// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8, PT_FASTRCP=1.
 // AUTO picks the wavefront pipeline once a call has this many paths: below it the fixed
 // cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.
 constexpr uint64_t kWfAutoMinPaths = 1ull << 20;
@@ -401,6 +414,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
         if (!std::strcmp(e, "mega") || lo.literal) lo.wavefront = false;
     }
     if (const char* e = std::getenv("PT_LDS")) lo.lds = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("PT_FASTRCP")) lo.fast_rcp = std::strcmp(e, "1") == 0;
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : -1;
     return lo;
 }
@@ -561,6 +575,25 @@ int pt_selftest_math(int device, int fn, const float* a, const float* b, float* 
     if (e == hipSuccess) e = hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
     hipFree(da); hipFree(db); hipFree(dout);
     if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
+    return PT_OK;
+}
+
+int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
+                    uint32_t* failing_bits) {
+    if (!mismatches || steps < -1 || steps > 2 || lo_bits > hi_bits || hi_bits >= 0x80000000u)
+        return fail(PT_ERR_INVALID, "bad argument");
+    if (steps < 0) steps = kRcpSteps;
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 2 * sizeof(unsigned long long)));
+    unsigned long long h[2] = {0, 0};
+    hipError_t e = hipMemset(d, 0, sizeof(h));
+    if (e == hipSuccess) e = launch_selftest_rcp(steps, lo_bits, hi_bits, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
+    *mismatches = h[0];
+    if (failing_bits) *failing_bits = (uint32_t)h[1];
     return PT_OK;
 }
 

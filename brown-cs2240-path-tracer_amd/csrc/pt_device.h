@@ -179,6 +179,7 @@ __device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, Tra
 // Branch-free triangle test with the exact arithmetic of test_tri: every quantity of the
 // reference's early-out chain is computed and the chain becomes one predicate (the values
 // skipped by an early return never reach `hit`, so the result is identical).
+template <bool FAST_RCP = false>
 __device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, const Ray& r, float& t_out) {
     const float eps = 1e-8f;
     const float4* tp = reinterpret_cast<const float4*>(tris + i);
@@ -186,7 +187,9 @@ __device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, con
     f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
     f3 rce2 = cross(r.d, e2);
     float det = dot(e1, rce2);
-    float inv_det = 1.0f / det;
+    // FAST_RCP (SceneView::fast_rcp): |det| < 2^126 for this scene, where rcp_rn is the IEEE
+    // 1/det bit for bit; below 2^-126 the det test rejects the triangle whatever inv_det is
+    float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
     f3 s = r.o - v0;
     float u = inv_det * dot(s, rce2);
     f3 sce1 = cross(s, e1);
@@ -279,7 +282,7 @@ __device__ __forceinline__ bool trav_finished(const TravState& s) { return s.don
 // K = triangle tests per leaf turn: a lane with at least two triangles of its leaf pair left
 // runs two in sequence (same order, each against the closest t so far), which halves the
 // per-iteration overhead (scheduling ballots, decision, loop control) per test.
-template <int K, bool COUNT>
+template <int K, bool COUNT, bool FAST_RCP>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
                                                int stride, Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE);
@@ -294,7 +297,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
                 const bool live = j == 0 || s.k < s.nt;  // the first test always is
                 const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
                 float t;
-                const bool take = tri_hit(sc.tris, live ? idx : s.la, r, t) & live &
+                const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
                                   ((s.best_t < 0.0f) | (t < s.best_t));
                 s.best_t = take ? t : s.best_t;
                 s.best = take ? idx : s.best;
@@ -334,25 +337,21 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
 
 // Traversal flavours (LaunchOpts.trav): 0 nested loops (trace), 1 flattened with per-lane
 // branches (trav_step), 2 flattened and predicated (trav_step_pred), 3 lean (trav_step_lean),
-// 4 lean with two triangle tests per leaf turn, 5 with four, 6 with eight.
-template <int TRAV>
+// 4 lean with two triangle tests per leaf turn, 5 with four, 6 with eight; +10: the lean
+// flavours with 1/det from rcp_rn (scenes with SceneView::fast_rcp).
+template <int TRAV, bool LEAN = (TRAV >= 3)>
 struct TravSel { using type = TravState; };
-template <>
-struct TravSel<3> { using type = TravLean; };
-template <>
-struct TravSel<4> { using type = TravLean; };
-template <>
-struct TravSel<5> { using type = TravLean; };
-template <>
-struct TravSel<6> { using type = TravLean; };
+template <int TRAV>
+struct TravSel<TRAV, true> { using type = TravLean; };
 
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
                                              int32_t* stack, int stride, Counters& cnt) {
-    if constexpr (TRAV == 3) return trav_step_lean<1, COUNT>(sc, r, s, stack, stride, cnt);
-    else if constexpr (TRAV == 4) return trav_step_lean<2, COUNT>(sc, r, s, stack, stride, cnt);
-    else if constexpr (TRAV == 5) return trav_step_lean<4, COUNT>(sc, r, s, stack, stride, cnt);
-    else if constexpr (TRAV == 6) return trav_step_lean<8, COUNT>(sc, r, s, stack, stride, cnt);
+    if constexpr (TRAV >= 3) {  // TRAV + 10: the same with the fast reciprocal (SceneView::fast_rcp)
+        constexpr int B = TRAV % 10;
+        constexpr int K = B == 3 ? 1 : (B == 4 ? 2 : (B == 5 ? 4 : 8));
+        return trav_step_lean<K, COUNT, (TRAV >= 10)>(sc, r, s, stack, stride, cnt);
+    }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
     else return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);
 }

@@ -51,6 +51,7 @@ struct LaunchOpts {
     bool wavefront = false;  // wavefront pipeline (pt_wavefront.hip)
     bool literal = false;  // k_mega: the reference's control flow
     bool lds = true;       // stage the scene in LDS when it fits
+    bool fast_rcp = false; // rcp_rn for 1/det where SceneView::fast_rcp says it is exact (opt-in: measured no faster)
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 
@@ -89,6 +90,7 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
                              uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
                              hipStream_t stream);
 
+hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);
 
 }  // namespace pt

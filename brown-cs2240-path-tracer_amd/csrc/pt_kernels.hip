@@ -137,6 +137,29 @@ __global__ __launch_bounds__(kMegaBlock) void k_regen(SceneView sc, FrameParams 
     if (COUNT) flush_counters(c, cnt_out);
 }
 
+// Exhaustive check of rcp_rn against the IEEE division over every float x whose magnitude
+// bits lie in [lo, hi] (both signs): bad[0] += mismatches, bad[1] = some failing bit pattern.
+__global__ void k_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad) {
+    const uint64_t n = (uint64_t)(hi - lo + 1) * 2;
+    unsigned long long mis = 0, first = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t u = (lo + (uint32_t)(k >> 1)) | ((uint32_t)(k & 1) << 31);
+        const float x = __builtin_bit_cast(float, u);
+        const float want = 1.0f / x;
+        const float got = steps == 1 ? rcp_rn(x, 1) : (steps == 2 ? rcp_rn(x, 2) : rcp_rn(x, 0));
+        if (__builtin_bit_cast(uint32_t, got) != __builtin_bit_cast(uint32_t, want)) { ++mis; first = u; }
+    }
+    if (mis) {
+        atomicAdd(&bad[0], mis);
+        atomicExch(&bad[1], first);
+    }
+}
+
+hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream) {
+    hipLaunchKernelGGL(k_selftest_rcp, dim3(8192), dim3(256), 0, stream, steps, lo, hi, bad);
+    return hipGetLastError();
+}
+
 __global__ void k_selftest_math(int fn, const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ o,
                                 int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -207,13 +230,16 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
     const bool lds = lo.lds && scene_fits_lds(sc);
     // lean by default: the megakernel keeps the path state live across traversal, so the
     // multi-test leaf turns (lean2+) cost it occupancy (measured slower)
-    const int trav = lo.trav < 0 ? 3 : lo.trav;
+    const int trav0 = lo.trav < 0 ? 3 : std::min(lo.trav, 4);
+    const int trav = trav0 + ((trav0 >= 3 && lo.fast_rcp && sc.fast_rcp) ? 10 : 0);
 #define RA(L, T) launch_regen_a<L, T>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream)
+#define RA_T(L, T) else if (trav == T) RA(L, T);
     if (lds) {
-        if (trav == 0) RA(true, 0); else if (trav == 1) RA(true, 1); else if (trav == 3) RA(true, 3); else if (trav >= 4) RA(true, 4); else RA(true, 2);
+        if (trav == 0) RA(true, 0); RA_T(true, 1) RA_T(true, 2) RA_T(true, 3) RA_T(true, 4) RA_T(true, 13) RA_T(true, 14)
     } else {
-        if (trav == 0) RA(false, 0); else if (trav == 1) RA(false, 1); else if (trav == 3) RA(false, 3); else if (trav >= 4) RA(false, 4); else RA(false, 2);
+        if (trav == 0) RA(false, 0); RA_T(false, 1) RA_T(false, 2) RA_T(false, 3) RA_T(false, 4) RA_T(false, 13) RA_T(false, 14)
     }
+#undef RA_T
 #undef RA
     return hipGetLastError();
 }

@@ -70,7 +70,10 @@ struct SceneView {
     // byte offsets of each section from `nodes` (one contiguous device allocation), and
     // the span [nodes, end of lights) staged into LDS by kernels when it fits
     uint32_t off_tris, off_mats, off_lights, span_bytes;
-    int32_t pad[3];
+    // 1: every triangle has |e1|*|e2| < 2^124, so with unit ray directions |det| < 2^126 and
+    // the triangle test may take 1/det from rcp_rn (pt_math.h), bit-identical to the division
+    int32_t fast_rcp;
+    int32_t pad[2];
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

@@ -50,6 +50,22 @@ PT_HD f3 reflect(f3 wi, f3 n) {
     return f3{fmaf(k, n.x, wi.x), fmaf(k, n.y, wi.y), fmaf(k, n.z, wi.z)};
 }
 PT_HD f3 rcp3(f3 d) { return f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z}; }
+
+// Correctly rounded 1/x without the IEEE division sequence: the hardware reciprocal
+// (v_rcp_f32, about 1 ulp) refined by kRcpSteps Newton steps e = 1 - x*y, y += y*e, each an
+// exact-residual FMA pair.  Valid for 2^-126 <= |x| <= kRcpHi, where it equals 1.0f / x bit
+// for bit — verified on gfx950 over every float of that range (pt_selftest_rcp,
+// tests/test_gpu_parity.py); outside it the callers use the division.
+constexpr float kRcpHi = 0x1p125f;
+constexpr int kRcpSteps = 1;
+__device__ __forceinline__ float rcp_rn(float x, int steps = kRcpSteps) {
+    float y = __builtin_amdgcn_rcpf(x);
+    for (int i = 0; i < steps; ++i) {
+        const float e = fmaf(-x, y, 1.0f);
+        y = fmaf(e, y, y);
+    }
+    return y;
+}
 PT_HD float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 
 PT_HD float bits_f(uint32_t u) { return __builtin_bit_cast(float, u); }

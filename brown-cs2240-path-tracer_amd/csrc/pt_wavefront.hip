@@ -117,7 +117,7 @@ constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8;
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 
 template <bool LDS, int TRAV, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(TRAV == 6 ? 5 : (TRAV >= 4 ? 6 : 1), 8))) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(TRAV % 10 == 6 ? 5 : (TRAV % 10 >= 4 ? 6 : 1), 8))) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
@@ -325,20 +325,20 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
     // lean4 by default (measured best on gfx950); the wavefront always uses a flattened traversal
     const int trav = lo.trav < 0 ? 5 : (lo.trav == 0 ? 1 : lo.trav);
 #define WF(L, T, C) return wf_render_t<L, T, C>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream)
+#define WF_T(L, T) \
+    if (trav == T) { if (count) WF(L, T, true); else WF(L, T, false); }
+    const int t = trav + ((trav >= 3 && sc.fast_rcp) ? 10 : 0);
+    (void)t;
     if (lds) {
-        if (trav == 1) { if (count) WF(true, 1, true); else WF(true, 1, false); }
-        if (trav == 3) { if (count) WF(true, 3, true); else WF(true, 3, false); }
-        if (trav == 4) { if (count) WF(true, 4, true); else WF(true, 4, false); }
-        if (trav == 5) { if (count) WF(true, 5, true); else WF(true, 5, false); }
-        if (trav == 6) { if (count) WF(true, 6, true); else WF(true, 6, false); }
-        if (count) WF(true, 2, true); else WF(true, 2, false);
+        { const int trav = t; WF_T(true, 1) WF_T(true, 2) WF_T(true, 3) WF_T(true, 4) WF_T(true, 5) WF_T(true, 6)
+          WF_T(true, 13) WF_T(true, 14) WF_T(true, 15) WF_T(true, 16) }
+    } else {
+        const int trav = t;
+        WF_T(false, 1) WF_T(false, 2) WF_T(false, 3) WF_T(false, 4) WF_T(false, 5) WF_T(false, 6)
+        WF_T(false, 13) WF_T(false, 14) WF_T(false, 15) WF_T(false, 16)
     }
-    if (trav == 1) { if (count) WF(false, 1, true); else WF(false, 1, false); }
-    if (trav == 3) { if (count) WF(false, 3, true); else WF(false, 3, false); }
-    if (trav == 4) { if (count) WF(false, 4, true); else WF(false, 4, false); }
-    if (trav == 5) { if (count) WF(false, 5, true); else WF(false, 5, false); }
-    if (trav == 6) { if (count) WF(false, 6, true); else WF(false, 6, false); }
-    if (count) WF(false, 2, true); else WF(false, 2, false);
+    return hipErrorInvalidValue;
+#undef WF_T
 #undef WF
 }
 

@@ -23,6 +23,7 @@ from ._lib import (  # noqa: F401
     lib_path,
     load_library,
     selftest_math,
+    selftest_rcp,
     tonemap,
 )
 from .host import PackedScene, load_scene, program_entry  # noqa: F401

@@ -90,9 +90,10 @@ def load_library():
     L.pt_tonemap.argtypes = [p, sz, u32, p]
     L.pt_selftest_math.argtypes = [i, i, p, p, p, sz]
     L.pt_profile_enable.argtypes = [p, i]
+    L.pt_selftest_rcp.argtypes = [i, i, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read"):
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read", "pt_selftest_rcp"):
         getattr(L, fn).restype = i
     _lib = L
     return L
@@ -218,3 +219,13 @@ def selftest_math(fn: str, a, b=None, device: int = 0) -> np.ndarray:
     out = np.zeros_like(a)
     _check(load_library().pt_selftest_math(device, MATH_FNS.index(fn), _ptr(a), _ptr(b), _ptr(out), a.size))
     return out
+
+
+def selftest_rcp(steps: int = -1, lo_bits: int = 0x00800000, hi_bits: int = 0x7E000000, device: int = 0):
+    """(mismatches, failing input bits) of the core's reciprocal vs IEEE 1/x for every float whose
+    magnitude bits lie in [lo_bits, hi_bits] (default 2^-126..2^125), both signs."""
+    L = load_library()
+    m = ctypes.c_uint64(0)
+    b = ctypes.c_uint32(0)
+    _check(L.pt_selftest_rcp(device, steps, lo_bits, hi_bits, ctypes.byref(m), ctypes.byref(b)))
+    return int(m.value), int(b.value)

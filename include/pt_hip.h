@@ -136,6 +136,14 @@ int pt_profile_read(pt_scene* scene, pt_kernel_time* out, int max_entries, int* 
  * bit patterns of a[i]). */
 int pt_selftest_math(int device, int fn, const float* a, const float* b, float* out, size_t n);
 
+/* Exhaustive self-test of the core's division-free reciprocal (pt_math.h rcp_rn, used by the
+ * triangle test for 1/det): compares it with IEEE 1.0f/x on the device for every float x whose
+ * magnitude bit pattern lies in [lo_bits, hi_bits] (< 0x80000000), both signs.  steps: Newton
+ * steps (0..2), -1 = the core's own.  *mismatches = number of differing results;
+ * *failing_bits = one failing input (nullable). */
+int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
+                    uint32_t* failing_bits);
+
 #ifdef __cplusplus
 }
 #endif

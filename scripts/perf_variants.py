@@ -37,11 +37,14 @@ VARIANTS = {
     "wavefront_lean4_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4"},
     "wavefront_lean8_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8"},
     "mega_lean2_lds": {"PT_KERNEL": "mega", "PT_TRAV": "lean2"},
+    "mega_lean_fastrcp": {"PT_KERNEL": "mega", "PT_TRAV": "lean", "PT_FASTRCP": "1"},
+    "wavefront_lean4_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_FASTRCP": "1"},
+    "wavefront_lean8_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "1"},
 }
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

@@ -31,13 +31,16 @@ KERNELS = {
     "wavefront_lean2_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean2"},
     "wavefront_lean4_lds": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4"},
     "mega_lean2_lds": {"PT_KERNEL": "mega", "PT_TRAV": "lean2"},
+    "mega_lean_fastrcp": {"PT_KERNEL": "mega", "PT_TRAV": "lean", "PT_FASTRCP": "1"},
+    "wavefront_lean4_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_FASTRCP": "1"},
+    "wavefront_lean8_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "1"},
 }
 
 
 @pytest.fixture(params=list(KERNELS))
 def kernel(request, monkeypatch):
     """Every kernel variant must give the same bits."""
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in KERNELS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -112,6 +115,17 @@ def test_math_minmax_nan_handling():
     mx = pt_amd.selftest_math("max", a, b)
     assert mn[0] == 2.0 and mn[1] == 1.0 and np.isnan(mn[2]) and mn[4] == -3.0
     assert mx[0] == 2.0 and mx[1] == 1.0 and np.isnan(mx[2]) and mx[4] == 3.0
+
+
+def test_rcp_rn_exhaustive():
+    """The triangle test's division-free 1/det (pt_math.h rcp_rn: v_rcp_f32 + one Newton FMA
+    step) equals IEEE 1.0f/x for EVERY float with 2^-126 <= |x| <= 2^126 (checked on the device,
+    4.3e9 inputs); above 2^126 the hardware reciprocal flushes, which is why scenes with
+    max |e1||e2| >= 2^124 keep the division (SceneView::fast_rcp)."""
+    assert pt_amd.selftest_rcp() == (0, 0)                                  # 2^-126 .. 2^125
+    assert pt_amd.selftest_rcp(-1, 0x7E000000, 0x7E800000) == (0, 0)        # 2^125 .. 2^126
+    assert pt_amd.selftest_rcp(-1, 0x7E800000, 0x7F7FFFFF)[0] > 0           # above 2^126: flushed
+    assert pt_amd.selftest_rcp(0)[0] > 0                                    # the check can fail
 
 
 def test_hash_bitexact():
@@ -213,7 +227,7 @@ def test_invalid_scene_rejected():
 # kernel timing (pt_profile_*) and the AUTO policy (megakernel below 2^20 paths per call)
 # ---------------------------------------------------------------------------------------------
 def test_profile_records_every_launch(packed, monkeypatch):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP"):
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(64, 64)
@@ -237,7 +251,7 @@ def test_profile_records_every_launch(packed, monkeypatch):
 
 
 def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP"):
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
@@ -255,7 +269,7 @@ def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
 def test_auto_large_render_matches_megakernel(packed, monkeypatch):
     """At the AUTO switch point the wavefront result equals the megakernel's bit for bit
     (both equal the oracle on the smaller cases above)."""
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP"):
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(512, 512)
