@@ -51,7 +51,7 @@ struct LaunchOpts {
     bool wavefront = false;  // wavefront pipeline (pt_wavefront.hip)
     bool literal = false;  // k_mega: the reference's control flow
     bool lds = true;       // stage the scene in LDS when it fits
-    bool fast_rcp = false; // rcp_rn for 1/det where SceneView::fast_rcp says it is exact (opt-in: measured no faster)
+    int fast_rcp = -1;     // rcp_rn for 1/det where SceneView::fast_rcp says it is exact: -1 per-pipeline default
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 

@@ -231,7 +231,8 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
     // lean by default: the megakernel keeps the path state live across traversal, so the
     // multi-test leaf turns (lean2+) cost it occupancy (measured slower)
     const int trav0 = lo.trav < 0 ? 3 : std::min(lo.trav, 4);
-    const int trav = trav0 + ((trav0 >= 3 && lo.fast_rcp && sc.fast_rcp) ? 10 : 0);
+    const bool fast = lo.fast_rcp == 1 && sc.fast_rcp;  // off by default here: measured slower (occupancy)
+    const int trav = trav0 + ((trav0 >= 3 && fast) ? 10 : 0);
 #define RA(L, T) launch_regen_a<L, T>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream)
 #define RA_T(L, T) else if (trav == T) RA(L, T);
     if (lds) {

@@ -34,6 +34,7 @@ KERNELS = {
     "mega_lean_fastrcp": {"PT_KERNEL": "mega", "PT_TRAV": "lean", "PT_FASTRCP": "1"},
     "wavefront_lean4_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_FASTRCP": "1"},
     "wavefront_lean8_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "1"},
+    "wavefront_lean8_div": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "0"},
 }
 
 
