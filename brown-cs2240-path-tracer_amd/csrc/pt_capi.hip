@@ -400,7 +400,7 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 }
 
 // PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
-// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8, PT_FASTRCP=0|1.
+// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8|lean16, PT_FASTRCP=0|1.
 // AUTO picks the wavefront pipeline once a call has this many paths: below it the fixed
 // cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.
 constexpr uint64_t kWfAutoMinPaths = 1ull << 20;
@@ -415,7 +415,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     }
     if (const char* e = std::getenv("PT_LDS")) lo.lds = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("PT_FASTRCP")) lo.fast_rcp = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : -1;
+    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : -1;
     return lo;
 }
 

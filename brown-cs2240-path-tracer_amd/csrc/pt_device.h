@@ -337,7 +337,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
 
 // Traversal flavours (LaunchOpts.trav): 0 nested loops (trace), 1 flattened with per-lane
 // branches (trav_step), 2 flattened and predicated (trav_step_pred), 3 lean (trav_step_lean),
-// 4 lean with two triangle tests per leaf turn, 5 with four, 6 with eight; +10: the lean
+// 4 lean with two triangle tests per leaf turn, 5 with four, 6 with eight, 7 with sixteen; +10: the lean
 // flavours with 1/det from rcp_rn (scenes with SceneView::fast_rcp).
 template <int TRAV, bool LEAN = (TRAV >= 3)>
 struct TravSel { using type = TravState; };
@@ -349,7 +349,7 @@ __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, 
                                              int32_t* stack, int stride, Counters& cnt) {
     if constexpr (TRAV >= 3) {  // TRAV + 10: the same with the fast reciprocal (SceneView::fast_rcp)
         constexpr int B = TRAV % 10;
-        constexpr int K = B == 3 ? 1 : (B == 4 ? 2 : (B == 5 ? 4 : 8));
+        constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16
         return trav_step_lean<K, COUNT, (TRAV >= 10)>(sc, r, s, stack, stride, cnt);
     }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);

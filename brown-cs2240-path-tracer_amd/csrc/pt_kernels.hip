@@ -228,9 +228,9 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
         return hipGetLastError();
     }
     const bool lds = lo.lds && scene_fits_lds(sc);
-    // lean by default: the megakernel keeps the path state live across traversal, so the
-    // multi-test leaf turns (lean2+) cost it occupancy (measured slower)
-    const int trav0 = lo.trav < 0 ? 3 : std::min(lo.trav, 4);
+    // lean2 by default (measured: 604 vs 551 lean, 456 lean4); wider leaf turns cost the
+    // megakernel occupancy since it keeps the path state live across traversal
+    const int trav0 = lo.trav < 0 ? 4 : std::min(lo.trav, 4);
     const bool fast = lo.fast_rcp == 1 && sc.fast_rcp;  // off by default here: measured slower (occupancy)
     const int trav = trav0 + ((trav0 >= 3 && fast) ? 10 : 0);
 #define RA(L, T) launch_regen_a<L, T>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream)

@@ -117,7 +117,7 @@ constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8;
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 
 template <bool LDS, int TRAV, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(TRAV % 10 == 6 ? 5 : (TRAV % 10 >= 4 ? 6 : 1), 8))) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
+__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
@@ -334,11 +334,11 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
         return wf_render_t<L, T, false>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream);         \
     }
     if (lds) {
-        WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6)
-        WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16)
+        WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7)
+        WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17)
     } else {
-        WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6)
-        WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16)
+        WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7)
+        WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17)
     }
 #undef WF
     return hipErrorInvalidValue;

@@ -35,6 +35,7 @@ KERNELS = {
     "wavefront_lean4_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_FASTRCP": "1"},
     "wavefront_lean8_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "1"},
     "wavefront_lean8_div": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "0"},
+    "wavefront_lean16_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_FASTRCP": "1"},
 }
 
 
