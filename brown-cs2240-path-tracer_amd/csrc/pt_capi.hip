@@ -344,6 +344,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.inv_ntri = 1.0f / (float)L.ntri;  // intersection-logic.wgsl:284
     s->view.max_stack = (int32_t)L.info.max_stack;
     s->view.fast_rcp = L.fast_rcp ? 1 : 0;
+    s->view.node_bias = 0;  // per-pipeline default (launch_wavefront / launch_megakernel)
     s->view.off_tris = (uint32_t)(o_tris - o_nodes);
     s->view.off_mats = (uint32_t)(o_mats - o_nodes);
     s->view.off_lights = (uint32_t)(o_lights - o_nodes);
@@ -400,7 +401,7 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 }
 
 // PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
-// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8|lean16, PT_FASTRCP=0|1.
+// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32, PT_FASTRCP=0|1.
 // AUTO picks the wavefront pipeline once a call has this many paths: below it the fixed
 // cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.
 constexpr uint64_t kWfAutoMinPaths = 1ull << 20;
@@ -415,7 +416,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     }
     if (const char* e = std::getenv("PT_LDS")) lo.lds = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("PT_FASTRCP")) lo.fast_rcp = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : -1;
+    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
     return lo;
 }
 
@@ -444,6 +445,7 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     w.hitq = reinterpret_cast<int2*>(b + o_hit);
     w.rad = reinterpret_cast<float*>(b + o_rad);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
+    if (hipMemset(w.ctl, 0, 4 * WF_CTL_WORDS) != hipSuccess) return fail(PT_ERR_HIP, "hipMemset wavefront control words");
     w.capacity = (uint32_t)n;
     return PT_OK;
 }
@@ -465,15 +467,17 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         explicit ProfScope(KernelProfiler* p) { t_prof = p; }
         ~ProfScope() { t_prof = nullptr; }
     } prof_scope(s->prof_on ? &s->prof : nullptr);
+    SceneView view = s->view;
+    if (const char* e = std::getenv("PT_NODE_BIAS")) view.node_bias = std::max(1, std::atoi(e));  // A/B runs
     if (lo.wavefront) {
         const uint64_t want = std::max<uint64_t>(npix, std::min<uint64_t>(npix * (accum ? nframes : 1), kWfTargetPaths));
         int rc2 = ensure_wavefront(s, want);
         if (rc2 != PT_OK) return rc2;
-        HIP_TRY(launch_wavefront(lo, s->view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
+        HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
                                  stream));
         return PT_OK;
     }
-    HIP_TRY(launch_megakernel(lo, s->view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt, stream));
+    HIP_TRY(launch_megakernel(lo, view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt, stream));
     return PT_OK;
 }
 
@@ -498,6 +502,23 @@ int pt_render_async(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t
                        reinterpret_cast<Counters*>(d_counters), static_cast<hipStream_t>(stream));
 }
 
+// After a synchronised call: a trace wave that hit kTraceWatchdog left a flag (cleared here).
+static int check_watchdog(pt_scene* s) {
+    if (!s->d_wf) return PT_OK;
+    uint32_t flag = 0;
+    HIP_TRY(hipMemcpy(&flag, s->wf.ctl + WF_WATCHDOG, sizeof(flag), hipMemcpyDeviceToHost));
+    if (!flag) return PT_OK;
+    uint32_t v[WF_SNAP_WORDS] = {};
+    HIP_TRY(hipMemcpy(v, s->wf.ctl + WF_SNAP, sizeof(v), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(s->wf.ctl + WF_WATCHDOG, 0, (WF_SNAP + WF_SNAP_WORDS - WF_WATCHDOG) * sizeof(uint32_t)));
+    char msg[320];
+    std::snprintf(msg, sizeof(msg),
+                  "wavefront trace gave up after kTraceWatchdog iterations (result invalid); first wave: count=%u "
+                  "nwaves=%u w=%u J=%u jl=%u wv=%u nv=%u cur=%u flushed=%u in_flight=%u mask=%08x%08x queue=%u",
+                  v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[11], v[10], v[12]);
+    return fail(PT_ERR_HIP, msg);
+}
+
 int pt_render(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
               int max_depth, int mode, float* accum, pt_counters* counters) {
     if (!s || !accum || !meta) return fail(PT_ERR_INVALID, "null argument");
@@ -515,7 +536,7 @@ int pt_render(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nfram
     HIP_TRY(hipMemcpyAsync(accum, s->d_accum, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     if (counters) HIP_TRY(hipMemcpyAsync(counters, s->d_counters, sizeof(Counters), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    return PT_OK;
+    return check_watchdog(s);
 }
 
 int pt_frame_async(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float* d_radiance, void* stream) {
@@ -536,7 +557,7 @@ int pt_frame(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float
     if (rc != PT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(radiance, s->d_accum, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    return PT_OK;
+    return check_watchdog(s);
 }
 
 int pt_tonemap(const float* acc, size_t npix, uint32_t sample_runs, uint8_t* rgba) {

@@ -290,11 +290,12 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     const uint64_t want_node = __ballot(state == 0);
     if ((want_leaf | want_node) == 0) return false;
     bool decide = false;
-    if (__popcll(want_leaf) >= __popcll(want_node)) {  // wave-uniform
+    if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
         if (state == TF_LEAF) {
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const bool live = j == 0 || s.k < s.nt;  // the first test always is
+                if (j > 0 && !__any(live)) break;        // every lane's leaf pair is done
                 const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
                 float t;
                 const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
@@ -349,7 +350,7 @@ __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, 
                                              int32_t* stack, int stride, Counters& cnt) {
     if constexpr (TRAV >= 3) {  // TRAV + 10: the same with the fast reciprocal (SceneView::fast_rcp)
         constexpr int B = TRAV % 10;
-        constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16
+        constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
         return trav_step_lean<K, COUNT, (TRAV >= 10)>(sc, r, s, stack, stride, cnt);
     }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);

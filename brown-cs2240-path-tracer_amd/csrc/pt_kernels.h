@@ -61,7 +61,10 @@ bool scene_fits_lds(const SceneView& sc);
 // path's state travels with its ray: queue entry i holds the ray AND the path state, and
 // a shade kernel writes the surviving path to its compacted slot of the other queue, so no
 // kernel gathers by path index.  Iterations alternate extension / shadow queues.
-enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_CTL_WORDS = 64 };
+enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_WATCHDOG = 2, WF_SNAP_CLAIM = 3, WF_SNAP = 8, WF_SNAP_WORDS = 16, WF_CTL_WORDS = 64 };
+// iterations after which a trace wave gives up: it sets ctl[WF_WATCHDOG], the first such wave
+// leaves its scheduling state in ctl[WF_SNAP..], and the host reports an error
+constexpr uint32_t kTraceWatchdog = 1u << 24;
 struct WfQueue {
     float4* ray;  // [i][2]: (o.xyz, d.x), (d.y, d.z, path index bits, depth | spec << 16)
     float4* q2;   // (L.xyz, seed bits)

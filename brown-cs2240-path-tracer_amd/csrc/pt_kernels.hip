@@ -215,9 +215,13 @@ static void launch_regen_a(const SceneView& sc, const FrameParams& fp, uint32_t 
     }
 }
 
-hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
+constexpr int kMegaNodeBias = 8;  // measured with lean4: 1 -> 8 = +9 %
+
+hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& scene, const FrameParams& fp, uint32_t frame0,
                              uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
                              hipStream_t stream) {
+    SceneView sc = scene;
+    if (sc.node_bias <= 0) sc.node_bias = kMegaNodeBias;
     if (!accum) { nframes = 1; stride = 1; }
     if (lo.literal) {
         dim3 grid((fp.width + 15) / 16, (fp.height + 15) / 16), block(kMegaBlock);
@@ -228,17 +232,17 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
         return hipGetLastError();
     }
     const bool lds = lo.lds && scene_fits_lds(sc);
-    // lean2 by default (measured: 604 vs 551 lean, 456 lean4); wider leaf turns cost the
-    // megakernel occupancy since it keeps the path state live across traversal
-    const int trav0 = lo.trav < 0 ? 4 : std::min(lo.trav, 4);
-    const bool fast = lo.fast_rcp == 1 && sc.fast_rcp;  // off by default here: measured slower (occupancy)
+    // lean4 + node bias 8 + fast reciprocal by default (measured at 1024^2 64 spp: 848 vs 611
+    // for lean2 with majority turns and the division; scripts/perf_variants.py)
+    const int trav0 = lo.trav < 0 ? 5 : std::min(lo.trav, 5);
+    const bool fast = lo.fast_rcp != 0 && sc.fast_rcp;
     const int trav = trav0 + ((trav0 >= 3 && fast) ? 10 : 0);
 #define RA(L, T) launch_regen_a<L, T>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream)
 #define RA_T(L, T) else if (trav == T) RA(L, T);
     if (lds) {
-        if (trav == 0) RA(true, 0); RA_T(true, 1) RA_T(true, 2) RA_T(true, 3) RA_T(true, 4) RA_T(true, 13) RA_T(true, 14)
+        if (trav == 0) RA(true, 0); RA_T(true, 1) RA_T(true, 2) RA_T(true, 3) RA_T(true, 4) RA_T(true, 5) RA_T(true, 13) RA_T(true, 14) RA_T(true, 15)
     } else {
-        if (trav == 0) RA(false, 0); RA_T(false, 1) RA_T(false, 2) RA_T(false, 3) RA_T(false, 4) RA_T(false, 13) RA_T(false, 14)
+        if (trav == 0) RA(false, 0); RA_T(false, 1) RA_T(false, 2) RA_T(false, 3) RA_T(false, 4) RA_T(false, 5) RA_T(false, 13) RA_T(false, 14) RA_T(false, 15)
     }
 #undef RA_T
 #undef RA

@@ -73,7 +73,11 @@ struct SceneView {
     // 1: every triangle has |e1|*|e2| < 2^124, so with unit ray directions |det| < 2^126 and
     // the triangle test may take 1/det from rcp_rn (pt_math.h), bit-identical to the division
     int32_t fast_rcp;
-    int32_t pad[2];
+    // lean traversal turn policy: a leaf turn needs leaf lanes >= node_bias * node lanes
+    // (1 = plain majority; a leaf turn costs up to K triangle tests, a node turn one node
+    // step, so node turns that feed lanes into their leaves pay off); 0 = pipeline default
+    int32_t node_bias;
+    int32_t pad[1];
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

@@ -24,6 +24,7 @@
 #include "pt_path.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pt {
 
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
     if (COUNT) flush_counters(c, cnt_out);
 }
 
-// Per-wave LDS staging for k_wf_trace: the current window of 64 queued rays and a ring of
+// Per-wave LDS staging for k_wf_trace: the current window of 32 queued rays and a ring of
 // hit records.  Keeping both in LDS takes every global load and store out of the traversal
 // loop: on gfx9 loads and stores share the wave's in-order vmcnt, so a per-lane global store
 // (or prefetch) in the loop makes the next use of any loaded register wait for it.
@@ -116,6 +117,12 @@ constexpr uint32_t kHitRing = 128;  // entries; power of two, multiple of kWinRa
 constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8;
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 
+// Work split: the queue is cut into windows of 32 entries and wave w of N takes windows
+// w, w+N, w+2N, ...  Interleaving (not contiguous chunks) balances the waves: queue order is
+// spatially coherent (camera rays in pixel order, survivors compacted block by block), so a
+// contiguous chunk is an image region whose cost differs systematically from the others.
+// Inside a wave, window j's entries have the wave-local sequence numbers 32j .. 32j+31, which
+// index the hit ring.
 template <bool LDS, int TRAV, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -126,63 +133,94 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [kHitRing]
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     const uint32_t count = wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
-    const uint32_t nwaves = gridDim.x * (blockDim.x / 64), w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    const uint32_t per = (count + nwaves - 1) / nwaves;
-    const uint32_t begin = min(w * per, count), end = min(begin + per, count);
+    // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    const uint32_t nwin = (count + kWinRays - 1) / kWinRays;
     if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * kStageBytes);
-    if (begin >= end) return;  // wave-uniform
+    if (w >= nwin) return;  // wave-uniform
+    const uint32_t J = (nwin - w + nwaves - 1) / nwaves;  // windows of this wave
+    auto wbase = [&](uint32_t j) { return (w + j * nwaves) * kWinRays; };
+    auto wcount = [&](uint32_t j) { return min(kWinRays, count - wbase(j)); };
     // lanes 0..31 load the first halves of a window's ray records, lanes 32..63 the second
     const uint32_t lane = lane_id();
+    const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
     const float4* q = in_q ? wb.shd.ray : wb.ext.ray;
     Counters c = {};
-    // window [ws, we) sits in LDS; the following window [ns, ne) is in flight in registers
-    uint32_t ws = begin, we = min(begin + kWinRays, end);
-    const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
-    if (ws + wl < we) wray[2 * wl + half] = q[2 * (size_t)(ws + wl) + half];
-    uint32_t ns = we, ne = min(we + kWinRays, end);
+    // window jl sits in LDS; window jl + 1 is in flight in registers
+    uint32_t jl = 0, wv = wcount(0);
+    if (wl < wv) wray[2 * wl + half] = q[2 * (size_t)(wbase(0) + wl) + half];
+    uint32_t nv = 0;
     float4 na = make_float4(0, 0, 0, 0);
-    if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
-    uint32_t cur = ws;      // next queue entry to hand out
-    uint32_t flushed = ws;  // entries below this are in wb.hitq
-    uint32_t idx = 0, p = 0;
+    if (J > 1) {
+        nv = wcount(1);
+        if (wl < nv) na = q[2 * (size_t)(wbase(1) + wl) + half];
+    }
+    uint32_t cur = 0;      // sequence number of the next entry to hand out (in window jl)
+    uint32_t flushed = 0;  // sequence numbers below this are written back to wb.hitq
+    uint32_t sq = 0, p = 0;
     bool has = false;
     Ray r;
     r.o = r.d = r.inv = mk(0.0f, 0.0f, 0.0f);
     typename TravSel<TRAV>::type s;
     trav_init(s, false);
-    while (true) {
+    for (uint32_t guard = 0;; ++guard) {
+        if (guard == kTraceWatchdog) {  // every wave reaches an exit: report instead of hanging
+            const uint64_t hm = __ballot(has);
+            if (lane == 0) {
+                atomicOr(&wb.ctl[WF_WATCHDOG], 1u);
+                if (atomicCAS(&wb.ctl[WF_SNAP_CLAIM], 0u, 1u) == 0u) {
+                    const uint32_t v[WF_SNAP_WORDS] = {count, nwaves, w, J, jl, wv, nv, cur, flushed,
+                                                       (uint32_t)__popcll(hm), (uint32_t)hm, (uint32_t)(hm >> 32),
+                                                       (uint32_t)in_q, 0u, 0u, 0u};
+                    for (int i = 0; i < WF_SNAP_WORDS; ++i) wb.ctl[WF_SNAP + i] = v[i];
+                }
+            }
+            break;
+        }
+        // write back every window whose entries are all handed out and traced (coalesced)
+        while (flushed < J * kWinRays) {
+            const uint32_t jf = flushed / kWinRays;
+            const bool handed = jf < jl || (jf == jl && cur == jl * kWinRays + wv);
+            if (!handed || __any(has && sq < flushed + kWinRays)) break;
+            const uint32_t fv = wcount(jf);
+            if (lane < fv) wb.hitq[wbase(jf) + lane] = ring[(flushed + lane) & (kHitRing - 1)];
+            flushed += kWinRays;
+        }
         // hand the next entries to idle lanes (wave-uniform control)
         const uint64_t need = __ballot(!has);
-        if (need && cur < end) {
-            if (cur == we && ne - flushed <= kHitRing) {  // next window, if the hit ring has room
-                if (ns + wl < ne) wray[2 * wl + half] = na;
-                ws = ns; we = ne; ns = we; ne = min(we + kWinRays, end);
-                if (ns + wl < ne) na = q[2 * (size_t)(ns + wl) + half];
+        if (need) {
+            if (cur == jl * kWinRays + wv && jl + 1 < J && (jl + 2) * kWinRays - flushed <= kHitRing) {
+                if (wl < nv) wray[2 * wl + half] = na;  // next window, if the hit ring has room
+                ++jl;
+                wv = nv;
+                cur = jl * kWinRays;
+                if (jl + 1 < J) {
+                    nv = wcount(jl + 1);
+                    if (wl < nv) na = q[2 * (size_t)(wbase(jl + 1) + wl) + half];
+                }
             }
-            if (cur < we) {
-                const uint32_t j = cur + rank_below(need);
-                if (!has && j < we) {
-                    r = unpack_ray(wray[2 * (j - ws)], wray[2 * (j - ws) + 1], p);
-                    idx = j;
+            const uint32_t wend = jl * kWinRays + wv;
+            if (cur < wend) {
+                const uint32_t k = cur + rank_below(need);
+                if (!has && k < wend) {
+                    const uint32_t o = k - jl * kWinRays;
+                    r = unpack_ray(wray[2 * o], wray[2 * o + 1], p);
+                    sq = k;
                     trav_init(s, true);
                     has = true;
                 }
-                cur = min(cur + (uint32_t)__popcll(need), we);
+                cur = min(cur + (uint32_t)__popcll(need), wend);
             }
         }
-        if (!__any(has)) break;  // nothing in flight and nothing left to hand out
+        if (!__any(has)) {
+            if (jl + 1 >= J && cur == jl * kWinRays + wv && flushed >= J * kWinRays) break;  // all done
+            continue;  // ring full with nothing in flight: the flush above frees it
+        }
         trav_advance<TRAV, COUNT>(sc, r, s, stack, blockDim.x, c);
         if (has && trav_finished(s)) {
-            ring[(idx - begin) & (kHitRing - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
+            ring[sq & (kHitRing - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;
-        }
-        // write back every fully traced window: coalesced, once per 64 entries
-        while (true) {
-            const uint32_t fe = min(flushed + kWinRays, end);
-            if (fe > cur || flushed >= end || __any(has && idx < fe)) break;
-            const uint32_t e = flushed + lane;  // fe - flushed <= 32: the upper half of the wave idles
-            if (e < fe) wb.hitq[e] = ring[(e - begin) & (kHitRing - 1)];
-            flushed = fe;
         }
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -211,12 +249,15 @@ __global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneView sc, FramePar
         r = load_entry(in, i, p, ps);
         const int2 h = wb.hitq[i];
         const float t = __builtin_bit_cast(float, h.y);
+        // a trace that gave up (watchdog, reported by the host) leaves stale records: never
+        // let one index outside the triangle array
+        const int rec = (uint32_t)h.x < (uint32_t)sc.n_tris ? h.x : -1;
         if (EXT) {
-            more = path_after_ext(sc, h.x, t, r, ps);
+            more = path_after_ext(sc, rec, t, r, ps);
             if (more && COUNT) c.shadow_queries++;
         } else {
             load_shading_point(wb, i, ps);
-            more = path_after_shadow(sc, fp, h.x, t, r, ps);
+            more = path_after_shadow(sc, fp, rec, t, r, ps);
             if (more && COUNT) c.ext_queries++;
         }
         if (!more) {
@@ -295,7 +336,8 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     const uint32_t npix = fp.width * fp.height;
     const uint32_t F = std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
     const size_t lds = (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * kStageBytes + (LDS ? sc.span_bytes : 0);
-    const int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
+    int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
+    if (const char* e = std::getenv("PT_WF_TRACE_BLOCKS")) tblocks = std::max(1, std::min(tblocks, std::atoi(e)));  // tests
     const int iters = 2 * (fp.max_depth + 1);
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
@@ -317,15 +359,17 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     return hipGetLastError();
 }
 
-hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
+hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
                             Counters* cnt, hipStream_t stream) {
     if (!accum) { nframes = 1; stride = 1; }
+    SceneView sc = scene;
+    if (sc.node_bias <= 0) sc.node_bias = 8;  // measured best with lean16 (1 = majority: -13 %)
     const bool lds = lo.lds && scene_fits_lds(sc);
-    // lean8 with the fast reciprocal by default (measured best on gfx950: 750 vs 741 lean4,
-    // 697 lean8 with the division); the wavefront always uses a flattened traversal; lean
-    // flavours take the fast reciprocal (+10) when it is exact for the scene
-    const int base = lo.trav < 0 ? 6 : (lo.trav == 0 ? 1 : lo.trav);
+    // lean16 with the fast reciprocal by default (measured best on gfx950, scripts/perf_variants.py);
+    // the wavefront always uses a flattened traversal; lean flavours take the fast reciprocal
+    // (+10) when it is exact for the scene
+    const int base = lo.trav < 0 ? 7 : (lo.trav == 0 ? 1 : lo.trav);
     const bool fast = lo.fast_rcp != 0 && sc.fast_rcp;
     const int trav = base + ((base >= 3 && fast) ? 10 : 0);
 #define WF(L, T)                                                                                               \
@@ -334,11 +378,11 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
         return wf_render_t<L, T, false>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream);         \
     }
     if (lds) {
-        WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7)
-        WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17)
+        WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7) WF(true, 8)
+        WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18)
     } else {
-        WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7)
-        WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17)
+        WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
+        WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18)
     }
 #undef WF
     return hipErrorInvalidValue;

@@ -42,11 +42,32 @@ VARIANTS = {
     "wavefront_lean8_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "1"},
     "wavefront_lean8_div": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_FASTRCP": "0"},
     "wavefront_lean16_fastrcp": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_FASTRCP": "1"},
+    "wf_lean8_bias2": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_NODE_BIAS": "2"},
+    "wf_lean8_bias4": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_NODE_BIAS": "4"},
+    "wf_lean16_bias2": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "2"},
+    "wf_lean16_bias4": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "4"},
+    "wf_lean16_bias8": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "8"},
+    "wf_lean16_bias16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "16"},
+    "wf_lean16_bias64": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "64"},
+    "wf_lean32_bias8": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean32", "PT_NODE_BIAS": "8"},
+    "wf_lean32_bias16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean32", "PT_NODE_BIAS": "16"},
+    "wf_lean32_bias64": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean32", "PT_NODE_BIAS": "64"},
+    "wf_lean8_bias16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_NODE_BIAS": "16"},
+    "mega_lean2_bias2": {"PT_KERNEL": "mega", "PT_TRAV": "lean2", "PT_NODE_BIAS": "2"},
+    "mega_lean2_bias4": {"PT_KERNEL": "mega", "PT_TRAV": "lean2", "PT_NODE_BIAS": "4"},
+    "mega_lean_bias2": {"PT_KERNEL": "mega", "PT_TRAV": "lean", "PT_NODE_BIAS": "2"},
+    "mega_lean2_bias8": {"PT_KERNEL": "mega", "PT_TRAV": "lean2", "PT_NODE_BIAS": "8"},
+    "mega_lean4_bias4": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "4"},
+    "mega_lean4_bias8": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "8"},
+    "mega_lean2_bias4_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean2", "PT_NODE_BIAS": "4", "PT_FASTRCP": "1"},
+    "mega_lean4_bias8_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "8", "PT_FASTRCP": "1"},
+    "mega_lean4_bias16_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "16", "PT_FASTRCP": "1"},
+    "mega_lean2_bias8_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean2", "PT_NODE_BIAS": "8", "PT_FASTRCP": "1"},
 }
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 
