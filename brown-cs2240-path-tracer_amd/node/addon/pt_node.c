@@ -267,6 +267,46 @@ static napi_value js_tonemap(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
+/* profileEnable(scene, bool): bracket every kernel launch of the scene with HIP events */
+static napi_value js_profile_enable(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
+    bool on = true;
+    if (!s || (argc > 1 && napi_get_value_bool(env, argv[1], &on) != napi_ok)) {
+        napi_throw_type_error(env, NULL, "profileEnable(scene, enable)");
+        return NULL;
+    }
+    int rc = pt_profile_enable(s, on ? 1 : 0);
+    if (rc) return throw_pt(env, rc);
+    return NULL;
+}
+
+/* profileRead(scene) -> {kernel: {launches, totalMs, minMs, maxMs}} */
+static napi_value js_profile_read(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
+    if (!s) { napi_throw_type_error(env, NULL, "profileRead(scene)"); return NULL; }
+    pt_kernel_time kt[16];
+    int n = 0;
+    int rc = pt_profile_read(s, kt, 16, &n);
+    if (rc) return throw_pt(env, rc);
+    napi_value o, k, v;
+    napi_create_object(env, &o);
+    for (int i = 0; i < n; ++i) {
+        napi_create_object(env, &k);
+        napi_create_double(env, (double)kt[i].launches, &v); napi_set_named_property(env, k, "launches", v);
+        napi_create_double(env, kt[i].total_ms, &v); napi_set_named_property(env, k, "totalMs", v);
+        napi_create_double(env, kt[i].min_ms, &v); napi_set_named_property(env, k, "minMs", v);
+        napi_create_double(env, kt[i].max_ms, &v); napi_set_named_property(env, k, "maxMs", v);
+        napi_set_named_property(env, o, kt[i].name, k);
+    }
+    return o;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     napi_property_descriptor props[] = {
         {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_enumerable, NULL},
@@ -277,6 +317,8 @@ static napi_value init(napi_env env, napi_value exports) {
         {"renderSync", NULL, js_render_sync, NULL, NULL, NULL, napi_enumerable, NULL},
         {"frame", NULL, js_frame, NULL, NULL, NULL, napi_enumerable, NULL},
         {"tonemap", NULL, js_tonemap, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"profileEnable", NULL, js_profile_enable, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"profileRead", NULL, js_profile_read, NULL, NULL, NULL, napi_enumerable, NULL},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;
