@@ -179,11 +179,16 @@ __device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, Tra
 // Branch-free triangle test with the exact arithmetic of test_tri: every quantity of the
 // reference's early-out chain is computed and the chain becomes one predicate (the values
 // skipped by an early return never reach `hit`, so the result is identical).
-template <bool FAST_RCP = false>
-__device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, const Ray& r, float& t_out) {
-    const float eps = 1e-8f;
+struct TriRec { float4 a, b, c; };  // (v0, material), e1, e2
+__device__ __forceinline__ TriRec load_tri(const Tri* __restrict__ tris, int i) {
     const float4* tp = reinterpret_cast<const float4*>(tris + i);
-    float4 a = tp[0], b = tp[1], c = tp[2];
+    return TriRec{tp[0], tp[1], tp[2]};
+}
+
+template <bool FAST_RCP = false>
+__device__ __forceinline__ bool tri_hit(const TriRec& tr, const Ray& r, float& t_out) {
+    const float eps = 1e-8f;
+    const float4 a = tr.a, b = tr.b, c = tr.c;
     f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
     f3 rce2 = cross(r.d, e2);
     float det = dot(e1, rce2);
@@ -200,6 +205,10 @@ __device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, con
     const bool ok_u = !(u < 0.0f || u > 1.0f);
     const bool ok_v = !(v < 0.0f || u + v > 1.0f);
     return ok_det & ok_u & ok_v & (t > eps);
+}
+template <bool FAST_RCP = false>
+__device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, const Ray& r, float& t_out) {
+    return tri_hit<FAST_RCP>(load_tri(tris, i), r, t_out);
 }
 
 // trav_step with every per-lane branch replaced by selects (the scalar unit is shared by
@@ -282,7 +291,7 @@ __device__ __forceinline__ bool trav_finished(const TravState& s) { return s.don
 // K = triangle tests per leaf turn: a lane with at least two triangles of its leaf pair left
 // runs two in sequence (same order, each against the closest t so far), which halves the
 // per-iteration overhead (scheduling ballots, decision, loop control) per test.
-template <int K, bool COUNT, bool FAST_RCP>
+template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
                                                int stride, Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE);
@@ -292,18 +301,42 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     bool decide = false;
     if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
         if (state == TF_LEAF) {
+            if constexpr (!PIPE) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const bool live = j == 0 || s.k < s.nt;  // the first test always is
-                if (j > 0 && !__any(live)) break;        // every lane's leaf pair is done
-                const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
-                float t;
-                const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
-                                  ((s.best_t < 0.0f) | (t < s.best_t));
-                s.best_t = take ? t : s.best_t;
-                s.best = take ? idx : s.best;
-                if (COUNT) cnt.tri_tests += live ? 1 : 0;
-                s.k += live ? 1 : 0;
+                for (int j = 0; j < K; ++j) {
+                    const bool live = j == 0 || s.k < s.nt;  // the first test always is
+                    if (j > 0 && !__any(live)) break;        // every lane's leaf pair is done
+                    const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+                    float t;
+                    const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
+                                      ((s.best_t < 0.0f) | (t < s.best_t));
+                    s.best_t = take ? t : s.best_t;
+                    s.best = take ? idx : s.best;
+                    if (COUNT) cnt.tri_tests += live ? 1 : 0;
+                    s.k += live ? 1 : 0;
+                }
+            } else {
+                // the record of test j+1 is loaded (LDS) while test j computes; a lane whose
+                // leaf pair ends loads a valid record it will not use
+                int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+                TriRec cur = load_tri(sc.tris, idx);
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const bool live = j == 0 || s.k < s.nt;
+                    if (j > 0 && !__any(live)) break;
+                    const int k1 = s.k + 1;
+                    const int idx1 = k1 < s.nt ? (k1 < s.na ? s.la + k1 : s.lb + (k1 - s.na)) : idx;
+                    TriRec nxt;
+                    if (j + 1 < K) nxt = load_tri(sc.tris, idx1);
+                    float t;
+                    const bool take =
+                        tri_hit<FAST_RCP>(cur, r, t) & live & ((s.best_t < 0.0f) | (t < s.best_t));
+                    s.best_t = take ? t : s.best_t;
+                    s.best = take ? idx : s.best;
+                    if (COUNT) cnt.tri_tests += live ? 1 : 0;
+                    s.k += live ? 1 : 0;
+                    if (j + 1 < K) { cur = nxt; idx = idx1; }
+                }
             }
             decide = s.k == s.nt;
             s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
@@ -348,10 +381,10 @@ struct TravSel<TRAV, true> { using type = TravLean; };
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
                                              int32_t* stack, int stride, Counters& cnt) {
-    if constexpr (TRAV >= 3) {  // TRAV + 10: the same with the fast reciprocal (SceneView::fast_rcp)
+    if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal (SceneView::fast_rcp); + 20: pipelined leaf loads
         constexpr int B = TRAV % 10;
         constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
-        return trav_step_lean<K, COUNT, (TRAV >= 10)>(sc, r, s, stack, stride, cnt);
+        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, ((TRAV / 20) & 1) != 0>(sc, r, s, stack, stride, cnt);
     }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
     else return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);

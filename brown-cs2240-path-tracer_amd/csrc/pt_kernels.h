@@ -52,6 +52,7 @@ struct LaunchOpts {
     bool literal = false;  // k_mega: the reference's control flow
     bool lds = true;       // stage the scene in LDS when it fits
     int fast_rcp = -1;     // rcp_rn for 1/det where SceneView::fast_rcp says it is exact: -1 per-pipeline default
+    int pipe = -1;         // lean leaf turns load the next triangle while testing one: -1 per-pipeline default
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 
@@ -65,6 +66,7 @@ enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_WATCHDOG = 2, WF_SNAP_CLAIM = 3, WF_SNAP
 // iterations after which a trace wave gives up: it sets ctl[WF_WATCHDOG], the first such wave
 // leaves its scheduling state in ctl[WF_SNAP..], and the host reports an error
 constexpr uint32_t kTraceWatchdog = 1u << 24;
+constexpr uint64_t kTraceWatchdogTicks = 500000000ull;  // 5 s of wall_clock64 (100 MHz)
 struct WfQueue {
     float4* ray;  // [i][2]: (o.xyz, d.x), (d.y, d.z, path index bits, depth | spec << 16)
     float4* q2;   // (L.xyz, seed bits)

@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
     int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [kHitRing]
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
-    const uint32_t count = wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
+    const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip
     // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
@@ -164,8 +164,12 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     r.o = r.d = r.inv = mk(0.0f, 0.0f, 0.0f);
     typename TravSel<TRAV>::type s;
     trav_init(s, false);
+    const uint64_t t_start = wall_clock64();
     for (uint32_t guard = 0;; ++guard) {
-        if (guard == kTraceWatchdog) {  // every wave reaches an exit: report instead of hanging
+        // every wave reaches an exit: after kTraceWatchdog iterations or kTraceWatchdogTicks of
+        // wall clock it reports instead of hanging (and later launches of the render skip)
+        if (guard == kTraceWatchdog ||
+            ((guard & 1023u) == 1023u && wall_clock64() - t_start > kTraceWatchdogTicks)) {
             const uint64_t hm = __ballot(has);
             if (lane == 0) {
                 atomicOr(&wb.ctl[WF_WATCHDOG], 1u);
@@ -371,7 +375,8 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     // (+10) when it is exact for the scene
     const int base = lo.trav < 0 ? 7 : (lo.trav == 0 ? 1 : lo.trav);
     const bool fast = lo.fast_rcp != 0 && sc.fast_rcp;
-    const int trav = base + ((base >= 3 && fast) ? 10 : 0);
+    const bool pipe = lo.pipe > 0;
+    const int trav = base + ((base >= 3 && fast) ? 10 : 0) + ((base >= 3 && fast && pipe) ? 20 : 0);
 #define WF(L, T)                                                                                               \
     if (trav == T) {                                                                                           \
         if (count) return wf_render_t<L, T, true>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream); \
@@ -379,10 +384,10 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     }
     if (lds) {
         WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7) WF(true, 8)
-        WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18)
+        WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18) WF(true, 35) WF(true, 36) WF(true, 37)
     } else {
         WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
-        WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18)
+        WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18) WF(false, 35) WF(false, 36) WF(false, 37)
     }
 #undef WF
     return hipErrorInvalidValue;
