@@ -1,0 +1,163 @@
+// pt_bvh.cpp — native BVH build + pack (host C++, no GPU): SURVEY.md §8(f) row 2.
+//
+// Same algorithm as src/ts-util/bvh.ts:14-188 and src/packer.ts:83-137 (restated in the Node
+// host as node/lib/bvh.js + packer.js: pack_bvh), in IEEE double exactly as the JS numbers
+// are, so the packed buffer is byte-identical and the traversal (whose order and exit-distance
+// pruning depend on the topology) returns the same hits:
+//   * node split axis = longest extent of the node box (ties x > y > z);
+//   * 18 candidate split fractions s = 0.05, 0.05+0.05, ... accumulated in double while
+//     s <= 0.95 (the last is 0.9000000000000002); cost |nL - avg| + |nR - avg| with
+//     inclusive box overlap counts, first minimum wins;
+//   * a triangle overlapping both halves goes to both children;
+//   * a child is a leaf with <= 16 objects or when the split separated nothing; depth 16
+//     (root = 1) forces a leaf;
+//   * every node but the root keeps axis -1 (bvh.ts never stores the axis it passes down).
+// Compiled with -ffp-contract=off: `w0 * hi + w1 * lo` must round twice, as in JS.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <vector>
+
+#include "../../include/pt_hip.h"
+
+namespace {
+
+struct Box {
+    double mn[3], mx[3];
+};
+
+struct BNode {
+    bool leaf = false;
+    int axis = -1;
+    Box box{};
+    std::vector<int32_t> objs;  // indices into the triangle list
+    std::unique_ptr<BNode> l, r;
+};
+
+constexpr int kMaxDepth = 16;
+constexpr size_t kMaxObjPerNode = 16;
+
+inline bool overlap(const Box& a, const Box& b) {  // math.ts:45-49 (inclusive)
+    for (int k = 0; k < 3; ++k)
+        if (!(b.mn[k] <= a.mx[k] && a.mn[k] <= b.mx[k])) return false;
+    return true;
+}
+
+inline Box split_box(const Box& b, int axis, double c, bool low) {
+    Box o = b;
+    if (low) o.mx[axis] = c; else o.mn[axis] = c;
+    return o;
+}
+
+struct Builder {
+    const std::vector<Box>& tb;  // triangle boxes
+
+    void recurse(BNode& n, int depth) {
+        if (depth >= kMaxDepth) { n.leaf = true; return; }
+        const Box& nb = n.box;
+        const double sx = nb.mx[0] - nb.mn[0], sy = nb.mx[1] - nb.mn[1], sz = nb.mx[2] - nb.mn[2];
+        int axis;
+        if (sx >= sy && sx >= sz) axis = 0;
+        else if (sy >= sx && sy >= sz) axis = 1;
+        else axis = 2;
+        const double lo = nb.mn[axis], hi = nb.mx[axis];
+        double split = 0.5, cost = std::numeric_limits<double>::infinity();
+        const double step = 0.05;
+        for (double s = step; s <= 1.0 - step; s += step) {
+            const double w0 = s, w1 = 1.0 - s;
+            const double c = w0 * hi + w1 * lo;
+            const Box lb = split_box(nb, axis, c, true), hb = split_box(nb, axis, c, false);
+            int nl = 0, nh = 0;
+            for (int32_t o : n.objs) {
+                if (overlap(tb[o], lb)) ++nl;
+                if (overlap(tb[o], hb)) ++nh;
+            }
+            const double avg = (nl + nh) * 0.5;
+            const double cur = std::fabs(nl - avg) + std::fabs(nh - avg);
+            if (cur < cost) { split = s; cost = cur; }
+        }
+        const double c = split * hi + (1.0 - split) * lo;
+        n.l = std::make_unique<BNode>();
+        n.r = std::make_unique<BNode>();
+        n.l->box = split_box(nb, axis, c, true);
+        n.r->box = split_box(nb, axis, c, false);
+        for (int32_t o : n.objs) {
+            if (overlap(tb[o], n.l->box)) n.l->objs.push_back(o);
+            if (overlap(tb[o], n.r->box)) n.r->objs.push_back(o);
+        }
+        for (BNode* ch : {n.l.get(), n.r.get()}) {
+            if (ch->objs.size() <= kMaxObjPerNode || ch->objs.size() == n.objs.size()) ch->leaf = true;
+            else recurse(*ch, depth + 1);
+        }
+    }
+};
+
+void pack(const BNode& n, const int32_t* tris, std::vector<double>& out) {
+    const size_t cur = out.size();
+    const size_t nchild = n.leaf ? 4 * n.objs.size() : 0;
+    const double z3[3] = {0, 0, 0};
+    out.push_back(n.leaf ? 1 : 0);
+    out.push_back(n.axis);
+    out.push_back(n.leaf ? -1.0 : (double)(cur + 5 + 12 + nchild));
+    out.push_back(-1);
+    out.push_back(n.leaf ? (double)nchild : -2.0);
+    for (const BNode* ch : {n.l.get(), n.r.get()}) {
+        const double* mn = ch ? ch->box.mn : z3;
+        const double* mx = ch ? ch->box.mx : z3;
+        out.insert(out.end(), mn, mn + 3);
+        out.insert(out.end(), mx, mx + 3);
+    }
+    if (n.leaf)
+        for (int32_t o : n.objs)
+            for (int q = 0; q < 4; ++q) out.push_back(tris[4 * (size_t)o + q]);
+    if (!n.leaf && n.l) pack(*n.l, tris, out);
+    if (!n.leaf && n.r) {
+        out[cur + 3] = (double)out.size();
+        pack(*n.r, tris, out);
+    }
+}
+
+}  // namespace
+
+extern "C" int pt_bvh_build(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count,
+                            float* bvh_out, size_t bvh_cap, size_t* bvh_len) {
+    if (!vertices || !tris || !bvh_len || vertex_count == 0 || tri_count == 0 || (bvh_cap && !bvh_out))
+        return PT_ERR_INVALID;
+    // object boxes (index.ts:140-147, bounds_of_vec3) and the root box over all vertices
+    std::vector<Box> tb(tri_count);
+    for (size_t t = 0; t < tri_count; ++t) {
+        Box b{};
+        for (int v = 0; v < 3; ++v) {
+            const int32_t i = tris[4 * t + v];
+            if (i < 1 || (size_t)i > vertex_count) return PT_ERR_INVALID;
+            const double* p = vertices + 3 * (size_t)(i - 1);
+            for (int k = 0; k < 3; ++k) {
+                if (v == 0 || p[k] <= b.mn[k]) b.mn[k] = p[k];
+                if (v == 0 || p[k] >= b.mx[k]) b.mx[k] = p[k];
+            }
+        }
+        tb[t] = b;
+    }
+    Box root{};
+    for (size_t i = 0; i < vertex_count; ++i)
+        for (int k = 0; k < 3; ++k) {
+            const double x = vertices[3 * i + k];
+            if (i == 0 || x <= root.mn[k]) root.mn[k] = x;
+            if (i == 0 || x >= root.mx[k]) root.mx[k] = x;
+        }
+    BNode top;
+    top.axis = 0;
+    top.box = root;
+    top.objs.resize(tri_count);
+    for (size_t t = 0; t < tri_count; ++t) top.objs[t] = (int32_t)t;
+    Builder{tb}.recurse(top, 1);
+    std::vector<double> out(root.mn, root.mn + 3);
+    out.insert(out.end(), root.mx, root.mx + 3);
+    pack(top, tris, out);
+    *bvh_len = out.size();
+    if (bvh_cap < out.size()) return bvh_cap ? PT_ERR_INVALID : PT_OK;  // cap 0: size query
+    for (size_t i = 0; i < out.size(); ++i) bvh_out[i] = (float)out[i];
+    return PT_OK;
+}

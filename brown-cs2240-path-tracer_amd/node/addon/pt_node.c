@@ -267,6 +267,34 @@ static napi_value js_tonemap(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
+/* bvhBuild(Float64Array vertices, Int32Array tris (i0,i1,i2,mat)) -> Float32Array bvh_data
+ * (native twin of node/lib/bvh.js + packer.js:pack_bvh, byte-identical) */
+static napi_value js_bvh_build(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    napi_typedarray_type t0, t1;
+    size_t n0 = 0, n1 = 0, off;
+    void *d0 = NULL, *d1 = NULL;
+    napi_value ab;
+    if (argc < 2 || napi_get_typedarray_info(env, argv[0], &t0, &n0, &d0, &ab, &off) != napi_ok ||
+        napi_get_typedarray_info(env, argv[1], &t1, &n1, &d1, &ab, &off) != napi_ok || t0 != napi_float64_array ||
+        t1 != napi_int32_array || n0 % 3 || n1 % 4) {
+        napi_throw_type_error(env, NULL, "bvhBuild(Float64Array vertices, Int32Array tris)");
+        return NULL;
+    }
+    size_t len = 0;
+    int rc = pt_bvh_build((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, NULL, 0, &len);
+    if (rc) return throw_pt(env, rc);
+    napi_value buf, arr;
+    void* data = NULL;
+    CHECK_NAPI(env, napi_create_arraybuffer(env, len * sizeof(float), &data, &buf));
+    rc = pt_bvh_build((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, (float*)data, len, &len);
+    if (rc) return throw_pt(env, rc);
+    CHECK_NAPI(env, napi_create_typedarray(env, napi_float32_array, len, buf, 0, &arr));
+    return arr;
+}
+
 /* profileEnable(scene, bool): bracket every kernel launch of the scene with HIP events */
 static napi_value js_profile_enable(napi_env env, napi_callback_info info) {
     size_t argc = 2;
@@ -319,6 +347,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"tonemap", NULL, js_tonemap, NULL, NULL, NULL, napi_enumerable, NULL},
         {"profileEnable", NULL, js_profile_enable, NULL, NULL, NULL, napi_enumerable, NULL},
         {"profileRead", NULL, js_profile_read, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"bvhBuild", NULL, js_bvh_build, NULL, NULL, NULL, napi_enumerable, NULL},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

@@ -4,7 +4,8 @@
 // bench/tests).  Writes <out>/triangle_data.f32, <out>/bvh_data.f32 (little-endian f32,
 // the reference's SceneObjectPacked) and <out>/scene.json (meta[48], screenDimension,
 // camera, settings) plus <out>/meta.f32.  Usage: pt-pack.js <scene.ini|scene.xml> <out_dir> [--web-root DIR]
-//                            [--width W --height H --spp N --rr P --direct-only]
+//                            [--width W --height H --spp N --rr P --direct-only --native-bvh]
+// --native-bvh builds the BVH with the library's C++ builder (pt_bvh_build, byte-identical).
 const fs = require('fs');
 const path = require('path');
 const host = require('..');
@@ -14,12 +15,13 @@ function main(argv) {
     for (let i = 0; i < argv.length; i++) {
         const a = argv[i];
         if (a === '--direct-only') args.direct_only = true;
+        else if (a === '--native-bvh') args.native_bvh = true;
         else if (a.startsWith('--')) args[a.slice(2).replace(/-/g, '_')] = argv[++i];
         else args._.push(a);
     }
     if (args._.length < 2) { console.error('usage: pt-pack.js <scene.ini|scene.xml> <out_dir> [options]'); process.exit(2); }
     const [src, out] = args._;
-    const opts = { web_root: args.web_root, quiet: true };
+    const opts = { web_root: args.web_root, quiet: true, native_bvh: !!args.native_bvh };
     let loaded;
     if (src.endsWith('.ini')) loaded = host.load_scene_from_ini(src, opts);
     else {

@@ -94,6 +94,12 @@ function pack_primitive(obj_data, mtl_data, ctm, opts) {
             bvh_objects.push({ obj: [ind[i], ind[i + 1], ind[i + 2], mat_i], bounds: bounds_of_vec3(tri) });
         }
     });
+    if (opts && opts.native_bvh) {  // the same build in C++ (pt_bvh_build), byte-identical, for big meshes
+        const tris = new Int32Array(bvh_objects.length * 4);
+        bvh_objects.forEach((o, t) => tris.set(o.obj, 4 * t));
+        const bvh_data = require('./addon').load().bvhBuild(Float64Array.from(vertices), tris);
+        return { triangle_data: packed_array, bvh_data, bounds: bvh_bounds };
+    }
     const bvh = new BVH(bvh_objects, bvh_bounds, opts);
     return { triangle_data: packed_array, bvh_data: pack_bvh(bvh), bounds: bvh_bounds };
 }
@@ -131,7 +137,7 @@ function load_scene_xml_file(scene_path, opts) {
         const obj_data = load_file(p.data.path);
         let mtl_data;
         try { mtl_data = load_file(p.data.path.slice(0, -3) + 'mtl'); } catch (e) { mtl_data = ''; }
-        return pack_primitive(obj_data, mtl_data, p.ctm, { quiet: opts.quiet !== false });
+        return pack_primitive(obj_data, mtl_data, p.ctm, { quiet: opts.quiet !== false, native_bvh: !!opts.native_bvh });
     });
     return { primitive_data, camera_data };
 }

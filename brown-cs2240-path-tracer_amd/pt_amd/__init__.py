@@ -19,6 +19,7 @@ from ._lib import (  # noqa: F401
     Scene,
     SceneInfo,
     abi_version,
+    bvh_build,
     device_count,
     lib_path,
     load_library,

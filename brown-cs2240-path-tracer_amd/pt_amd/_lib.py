@@ -91,9 +91,10 @@ def load_library():
     L.pt_selftest_math.argtypes = [i, i, p, p, p, sz]
     L.pt_profile_enable.argtypes = [p, i]
     L.pt_selftest_rcp.argtypes = [i, i, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
+    L.pt_bvh_build.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read", "pt_selftest_rcp"):
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build"):
         getattr(L, fn).restype = i
     _lib = L
     return L
@@ -229,3 +230,16 @@ def selftest_rcp(steps: int = -1, lo_bits: int = 0x00800000, hi_bits: int = 0x7E
     b = ctypes.c_uint32(0)
     _check(L.pt_selftest_rcp(device, steps, lo_bits, hi_bits, ctypes.byref(m), ctypes.byref(b)))
     return int(m.value), int(b.value)
+
+
+def bvh_build(vertices, tris) -> np.ndarray:
+    """Native BVH build + pack (host only, no GPU): vertices f64 [n, 3] (post-CTM), tris
+    int32 [m, 4] = (i0, i1, i2, material) with 1-based vertex indices -> packed bvh_data (f32)."""
+    L = load_library()
+    v = np.ascontiguousarray(vertices, dtype=np.float64).reshape(-1)
+    t = np.ascontiguousarray(tris, dtype=np.int32).reshape(-1)
+    n = ctypes.c_size_t(0)
+    _check(L.pt_bvh_build(_ptr(v), v.size // 3, _ptr(t), t.size // 4, None, 0, ctypes.byref(n)))
+    out = np.empty(n.value, np.float32)
+    _check(L.pt_bvh_build(_ptr(v), v.size // 3, _ptr(t), t.size // 4, _ptr(out), out.size, ctypes.byref(n)))
+    return out

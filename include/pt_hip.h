@@ -122,6 +122,15 @@ int pt_frame_async(pt_scene* scene, const float meta[48], uint32_t t, int max_de
  * clamped; rgba[i*4+3] = 255. */
 int pt_tonemap(const float* accum, size_t npix, uint32_t sample_runs, uint8_t* rgba_out);
 
+/* Native BVH build (host only, no GPU): the reference's f64 builder
+ * (src/ts-util/bvh.ts:14-188) and packer (src/packer.ts:83-137) in C++, byte-identical to them.
+ * vertices: x,y,z per vertex in double — the values the host's JS holds after the CTM, not the
+ * f32 copies in triangle_data; tris: (i0, i1, i2, material) per triangle, vertex indices
+ * 1-based as in the OBJ.  Writes the packed bvh_data floats; *bvh_len = their count.  bvh_cap
+ * = 0 asks for the size only; a smaller non-zero bvh_cap fails with PT_ERR_INVALID. */
+int pt_bvh_build(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count, float* bvh_out,
+                 size_t bvh_cap, size_t* bvh_len);
+
 /* Kernel timing (no counterpart in the reference, which has no GPU timing): while enabled,
  * every kernel the scene launches is bracketed by two HIP events on the launch stream (no
  * synchronisation, a few microseconds per launch).  enable != 0 also discards earlier
