@@ -214,6 +214,8 @@ struct pt_scene {
     WfBuffers wf{};
     bool prof_on = false;  // pt_profile_enable
     KernelProfiler prof;
+    uint8_t* d_rgba = nullptr;  // pt_render_image scratch
+    size_t rgba_cap = 0;
 };
 
 namespace pt {
@@ -362,6 +364,7 @@ void pt_scene_destroy(pt_scene* s) {
     if (s->stream) { hipStreamSynchronize(s->stream); hipStreamDestroy(s->stream); }
     if (s->d_accum) hipFree(s->d_accum);
     if (s->d_wf) hipFree(s->d_wf);
+    if (s->d_rgba) hipFree(s->d_rgba);
     if (s->d_mem) hipFree(s->d_mem);
     s->prof.destroy();
     delete s;
@@ -557,6 +560,47 @@ int pt_frame(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float
     rc = render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_AUTO, false, s->d_accum, nullptr, s->stream);
     if (rc != PT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(radiance, s->d_accum, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return check_watchdog(s);
+}
+
+int pt_tonemap_async(pt_scene* s, const float* d_accum, size_t npix, uint32_t sample_runs, uint8_t* d_rgba,
+                     void* stream) {
+    if (!s || !d_accum || !d_rgba || sample_runs == 0) return fail(PT_ERR_INVALID, "null argument or zero sample_runs");
+    HIP_TRY(hipSetDevice(s->device));
+    struct ProfScope {
+        explicit ProfScope(KernelProfiler* p) { t_prof = p; }
+        ~ProfScope() { t_prof = nullptr; }
+    } prof_scope(s->prof_on ? &s->prof : nullptr);
+    HIP_TRY(launch_tonemap(d_accum, npix, sample_runs, d_rgba, static_cast<hipStream_t>(stream)));
+    return PT_OK;
+}
+
+int pt_render_image(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
+                    int max_depth, int mode, uint8_t* rgba, pt_counters* counters) {
+    if (!s || !rgba || !meta) return fail(PT_ERR_INVALID, "null argument");
+    if (nframes == 0) return fail(PT_ERR_INVALID, "nframes == 0 (the image divides by the sample count)");
+    FrameParams fp;
+    int rc = make_params(meta, max_depth, fp);
+    if (rc != PT_OK) return rc;
+    const size_t npix = (size_t)fp.width * fp.height;
+    HIP_TRY(hipSetDevice(s->device));
+    if ((rc = ensure_accum(s, 3 * npix)) != PT_OK) return rc;
+    if (s->rgba_cap < 4 * npix) {
+        if (s->d_rgba) hipFree(s->d_rgba);
+        s->d_rgba = nullptr;
+        s->rgba_cap = 0;
+        if (hipMalloc(&s->d_rgba, 4 * npix) != hipSuccess) return fail(PT_ERR_NOMEM, "hipMalloc image");
+        s->rgba_cap = 4 * npix;
+    }
+    HIP_TRY(hipMemsetAsync(s->d_accum, 0, 3 * npix * sizeof(float), s->stream));
+    if (counters) HIP_TRY(hipMemsetAsync(s->d_counters, 0, sizeof(Counters), s->stream));
+    rc = render_impl(s, meta, frame0, nframes, frame_stride, max_depth, mode, true, s->d_accum,
+                     counters ? s->d_counters : nullptr, s->stream);
+    if (rc != PT_OK) return rc;
+    if ((rc = pt_tonemap_async(s, s->d_accum, npix, nframes, s->d_rgba, s->stream)) != PT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(rgba, s->d_rgba, 4 * npix, hipMemcpyDeviceToHost, s->stream));
+    if (counters) HIP_TRY(hipMemcpyAsync(counters, s->d_counters, sizeof(Counters), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     return check_watchdog(s);
 }

@@ -17,11 +17,12 @@ namespace pt {
 // Kernel timing (pt_profile_enable / pt_profile_read): while a profiler is attached to the
 // calling thread, every launch is bracketed by two HIP events on its stream.
 enum KernelId : int {
-    KID_MEGA = 0, KID_REGEN, KID_WF_GENERATE, KID_WF_TRACE, KID_WF_SHADE_EXT, KID_WF_SHADE_SHADOW, KID_WF_ACCUM, KID_COUNT
+    KID_MEGA = 0, KID_REGEN, KID_WF_GENERATE, KID_WF_TRACE, KID_WF_SHADE_EXT, KID_WF_SHADE_SHADOW, KID_WF_ACCUM,
+    KID_TONEMAP, KID_COUNT
 };
 inline const char* kernel_name(int k) {
-    static const char* const n[KID_COUNT] = {"k_mega",     "k_regen",         "k_wf_generate",     "k_wf_trace",
-                                             "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum"};
+    static const char* const n[KID_COUNT] = {"k_mega",         "k_regen",           "k_wf_generate", "k_wf_trace",
+                                             "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum",    "k_tonemap"};
     return (k >= 0 && k < KID_COUNT) ? n[k] : "?";
 }
 struct KernelProfiler {
@@ -94,6 +95,9 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
 hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
                              uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
                              hipStream_t stream);
+
+// display transform of program-raymarch.ts:295-316 on device (pt_image.hip)
+hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t* rgba, hipStream_t stream);
 
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);

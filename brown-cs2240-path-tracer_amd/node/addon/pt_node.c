@@ -148,6 +148,7 @@ typedef struct {
     uint32_t frame0, nframes, stride;
     int32_t max_depth, mode;
     float* accum;
+    uint8_t* rgba; /* renderImage: the displayed image instead of the accumulator */
     pt_counters counters;
     int rc;
     char err[512];
@@ -156,7 +157,10 @@ typedef struct {
 static void render_execute(napi_env env, void* data) {
     (void)env;
     render_job* j = (render_job*)data;
-    j->rc = pt_render(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->accum, &j->counters);
+    j->rc = j->rgba ? pt_render_image(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->rgba,
+                                      &j->counters)
+                    : pt_render(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->accum,
+                                &j->counters);
     if (j->rc) snprintf(j->err, sizeof j->err, "pt_hip error %d: %s", j->rc, pt_last_error());
 }
 
@@ -209,6 +213,44 @@ static napi_value js_render(napi_env env, napi_callback_info info) {
     napi_create_reference(env, argv[1], 1, &j->refs[1]);
     napi_create_reference(env, argv[7], 1, &j->refs[2]);
     napi_create_string_utf8(env, "pt_render", NAPI_AUTO_LENGTH, &name);
+    CHECK_NAPI(env, napi_create_async_work(env, NULL, name, render_execute, render_complete, j, &j->work));
+    CHECK_NAPI(env, napi_queue_async_work(env, j->work));
+    return promise;
+}
+
+/* renderImage(scene, meta, frame0, nframes, stride, maxDepth, mode, Uint8Array rgba[W*H*4]) -> Promise<counters>:
+ * programEntry's displayed image, tone-mapped on the device (pt_render_image) */
+static napi_value js_render_image(napi_env env, napi_callback_info info) {
+    size_t argc = 8;
+    napi_value argv[8];
+    render_job* j = (render_job*)calloc(1, sizeof(render_job));
+    if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
+    float* meta;
+    size_t ml = 0, il = 0;
+    int ok = napi_get_cb_info(env, info, &argc, argv, NULL, NULL) == napi_ok && argc >= 8;
+    if (ok) {
+        j->scene = get_scene(env, argv[0]);
+        ok = j->scene && get_f32(env, argv[1], &meta, &ml) && ml >= 48;
+    }
+    if (ok) {
+        memcpy(j->meta, meta, sizeof j->meta);
+        ok = get_u32(env, argv[2], &j->frame0) && get_u32(env, argv[3], &j->nframes) && get_u32(env, argv[4], &j->stride) &&
+             get_i32(env, argv[5], &j->max_depth) && get_i32(env, argv[6], &j->mode) && get_u8(env, argv[7], &j->rgba, &il) &&
+             il == (size_t)j->meta[0] * (size_t)j->meta[1] * 4;
+    }
+    if (!ok) {
+        free(j);
+        napi_throw_type_error(env, NULL,
+                              "renderImage(scene, Float32Array meta[48], frame0, nframes, stride, maxDepth, mode, "
+                              "Uint8Array rgba[W*H*4])");
+        return NULL;
+    }
+    napi_value promise, name;
+    CHECK_NAPI(env, napi_create_promise(env, &j->deferred, &promise));
+    napi_create_reference(env, argv[0], 1, &j->refs[0]);
+    napi_create_reference(env, argv[1], 1, &j->refs[1]);
+    napi_create_reference(env, argv[7], 1, &j->refs[2]);
+    napi_create_string_utf8(env, "pt_render_image", NAPI_AUTO_LENGTH, &name);
     CHECK_NAPI(env, napi_create_async_work(env, NULL, name, render_execute, render_complete, j, &j->work));
     CHECK_NAPI(env, napi_queue_async_work(env, j->work));
     return promise;
@@ -343,6 +385,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"sceneInfo", NULL, js_scene_info, NULL, NULL, NULL, napi_enumerable, NULL},
         {"render", NULL, js_render, NULL, NULL, NULL, napi_enumerable, NULL},
         {"renderSync", NULL, js_render_sync, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"renderImage", NULL, js_render_image, NULL, NULL, NULL, napi_enumerable, NULL},
         {"frame", NULL, js_frame, NULL, NULL, NULL, napi_enumerable, NULL},
         {"tonemap", NULL, js_tonemap, NULL, NULL, NULL, napi_enumerable, NULL},
         {"profileEnable", NULL, js_profile_enable, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -32,7 +32,9 @@ function make_meta(screenDimension, camera_data, scene_description, time_elapsed
 /**
  * programEntry(screenDimension, primitive_data, camera_data, scene_description, options?)
  *   -> Promise<{accum: Float32Array(W*H*3), sample_runs, rgba: Uint8ClampedArray(W*H*4), counters, scene_info}>
- * options: {device=0, maxDepth=16, mode='auto', frame0=0, chunk=spp, onFrames(done, total)}
+ * options: {device=0, maxDepth=16, mode='auto', frame0=0, chunk=spp, onFrames(done, total), imageOnly=false}
+ * imageOnly: render and tone-map on the device in one call and return only {rgba, counters, ...}
+ * (no accumulator crosses PCIe; pt_render_image).
  * As in the reference only primitive_data[0] is rendered (program-raymarch.wgsl:31,33).
  */
 async function programEntry(screenDimension, primitive_data, camera_data, scene_description, options) {
@@ -47,6 +49,11 @@ async function programEntry(screenDimension, primitive_data, camera_data, scene_
     const counters = { samples: 0, ext_queries: 0, shadow_queries: 0, nodes: 0, tri_tests: 0, box_tests: 0 };
     const mode = typeof o.mode === 'number' ? o.mode : MODE[o.mode];
     if (mode === undefined) throw Error(`unknown mode ${o.mode}`);
+    if (o.imageOnly) {
+        const rgba = new Uint8ClampedArray(W * H * 4);
+        const c = await pt.renderImage(scene, meta, o.frame0, spp, 1, o.maxDepth, mode, new Uint8Array(rgba.buffer));
+        return { accum: null, sample_runs: spp, rgba, counters: c, scene_info: pt.sceneInfo(scene) };
+    }
     for (let done = 0; done < spp; done += chunk) {
         const n = Math.min(chunk, spp - done);
         const c = await pt.render(scene, meta, o.frame0 + done, n, 1, o.maxDepth, mode, accum);

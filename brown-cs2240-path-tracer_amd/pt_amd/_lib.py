@@ -92,9 +92,11 @@ def load_library():
     L.pt_profile_enable.argtypes = [p, i]
     L.pt_selftest_rcp.argtypes = [i, i, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
     L.pt_bvh_build.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
+    L.pt_tonemap_async.argtypes = [p, p, sz, u32, p, p]
+    L.pt_render_image.argtypes = [p, p, u32, u32, u32, i, i, p, p]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build"):
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image"):
         getattr(L, fn).restype = i
     _lib = L
     return L
@@ -180,6 +182,22 @@ class Scene:
         _check(self._lib.pt_render_async(self._h, _ptr(meta), frame0, nframes, stride, max_depth, mode,
                                          ctypes.c_void_p(d_accum_ptr), ctypes.c_void_p(d_counters_ptr or None),
                                          ctypes.c_void_p(stream_ptr or None)))
+
+    def render_image(self, meta, frame0: int, nframes: int, stride: int = 1, max_depth: int = -1,
+                     mode: int = MODE_AUTO, counters: bool = False):
+        """programEntry's displayed image in one call: RGBA u8 [H, W, 4] (device tone map)."""
+        meta = _f32(meta)
+        W, H = int(meta[0]), int(meta[1])
+        out = np.zeros((H, W, 4), np.uint8)
+        c = Counters()
+        _check(self._lib.pt_render_image(self._h, _ptr(meta), frame0, nframes, stride, max_depth, mode, _ptr(out),
+                                         ctypes.byref(c) if counters else None))
+        return (out, c.as_dict()) if counters else out
+
+    def tonemap_async(self, d_accum_ptr: int, npix: int, sample_runs: int, d_rgba_ptr: int, stream_ptr: int = 0):
+        """Device tone map between caller-owned device buffers (e.g. torch tensors)."""
+        _check(self._lib.pt_tonemap_async(self._h, ctypes.c_void_p(d_accum_ptr), npix, sample_runs,
+                                          ctypes.c_void_p(d_rgba_ptr), ctypes.c_void_p(stream_ptr or None)))
 
     def profile_enable(self, enable: bool = True):
         """Bracket every kernel launch of this scene with HIP events (discards earlier records)."""

@@ -122,6 +122,18 @@ int pt_frame_async(pt_scene* scene, const float meta[48], uint32_t t, int max_de
  * clamped; rgba[i*4+3] = 255. */
 int pt_tonemap(const float* accum, size_t npix, uint32_t sample_runs, uint8_t* rgba_out);
 
+/* The same display transform on the device (double, as the JS): d_accum f32 [npix][3] ->
+ * d_rgba u8 [npix][4], asynchronous on `stream` (hipStream_t; NULL = default), on the scene's
+ * device. */
+int pt_tonemap_async(pt_scene* scene, const float* d_accum, size_t npix, uint32_t sample_runs, uint8_t* d_rgba,
+                     void* stream);
+
+/* programEntry's result in one call: render frames frame0 + i*stride (i < nframes) into a
+ * zeroed accumulator and return the displayed image (tone map with sample_runs = nframes)
+ * as host RGBA u8 [H][W][4] — only the image crosses PCIe.  counters: nullable.  Blocking. */
+int pt_render_image(pt_scene* scene, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
+                    int max_depth, int mode, uint8_t* rgba_out, pt_counters* counters);
+
 /* Native BVH build (host only, no GPU): the reference's f64 builder
  * (src/ts-util/bvh.ts:14-188) and packer (src/packer.ts:83-137) in C++, byte-identical to them.
  * vertices: x,y,z per vertex in double — the values the host's JS holds after the CTM, not the
