@@ -202,9 +202,11 @@ __device__ __forceinline__ bool tri_hit(const TriRec& tr, const Ray& r, float& t
     float t = inv_det * dot(e2, sce1);
     t_out = t;
     const bool ok_det = !(det > -eps && det < eps);
-    const bool ok_u = !(u < 0.0f || u > 1.0f);
-    const bool ok_v = !(v < 0.0f || u + v > 1.0f);
-    return ok_det & ok_u & ok_v & (t > eps);
+    // !(u < 0) & !(v < 0) & !(u > 1) & !(u + v > 1), NaN passing each test as in the early-out
+    // chain: minNum/maxNum return the non-NaN operand, so the folded forms are the same
+    // predicate in two compares
+    const bool ok_uv = !(fminf(u, v) < 0.0f) & !(fmaxf(u, u + v) > 1.0f);
+    return ok_det & ok_uv & (t > eps);
 }
 template <bool FAST_RCP = false>
 __device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, const Ray& r, float& t_out) {
@@ -291,7 +293,84 @@ __device__ __forceinline__ bool trav_finished(const TravState& s) { return s.don
 // K = triangle tests per leaf turn: a lane with at least two triangles of its leaf pair left
 // runs two in sequence (same order, each against the closest t so far), which halves the
 // per-iteration overhead (scheduling ballots, decision, loop control) per test.
-template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false>
+// The three pieces of a lean step, for lanes in the matching state.
+template <bool COUNT>
+__device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
+    const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * s.node;
+    float4 a = np[0], b = np[1], c = np[2];
+    int4 d = reinterpret_cast<const int4*>(np)[3];
+    if (COUNT) { cnt.nodes++; cnt.box_tests += 2; }
+    s.ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
+    s.rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
+    const bool li = 0.0f < s.ld, ri = 0.0f < s.rd;
+    const bool lleaf = d.z >= 0, rleaf = d.w >= 0;
+    s.na = (li & lleaf) ? d.z : 0;
+    s.nt = s.na + ((ri & rleaf) ? d.w : 0);
+    s.la = d.x; s.lb = d.y; s.k = 0;
+    s.fl = ((li & !lleaf) ? TF_LINT : 0) | ((ri & !rleaf) ? TF_RINT : 0) | (s.nt > 0 ? TF_LEAF : 0);
+    return s.nt == 0;  // no leaf to test: decide now
+}
+
+template <int K, bool COUNT, bool FAST_RCP, bool PIPE>
+__device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
+    if constexpr (!PIPE) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const bool live = j == 0 || s.k < s.nt;  // the first test always is
+            if (j > 0 && !__any(live)) break;        // every lane's leaf pair is done
+            const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+            float t;
+            const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
+                              ((s.best_t < 0.0f) | (t < s.best_t));
+            s.best_t = take ? t : s.best_t;
+            s.best = take ? idx : s.best;
+            if (COUNT) cnt.tri_tests += live ? 1 : 0;
+            s.k += live ? 1 : 0;
+        }
+    } else {
+        // the record of test j+1 is loaded (LDS) while test j computes; a lane whose leaf
+        // pair ends loads a valid record it will not use
+        int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+        TriRec cur = load_tri(sc.tris, idx);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const bool live = j == 0 || s.k < s.nt;
+            if (j > 0 && !__any(live)) break;
+            const int k1 = s.k + 1;
+            const int idx1 = k1 < s.nt ? (k1 < s.na ? s.la + k1 : s.lb + (k1 - s.na)) : idx;
+            TriRec nxt;
+            if (j + 1 < K) nxt = load_tri(sc.tris, idx1);
+            float t;
+            const bool take = tri_hit<FAST_RCP>(cur, r, t) & live & ((s.best_t < 0.0f) | (t < s.best_t));
+            s.best_t = take ? t : s.best_t;
+            s.best = take ? idx : s.best;
+            if (COUNT) cnt.tri_tests += live ? 1 : 0;
+            s.k += live ? 1 : 0;
+            if (j + 1 < K) { cur = nxt; idx = idx1; }
+        }
+    }
+    const bool decide = s.k == s.nt;
+    s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
+    return decide;
+}
+
+__device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int stride) {
+    const bool tl = (s.fl & TF_LINT) && !((s.best_t > 0.0f) & (s.ld > s.best_t));
+    const bool tr = (s.fl & TF_RINT) && !((s.best_t > 0.0f) & (s.rd > s.best_t));
+    const bool pop = !tl & !tr;
+    stack[s.sp * stride] = s.la;  // a push keeps it, anything else leaves the slot free
+    const int top = stack[max(s.sp - 1, 0) * stride];
+    s.node = tr ? s.lb : (tl ? s.la : top);
+    s.fl |= (pop & (s.sp == 0)) ? TF_DONE : 0;
+    s.sp += (tl & tr) ? 1 : (pop ? -1 : 0);  // sp < 0 only once done
+}
+
+// IFIF = false: each iteration runs ONE unit type for the whole wave — a leaf turn (up to K
+// triangle tests) when leaf lanes >= node_bias * node lanes, else a node turn.  IFIF = true:
+// each iteration runs a node step for every lane that wants one and then the leaf loop for
+// every lane in a leaf (including lanes that just entered one), then one decision — no lane
+// waits a whole leaf turn for its node step.  Both keep each lane's unit order.
+template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false, bool IFIF = false>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
                                                int stride, Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE);
@@ -299,73 +378,18 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     const uint64_t want_node = __ballot(state == 0);
     if ((want_leaf | want_node) == 0) return false;
     bool decide = false;
-    if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
-        if (state == TF_LEAF) {
-            if constexpr (!PIPE) {
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    const bool live = j == 0 || s.k < s.nt;  // the first test always is
-                    if (j > 0 && !__any(live)) break;        // every lane's leaf pair is done
-                    const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
-                    float t;
-                    const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
-                                      ((s.best_t < 0.0f) | (t < s.best_t));
-                    s.best_t = take ? t : s.best_t;
-                    s.best = take ? idx : s.best;
-                    if (COUNT) cnt.tri_tests += live ? 1 : 0;
-                    s.k += live ? 1 : 0;
-                }
-            } else {
-                // the record of test j+1 is loaded (LDS) while test j computes; a lane whose
-                // leaf pair ends loads a valid record it will not use
-                int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
-                TriRec cur = load_tri(sc.tris, idx);
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    const bool live = j == 0 || s.k < s.nt;
-                    if (j > 0 && !__any(live)) break;
-                    const int k1 = s.k + 1;
-                    const int idx1 = k1 < s.nt ? (k1 < s.na ? s.la + k1 : s.lb + (k1 - s.na)) : idx;
-                    TriRec nxt;
-                    if (j + 1 < K) nxt = load_tri(sc.tris, idx1);
-                    float t;
-                    const bool take =
-                        tri_hit<FAST_RCP>(cur, r, t) & live & ((s.best_t < 0.0f) | (t < s.best_t));
-                    s.best_t = take ? t : s.best_t;
-                    s.best = take ? idx : s.best;
-                    if (COUNT) cnt.tri_tests += live ? 1 : 0;
-                    s.k += live ? 1 : 0;
-                    if (j + 1 < K) { cur = nxt; idx = idx1; }
-                }
-            }
-            decide = s.k == s.nt;
-            s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
+    if constexpr (IFIF) {
+        if (want_node && state == 0) decide = lean_node_unit<COUNT>(sc, r, s, cnt);
+        const bool in_leaf = (s.fl & (TF_LEAF | TF_DONE)) == TF_LEAF;
+        if (__any(in_leaf) && in_leaf) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE>(sc, r, s, cnt);
+    } else {
+        if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
+            if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE>(sc, r, s, cnt);
+        } else if (state == 0) {
+            decide = lean_node_unit<COUNT>(sc, r, s, cnt);
         }
-    } else if (state == 0) {
-        const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * s.node;
-        float4 a = np[0], b = np[1], c = np[2];
-        int4 d = reinterpret_cast<const int4*>(np)[3];
-        if (COUNT) { cnt.nodes++; cnt.box_tests += 2; }
-        s.ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
-        s.rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
-        const bool li = 0.0f < s.ld, ri = 0.0f < s.rd;
-        const bool lleaf = d.z >= 0, rleaf = d.w >= 0;
-        s.na = (li & lleaf) ? d.z : 0;
-        s.nt = s.na + ((ri & rleaf) ? d.w : 0);
-        s.la = d.x; s.lb = d.y; s.k = 0;
-        s.fl = ((li & !lleaf) ? TF_LINT : 0) | ((ri & !rleaf) ? TF_RINT : 0) | (s.nt > 0 ? TF_LEAF : 0);
-        decide = s.nt == 0;
     }
-    if (decide) {
-        const bool tl = (s.fl & TF_LINT) && !((s.best_t > 0.0f) & (s.ld > s.best_t));
-        const bool tr = (s.fl & TF_RINT) && !((s.best_t > 0.0f) & (s.rd > s.best_t));
-        const bool pop = !tl & !tr;
-        stack[s.sp * stride] = s.la;  // a push keeps it, anything else leaves the slot free
-        const int top = stack[max(s.sp - 1, 0) * stride];
-        s.node = tr ? s.lb : (tl ? s.la : top);
-        s.fl |= (pop & (s.sp == 0)) ? TF_DONE : 0;
-        s.sp += (tl & tr) ? 1 : (pop ? -1 : 0);  // sp < 0 only once done
-    }
+    if (decide) lean_decide(s, stack, stride);
     return true;
 }
 
@@ -381,10 +405,11 @@ struct TravSel<TRAV, true> { using type = TravLean; };
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
                                              int32_t* stack, int stride, Counters& cnt) {
-    if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal (SceneView::fast_rcp); + 20: pipelined leaf loads
+    if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 20: pipelined leaf loads; + 40: if-if step
         constexpr int B = TRAV % 10;
         constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
-        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, ((TRAV / 20) & 1) != 0>(sc, r, s, stack, stride, cnt);
+        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, ((TRAV / 20) & 1) != 0, ((TRAV / 40) & 1) != 0>(
+            sc, r, s, stack, stride, cnt);
     }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
     else return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);

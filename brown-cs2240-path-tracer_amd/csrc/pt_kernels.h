@@ -54,6 +54,7 @@ struct LaunchOpts {
     bool lds = true;       // stage the scene in LDS when it fits
     int fast_rcp = -1;     // rcp_rn for 1/det where SceneView::fast_rcp says it is exact: -1 per-pipeline default
     int pipe = -1;         // lean leaf turns load the next triangle while testing one: -1 per-pipeline default
+    int ifif = -1;         // lean step = node step for all lanes that want one, then leaf loop: -1 default
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 

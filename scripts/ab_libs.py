@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""A/B two (or more) builds of libpt_hip.so in ONE process on the same GPU, interleaved, so
+box-to-box clock differences cancel.  Each library is loaded privately (RTLD_LOCAL) and driven
+through the C ABI only.
+
+usage: ab_libs.py LIB [LIB ...] [--scene CornellBox] [--res 1024] [--spp 64] [--depth 8] [--rounds 5] [--mode 0]
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--scene", default="CornellBox")
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--mode", type=int, default=0)
+    a = ap.parse_args()
+    import torch  # one HIP runtime for the process (see pt_amd/_lib.py)
+    torch.cuda.init()
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.run(["node", os.path.join(ROOT, "brown-cs2240-path-tracer_amd", "node", "bin", "pt-pack.js"),
+                        os.path.join(ROOT, "scenes", "scene_assets", a.scene + ".xml"), td, "--width", str(a.res),
+                        "--height", str(a.res)], check=True, capture_output=True)
+        tri = np.fromfile(os.path.join(td, "triangle_data.f32"), np.float32)
+        bvh = np.fromfile(os.path.join(td, "bvh_data.f32"), np.float32)
+        meta = np.fromfile(os.path.join(td, "meta.f32"), np.float32)
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    runs = []
+    for path in a.libs:
+        L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+        L.pt_scene_create.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_void_p)]
+        L.pt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.pt_last_error.restype = ctypes.c_char_p
+        h = ctypes.c_void_p()
+        assert L.pt_scene_create(p(tri), tri.size, p(bvh), bvh.size, 0, ctypes.byref(h)) == 0, L.pt_last_error()
+        acc = np.zeros((a.res, a.res, 3), np.float32)
+        assert L.pt_render(h, p(meta), 0, a.spp, 1, a.depth, a.mode, p(acc), None) == 0, L.pt_last_error()  # warm-up
+        runs.append({"lib": path, "L": L, "h": h, "acc": acc, "ms": [], "ref": acc.copy()})
+    for _ in range(a.rounds):
+        for r in runs:
+            r["acc"][:] = 0
+            t = time.perf_counter()
+            assert r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode, p(r["acc"]), None) == 0
+            r["ms"].append((time.perf_counter() - t) * 1e3)
+    base = runs[0]["ref"]
+    for r in runs:
+        ms = float(np.median(r["ms"]))
+        print(json.dumps({"lib": r["lib"], "ms_median": round(ms, 3), "msamples_s": round(a.res * a.res * a.spp / ms / 1e3, 1),
+                          "same_bits_as_first": bool(np.array_equal(r["ref"].view(np.uint32), base.view(np.uint32)))}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -64,13 +64,16 @@ VARIANTS = {
     "mega_lean4_bias16_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "16", "PT_FASTRCP": "1"},
     "mega_lean2_bias8_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean2", "PT_NODE_BIAS": "8", "PT_FASTRCP": "1"},
     "wf_lean16_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_PIPE": "1"},
+    "wf_lean16_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_IFIF": "1"},
+    "wf_lean8_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_IFIF": "1"},
+    "wf_lean4_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_IFIF": "1"},
     "wf_lean8_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_PIPE": "1"},
     "wf_lean4_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_PIPE": "1"},
 }
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 
