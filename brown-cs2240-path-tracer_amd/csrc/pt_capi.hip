@@ -216,6 +216,7 @@ struct pt_scene {
     KernelProfiler prof;
     uint8_t* d_rgba = nullptr;  // pt_render_image scratch
     size_t rgba_cap = 0;
+    WfStreams ws;  // dual-stream wavefront: aux stream + fork/join events (created with d_wf)
 };
 
 namespace pt {
@@ -364,6 +365,11 @@ void pt_scene_destroy(pt_scene* s) {
     if (s->stream) { hipStreamSynchronize(s->stream); hipStreamDestroy(s->stream); }
     if (s->d_accum) hipFree(s->d_accum);
     if (s->d_wf) hipFree(s->d_wf);
+    for (int h = 0; h < 2; ++h) {
+        if (s->ws.aux[h]) { hipStreamSynchronize(s->ws.aux[h]); hipStreamDestroy(s->ws.aux[h]); }
+        if (s->ws.join[h]) hipEventDestroy(s->ws.join[h]);
+    }
+    if (s->ws.fork) hipEventDestroy(s->ws.fork);
     if (s->d_rgba) hipFree(s->d_rgba);
     if (s->d_mem) hipFree(s->d_mem);
     s->prof.destroy();
@@ -421,6 +427,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_FASTRCP")) lo.fast_rcp = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_PIPE")) lo.pipe = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
     return lo;
 }
@@ -438,7 +445,7 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     size_t oq[6];
     for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * n);
     const size_t o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(8 * n), o_hit = take(8 * n),
-                 o_rad = take(12 * n), o_ctl = take(4 * WF_CTL_WORDS);
+                 o_rad = take(12 * n), o_ctl = take(4 * 2 * WF_CTL_WORDS);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
     char* b = static_cast<char*>(s->d_wf);
     auto f4 = [&](size_t o) { return reinterpret_cast<float4*>(b + o); };
@@ -450,7 +457,15 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     w.hitq = reinterpret_cast<int2*>(b + o_hit);
     w.rad = reinterpret_cast<float*>(b + o_rad);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
-    if (hipMemset(w.ctl, 0, 4 * WF_CTL_WORDS) != hipSuccess) return fail(PT_ERR_HIP, "hipMemset wavefront control words");
+    if (hipMemset(w.ctl, 0, 4 * 2 * WF_CTL_WORDS) != hipSuccess) return fail(PT_ERR_HIP, "hipMemset wavefront control words");
+    if (!s->ws.aux[0]) {
+        if (hipStreamCreateWithFlags(&s->ws.aux[0], hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&s->ws.aux[1], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s->ws.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->ws.join[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->ws.join[1], hipEventDisableTiming) != hipSuccess)
+            return fail(PT_ERR_HIP, "creating the wavefront's streams");
+    }
     w.capacity = (uint32_t)n;
     return PT_OK;
 }
@@ -479,7 +494,7 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         int rc2 = ensure_wavefront(s, want);
         if (rc2 != PT_OK) return rc2;
         HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
-                                 stream));
+                                 stream, s->ws));
         return PT_OK;
     }
     HIP_TRY(launch_megakernel(lo, view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt, stream));
@@ -510,12 +525,16 @@ int pt_render_async(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t
 // After a synchronised call: a trace wave that hit kTraceWatchdog left a flag (cleared here).
 static int check_watchdog(pt_scene* s) {
     if (!s->d_wf) return PT_OK;
-    uint32_t flag = 0;
-    HIP_TRY(hipMemcpy(&flag, s->wf.ctl + WF_WATCHDOG, sizeof(flag), hipMemcpyDeviceToHost));
+    uint32_t flag = 0, h = 0;
+    for (; h < 2; ++h) {  // one control block per half of a dual-stream batch
+        HIP_TRY(hipMemcpy(&flag, s->wf.ctl + h * WF_CTL_WORDS + WF_WATCHDOG, sizeof(flag), hipMemcpyDeviceToHost));
+        if (flag) break;
+    }
     if (!flag) return PT_OK;
+    uint32_t* ctl = s->wf.ctl + h * WF_CTL_WORDS;
     uint32_t v[WF_SNAP_WORDS] = {};
-    HIP_TRY(hipMemcpy(v, s->wf.ctl + WF_SNAP, sizeof(v), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemset(s->wf.ctl + WF_WATCHDOG, 0, (WF_SNAP + WF_SNAP_WORDS - WF_WATCHDOG) * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(v, ctl + WF_SNAP, sizeof(v), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(ctl + WF_WATCHDOG, 0, (WF_SNAP + WF_SNAP_WORDS - WF_WATCHDOG) * sizeof(uint32_t)));
     char msg[320];
     std::snprintf(msg, sizeof(msg),
                   "wavefront trace gave up after kTraceWatchdog iterations (result invalid); first wave: count=%u "

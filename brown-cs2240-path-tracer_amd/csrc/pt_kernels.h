@@ -55,6 +55,7 @@ struct LaunchOpts {
     int fast_rcp = -1;     // rcp_rn for 1/det where SceneView::fast_rcp says it is exact: -1 per-pipeline default
     int pipe = -1;         // lean leaf turns load the next triangle while testing one: -1 per-pipeline default
     int ifif = -1;         // lean step = node step for all lanes that want one, then leaf loop: -1 default
+    int dual = -1;         // wavefront batch split in two halves on two streams: -1 default
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 
@@ -65,6 +66,7 @@ bool scene_fits_lds(const SceneView& sc);
 // a shade kernel writes the surviving path to its compacted slot of the other queue, so no
 // kernel gathers by path index.  Iterations alternate extension / shadow queues.
 enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_WATCHDOG = 2, WF_SNAP_CLAIM = 3, WF_SNAP = 8, WF_SNAP_WORDS = 16, WF_CTL_WORDS = 64 };
+// the control block holds WF_CTL_WORDS words per half of a dual-stream batch (wb_half)
 // iterations after which a trace wave gives up: it sets ctl[WF_WATCHDOG], the first such wave
 // leaves its scheduling state in ctl[WF_SNAP..], and the host reports an error
 constexpr uint32_t kTraceWatchdog = 1u << 24;
@@ -87,9 +89,16 @@ struct WfBuffers {
 };
 constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 
+// Dual-stream wavefront: two streams owned by the scene, created back to back so that HIP's
+// round-robin stream -> hardware-queue mapping puts them on different queues (a shared queue
+// serialises the halves), plus fork/join events with the caller's stream.  Null = one stream.
+struct WfStreams {
+    hipStream_t aux[2] = {nullptr, nullptr};
+    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+};
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
-                            Counters* cnt, hipStream_t stream);
+                            Counters* cnt, hipStream_t stream, const WfStreams& ws);
 
 // Megakernel render (accum=true: frames frame0 + i*stride, i < nframes, added to out) or one
 // dispatch (accum=false: raw radiance of salt frame0 written to out).

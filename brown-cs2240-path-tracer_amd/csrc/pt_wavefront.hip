@@ -316,6 +316,11 @@ __global__ __launch_bounds__(256) void k_wf_accum(const float* __restrict__ rad,
 // ---------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------
+#define HIP_RETURN_IF(expr)                      \
+    do {                                         \
+        const hipError_t e_ = (expr);            \
+        if (e_ != hipSuccess) return e_;         \
+    } while (0)
 template <bool LDS, int TRAV, bool COUNT>
 static int trace_blocks(size_t lds_bytes) {
     static int cached = 0;
@@ -333,39 +338,82 @@ static int trace_blocks(size_t lds_bytes) {
     return b;
 }
 
+// Paths [0, P) of half h of a batch: queue entries from h * capacity/2, radiance from
+// `rad_off` floats (so the two halves' radiance is contiguous in frame order), control words
+// from h * WF_CTL_WORDS.
+static WfBuffers wb_half(const WfBuffers& wb, int h, size_t rad_off) {
+    WfBuffers v = wb;
+    const size_t e = (size_t)h * (wb.capacity / 2);
+    for (WfQueue* q : {&v.ext, &v.shd}) { q->ray += 2 * e; q->q2 += e; q->q3 += e; }
+    v.sp0 += e; v.sp1 += e; v.sp2 += e; v.hitq += e;
+    v.rad += rad_off;
+    v.ctl += h * WF_CTL_WORDS;
+    v.capacity = wb.capacity / 2;
+    return v;
+}
+
 template <bool LDS, int TRAV, bool COUNT>
 static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const WfBuffers& wb, uint32_t frame0,
                               uint32_t nframes, uint32_t stride, bool accum, float* out, Counters* cnt,
-                              hipStream_t stream) {
+                              hipStream_t stream, const WfStreams& ws) {
     const uint32_t npix = fp.width * fp.height;
-    const uint32_t F = std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
+    // two halves on two streams when a half holds at least a frame: the trace of one half
+    // (VALU/LDS-bound) runs beside the shading of the other (HBM-bound)
+    const bool dual = ws.aux[0] != nullptr && nframes >= 2 && wb.capacity / 2 >= npix;
+    const uint32_t F = dual ? 2 * std::min<uint32_t>((nframes + 1) / 2, (uint32_t)(wb.capacity / 2 / npix))
+                            : std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
     const size_t lds = (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * kStageBytes + (LDS ? sc.span_bytes : 0);
     int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
     if (const char* e = std::getenv("PT_WF_TRACE_BLOCKS")) tblocks = std::max(1, std::min(tblocks, std::atoi(e)));  // tests
     const int iters = 2 * (fp.max_depth + 1);
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
-        const uint32_t P = Fb * npix;
-        const int sblocks = (int)((P + kShadeBlock - 1) / kShadeBlock);
-        PT_LAUNCH(KID_WF_GENERATE, stream, (k_wf_generate<COUNT>), dim3((P + 255) / 256), dim3(256), 0, stream, fp, wb, frame0, stride, fb,
-                           P, !accum, cnt);
+        const uint32_t FA = dual && Fb >= 2 ? (Fb + 1) / 2 : Fb, FB = Fb - FA;
+        const WfBuffers A = FB ? wb_half(wb, 0, 0) : wb;
+        const WfBuffers B = wb_half(wb, 1, (size_t)FA * npix * 3);
+        struct Half { const WfBuffers* w; uint32_t fbase, P; hipStream_t st; };
+        const int nh = FB ? 2 : 1;
+        Half hv[2] = {{&A, fb, FA * npix, FB ? ws.aux[0] : stream}, {&B, fb + FA, FB * npix, ws.aux[1]}};
+        if (FB) {
+            HIP_RETURN_IF(hipEventRecord(ws.fork, stream));
+            for (int h = 0; h < 2; ++h) HIP_RETURN_IF(hipStreamWaitEvent(ws.aux[h], ws.fork, 0));
+        }
+        for (int h = 0; h < nh; ++h)
+            PT_LAUNCH(KID_WF_GENERATE, hv[h].st, (k_wf_generate<COUNT>), dim3((hv[h].P + 255) / 256), dim3(256), 0, hv[h].st,
+                      fp, *hv[h].w, frame0, stride, hv[h].fbase, hv[h].P, !accum, cnt);
         int in_q = 0;
         for (int it = 0; it < iters; ++it) {
-            PT_LAUNCH(KID_WF_TRACE, stream, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, stream, sc, wb, in_q, cnt);
-            if ((it & 1) == 0)
-                PT_LAUNCH(KID_WF_SHADE_EXT, stream, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, stream, sc, fp, wb, cnt);
-            else
-                PT_LAUNCH(KID_WF_SHADE_SHADOW, stream, (k_wf_shade<false, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, stream, sc, fp, wb, cnt);
+            for (int h = 0; h < nh; ++h) {  // interleaved issue: the halves' kernels can overlap
+                const hipStream_t st = hv[h].st;
+                const WfBuffers& w = *hv[h].w;
+                const int sblocks = (int)((hv[h].P + kShadeBlock - 1) / kShadeBlock);
+                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc, w,
+                          in_q, cnt);
+                if ((it & 1) == 0)
+                    PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
+                              w, cnt);
+                else
+                    PT_LAUNCH(KID_WF_SHADE_SHADOW, st, (k_wf_shade<false, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc,
+                              fp, w, cnt);
+            }
             in_q ^= 1;
         }
-        PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix, Fb, accum);
+        if (FB) {
+            for (int h = 0; h < 2; ++h) {
+                HIP_RETURN_IF(hipEventRecord(ws.join[h], ws.aux[h]));
+                HIP_RETURN_IF(hipStreamWaitEvent(stream, ws.join[h], 0));
+            }
+        }
+        PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix, Fb,
+                  accum);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
-                            Counters* cnt, hipStream_t stream) {
+                            Counters* cnt, hipStream_t stream, const WfStreams& ws_in) {
+    const WfStreams ws = lo.dual != 0 ? ws_in : WfStreams{};  // dual by default: +14 % measured (in-process A/B)
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     if (sc.node_bias <= 0) sc.node_bias = 8;  // measured best with lean16 (1 = majority: -13 %)
@@ -380,8 +428,8 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
                      ((base >= 3 && fast && ifif && !pipe) ? 40 : 0);
 #define WF(L, T)                                                                                               \
     if (trav == T) {                                                                                           \
-        if (count) return wf_render_t<L, T, true>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream); \
-        return wf_render_t<L, T, false>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream);         \
+        if (count) return wf_render_t<L, T, true>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream, ws); \
+        return wf_render_t<L, T, false>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream, ws);         \
     }
     if (lds) {
         WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7) WF(true, 8)

@@ -3,7 +3,10 @@
 box-to-box clock differences cancel.  Each library is loaded privately (RTLD_LOCAL) and driven
 through the C ABI only.
 
-usage: ab_libs.py LIB [LIB ...] [--scene CornellBox] [--res 1024] [--spp 64] [--depth 8] [--rounds 5] [--mode 0]
+usage: ab_libs.py LIB[@ENV=VAL,ENV=VAL] ... [--scene CornellBox] [--res 1024] [--spp 64] [--depth 8]
+                 [--rounds 5] [--mode 0]
+The optional @ENV list is set around that variant's renders (the library reads its PT_* A/B
+switches on every call), so one build can be compared with itself under different switches.
 """
 import argparse
 import ctypes
@@ -41,8 +44,26 @@ def main():
         meta = np.fromfile(os.path.join(td, "meta.f32"), np.float32)
     p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     runs = []
-    for path in a.libs:
-        L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+    loaded = {}
+
+    def with_env(env, fn):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            return fn()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    for spec in a.libs:
+        path, _, envs = spec.partition("@")
+        env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
+        if path not in loaded:
+            loaded[path] = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+        L = loaded[path]
         L.pt_scene_create.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_void_p)]
         L.pt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -51,13 +72,16 @@ def main():
         h = ctypes.c_void_p()
         assert L.pt_scene_create(p(tri), tri.size, p(bvh), bvh.size, 0, ctypes.byref(h)) == 0, L.pt_last_error()
         acc = np.zeros((a.res, a.res, 3), np.float32)
-        assert L.pt_render(h, p(meta), 0, a.spp, 1, a.depth, a.mode, p(acc), None) == 0, L.pt_last_error()  # warm-up
-        runs.append({"lib": path, "L": L, "h": h, "acc": acc, "ms": [], "ref": acc.copy()})
+        rc = with_env(env, lambda: L.pt_render(h, p(meta), 0, a.spp, 1, a.depth, a.mode, p(acc), None))  # warm-up
+        assert rc == 0, L.pt_last_error()
+        runs.append({"lib": spec, "L": L, "h": h, "acc": acc, "ms": [], "ref": acc.copy(), "env": env})
     for _ in range(a.rounds):
         for r in runs:
             r["acc"][:] = 0
             t = time.perf_counter()
-            assert r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode, p(r["acc"]), None) == 0
+            rc = with_env(r["env"], lambda: r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode, p(r["acc"]),
+                                                             None))
+            assert rc == 0
             r["ms"].append((time.perf_counter() - t) * 1e3)
     base = runs[0]["ref"]
     for r in runs:

@@ -73,7 +73,7 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

@@ -44,6 +44,8 @@ KERNELS = {
     "mega_lean4_majority": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "1"},
     "wavefront_lean16_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_PIPE": "1"},
     "wavefront_lean8_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_IFIF": "1"},
+    "wavefront_single_stream": {"PT_KERNEL": "wavefront", "PT_DUAL": "0"},
+    "wavefront_dual_1block": {"PT_KERNEL": "wavefront", "PT_DUAL": "1", "PT_WF_TRACE_BLOCKS": "1"},
     "wavefront_3blocks_flat1": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1", "PT_WF_TRACE_BLOCKS": "3"},
 }
 
@@ -51,7 +53,7 @@ KERNELS = {
 @pytest.fixture(params=list(KERNELS))
 def kernel(request, monkeypatch):
     """Every kernel variant must give the same bits."""
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
         monkeypatch.delenv(k, raising=False)
     for k, v in KERNELS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -238,7 +240,7 @@ def test_invalid_scene_rejected():
 # kernel timing (pt_profile_*) and the AUTO policy (megakernel below 2^20 paths per call)
 # ---------------------------------------------------------------------------------------------
 def test_profile_records_every_launch(packed, monkeypatch):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(64, 64)
@@ -262,7 +264,7 @@ def test_profile_records_every_launch(packed, monkeypatch):
 
 
 def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
@@ -280,7 +282,7 @@ def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
 def test_auto_large_render_matches_megakernel(packed, monkeypatch):
     """At the AUTO switch point the wavefront result equals the megakernel's bit for bit
     (both equal the oracle on the smaller cases above)."""
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(512, 512)
