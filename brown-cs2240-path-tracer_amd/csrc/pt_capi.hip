@@ -219,6 +219,12 @@ struct pt_scene {
     WfStreams ws;  // dual-stream wavefront: aux stream + fork/join events (created with d_wf)
 };
 
+// The dual-stream wavefront needs its two streams on hardware queues of their own; with HIP's
+// default of 4 queues per process they share one with the caller's streams and the halves
+// serialise (bench: 962 vs 1238 Msamples/s with 8).  Ask for 8 when the library is loaded before
+// the HIP runtime starts (a value the process already set wins; after HIP is up this is inert).
+__attribute__((constructor)) static void pt_hw_queues() { setenv("GPU_MAX_HW_QUEUES", "8", 0); }
+
 namespace pt {
 thread_local KernelProfiler* t_prof = nullptr;
 
@@ -368,6 +374,7 @@ void pt_scene_destroy(pt_scene* s) {
     for (int h = 0; h < 2; ++h) {
         if (s->ws.aux[h]) { hipStreamSynchronize(s->ws.aux[h]); hipStreamDestroy(s->ws.aux[h]); }
         if (s->ws.join[h]) hipEventDestroy(s->ws.join[h]);
+        if (s->ws.traced[h]) hipEventDestroy(s->ws.traced[h]);
     }
     if (s->ws.fork) hipEventDestroy(s->ws.fork);
     if (s->d_rgba) hipFree(s->d_rgba);
@@ -428,6 +435,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_PIPE")) lo.pipe = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
     return lo;
 }
@@ -463,7 +471,9 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
             hipStreamCreateWithFlags(&s->ws.aux[1], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&s->ws.fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s->ws.join[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ws.join[1], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&s->ws.join[1], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->ws.traced[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->ws.traced[1], hipEventDisableTiming) != hipSuccess)
             return fail(PT_ERR_HIP, "creating the wavefront's streams");
     }
     w.capacity = (uint32_t)n;

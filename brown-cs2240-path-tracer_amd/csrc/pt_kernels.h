@@ -56,6 +56,7 @@ struct LaunchOpts {
     int pipe = -1;         // lean leaf turns load the next triangle while testing one: -1 per-pipeline default
     int ifif = -1;         // lean step = node step for all lanes that want one, then leaf loop: -1 default
     int dual = -1;         // wavefront batch split in two halves on two streams: -1 default
+    int stagger = -1;      // dual halves' traces alternate instead of overlapping: -1 default (off)
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 
@@ -95,6 +96,8 @@ constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 struct WfStreams {
     hipStream_t aux[2] = {nullptr, nullptr};
     hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+    hipEvent_t traced[2] = {nullptr, nullptr};  // "half h finished its trace i" (staggering)
+    bool stagger = false;
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

@@ -381,14 +381,20 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
         for (int h = 0; h < nh; ++h)
             PT_LAUNCH(KID_WF_GENERATE, hv[h].st, (k_wf_generate<COUNT>), dim3((hv[h].P + 255) / 256), dim3(256), 0, hv[h].st,
                       fp, *hv[h].w, frame0, stride, hv[h].fbase, hv[h].P, !accum, cnt);
+        // Optional staggering (PT_STAGGER=1; measured slower: 1026 vs 1231 Msamples/s): B's trace
+        // i waits for A's trace i and A's trace i+1 for B's trace i, so the persistent trace
+        // kernels never share the machine.  Default: the halves' kernels overlap freely.
+        const bool stagger = nh == 2 && ws.stagger;
         int in_q = 0;
         for (int it = 0; it < iters; ++it) {
-            for (int h = 0; h < nh; ++h) {  // interleaved issue: the halves' kernels can overlap
+            for (int h = 0; h < nh; ++h) {
                 const hipStream_t st = hv[h].st;
                 const WfBuffers& w = *hv[h].w;
                 const int sblocks = (int)((hv[h].P + kShadeBlock - 1) / kShadeBlock);
+                if (stagger && (h == 1 || it > 0)) HIP_RETURN_IF(hipStreamWaitEvent(st, ws.traced[1 - h], 0));
                 PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc, w,
                           in_q, cnt);
+                if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
                 if ((it & 1) == 0)
                     PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
                               w, cnt);
@@ -413,7 +419,8 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
                             Counters* cnt, hipStream_t stream, const WfStreams& ws_in) {
-    const WfStreams ws = lo.dual != 0 ? ws_in : WfStreams{};  // dual by default: +14 % measured (in-process A/B)
+    WfStreams ws = lo.dual != 0 ? ws_in : WfStreams{};  // dual by default: +15 % measured (in-process A/B)
+    ws.stagger = lo.stagger > 0;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     if (sc.node_bias <= 0) sc.node_bias = 8;  // measured best with lean16 (1 = majority: -13 %)

@@ -6,6 +6,11 @@ import os
 
 import numpy as np
 
+# The dual-stream wavefront wants its two streams on hardware queues of their own; HIP reads
+# this once, when its runtime starts (torch may start it on import, below), so set it first.
+# A value the process already set wins (csrc/pt_capi.hip does the same for non-Python hosts).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _LIB_FILE = os.path.join(_PKG_ROOT, "lib", "libpt_hip.so")
 

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--async-torch", action="store_true", help="pt_render_async on a torch stream (as bench.py)")
     a = ap.parse_args()
     import torch  # one HIP runtime for the process (see pt_amd/_lib.py)
     torch.cuda.init()
@@ -69,20 +70,40 @@ def main():
         L.pt_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.pt_last_error.restype = ctypes.c_char_p
+        L.pt_render_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         h = ctypes.c_void_p()
         assert L.pt_scene_create(p(tri), tri.size, p(bvh), bvh.size, 0, ctypes.byref(h)) == 0, L.pt_last_error()
         acc = np.zeros((a.res, a.res, 3), np.float32)
         rc = with_env(env, lambda: L.pt_render(h, p(meta), 0, a.spp, 1, a.depth, a.mode, p(acc), None))  # warm-up
         assert rc == 0, L.pt_last_error()
         runs.append({"lib": spec, "L": L, "h": h, "acc": acc, "ms": [], "ref": acc.copy(), "env": env})
+    if a.async_torch:
+        for r in runs:
+            r["stream"] = torch.cuda.Stream()
+            r["dacc"] = torch.zeros((a.res, a.res, 3), dtype=torch.float32, device="cuda")
     for _ in range(a.rounds):
         for r in runs:
-            r["acc"][:] = 0
-            t = time.perf_counter()
-            rc = with_env(r["env"], lambda: r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode, p(r["acc"]),
-                                                             None))
+            if a.async_torch:
+                st = r["stream"]
+                with torch.cuda.stream(st):
+                    r["dacc"].zero_()
+                st.synchronize()
+                t = time.perf_counter()
+                rc = with_env(r["env"], lambda: r["L"].pt_render_async(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode,
+                                                                      ctypes.c_void_p(r["dacc"].data_ptr()), None,
+                                                                      ctypes.c_void_p(st.cuda_stream)))
+                st.synchronize()
+            else:
+                r["acc"][:] = 0
+                t = time.perf_counter()
+                rc = with_env(r["env"], lambda: r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode,
+                                                                 p(r["acc"]), None))
             assert rc == 0
             r["ms"].append((time.perf_counter() - t) * 1e3)
+    if a.async_torch:
+        for r in runs:
+            r["ref"] = r["dacc"].cpu().numpy()
     base = runs[0]["ref"]
     for r in runs:
         ms = float(np.median(r["ms"]))

@@ -257,8 +257,10 @@ def test_profile_records_every_launch(packed, monkeypatch):
         assert s.profile_read() == {}
     assert set(mega) == {"k_regen"} and mega["k_regen"]["launches"] == 1
     assert set(wf) == {"k_wf_generate", "k_wf_trace", "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum"}
-    assert wf["k_wf_trace"]["launches"] == 2 * (depth + 1)  # one batch: 4 frames of 64^2 fit
-    assert wf["k_wf_shade_ext"]["launches"] == wf["k_wf_shade_shadow"]["launches"] == depth + 1
+    # one batch (4 frames of 64^2 fit) in two halves on two streams (dual-stream wavefront)
+    assert wf["k_wf_trace"]["launches"] == 2 * 2 * (depth + 1)
+    assert wf["k_wf_generate"]["launches"] == 2 and wf["k_wf_accum"]["launches"] == 1
+    assert wf["k_wf_shade_ext"]["launches"] == wf["k_wf_shade_shadow"]["launches"] == 2 * (depth + 1)
     for v in list(mega.values()) + list(wf.values()):
         assert 0.0 < v["min_ms"] <= v["avg_ms"] <= v["max_ms"] and v["total_ms"] > 0.0
 
