@@ -272,6 +272,14 @@ int pt_profile_enable(pt_scene* s, int enable) {
     return PT_OK;
 }
 
+int pt_profile_select(pt_scene* s, const char* kernel) {
+    if (!s) return fail(PT_ERR_INVALID, "null scene");
+    if (!kernel) { s->prof.only = -1; return PT_OK; }
+    for (int k = 0; k < KID_COUNT; ++k)
+        if (!std::strcmp(kernel, kernel_name(k))) { s->prof.only = k; return PT_OK; }
+    return fail(PT_ERR_INVALID, "unknown kernel name");
+}
+
 int pt_profile_read(pt_scene* s, pt_kernel_time* out, int max_entries, int* n_out) {
     if (!s || !n_out || (max_entries > 0 && !out)) return fail(PT_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(s->device));
@@ -336,8 +344,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     if (up(o_nodes, L.nodes.data(), L.nodes.size() * sizeof(Node)) != hipSuccess ||
         up(o_tris, L.tris.data(), L.tris.size() * sizeof(Tri)) != hipSuccess ||
         up(o_mats, L.mats.data(), L.mats.size() * sizeof(Material)) != hipSuccess ||
-        up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess ||
-        hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -446,7 +453,7 @@ constexpr uint64_t kWfTargetPaths = 8ull << 20;
 int ensure_wavefront(pt_scene* s, uint64_t paths) {
     if (s->d_wf && s->wf.capacity >= paths) return PT_OK;
     if (paths > 0x7fffffffull) return fail(PT_ERR_INVALID, "image too large for one wavefront batch");
-    if (s->d_wf) { hipStreamSynchronize(s->stream); hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; }
+    if (s->d_wf) { hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; }
     const size_t n = paths;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
@@ -553,6 +560,17 @@ static int check_watchdog(pt_scene* s) {
     return fail(PT_ERR_HIP, msg);
 }
 
+// The blocking calls' own stream, created on first use: asynchronous callers never pay for a
+// stream (HIP multiplexes every stream of the process onto GPU_MAX_HW_QUEUES hardware queues,
+// and an idle extra stream can push the dual-stream wavefront's two onto one queue).
+static int blocking_stream(pt_scene* s) {
+    if (!s->stream && hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        s->stream = nullptr;
+        return fail(PT_ERR_HIP, "hipStreamCreate");
+    }
+    return PT_OK;
+}
+
 int pt_render(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
               int max_depth, int mode, float* accum, pt_counters* counters) {
     if (!s || !accum || !meta) return fail(PT_ERR_INVALID, "null argument");
@@ -561,7 +579,7 @@ int pt_render(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nfram
     if (rc != PT_OK) return rc;
     const size_t n = (size_t)fp.width * fp.height * 3;
     HIP_TRY(hipSetDevice(s->device));
-    if ((rc = ensure_accum(s, n)) != PT_OK) return rc;
+    if ((rc = ensure_accum(s, n)) != PT_OK || (rc = blocking_stream(s)) != PT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(s->d_accum, accum, n * sizeof(float), hipMemcpyHostToDevice, s->stream));
     if (counters) HIP_TRY(hipMemsetAsync(s->d_counters, 0, sizeof(Counters), s->stream));
     rc = render_impl(s, meta, frame0, nframes, frame_stride, max_depth, mode, true, s->d_accum,
@@ -586,7 +604,7 @@ int pt_frame(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float
     if (rc != PT_OK) return rc;
     const size_t n = (size_t)fp.width * fp.height * 3;
     HIP_TRY(hipSetDevice(s->device));
-    if ((rc = ensure_accum(s, n)) != PT_OK) return rc;
+    if ((rc = ensure_accum(s, n)) != PT_OK || (rc = blocking_stream(s)) != PT_OK) return rc;
     rc = render_impl(s, meta, t, 1, 1, max_depth, PT_MODE_AUTO, false, s->d_accum, nullptr, s->stream);
     if (rc != PT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(radiance, s->d_accum, n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
@@ -615,7 +633,7 @@ int pt_render_image(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t
     if (rc != PT_OK) return rc;
     const size_t npix = (size_t)fp.width * fp.height;
     HIP_TRY(hipSetDevice(s->device));
-    if ((rc = ensure_accum(s, 3 * npix)) != PT_OK) return rc;
+    if ((rc = ensure_accum(s, 3 * npix)) != PT_OK || (rc = blocking_stream(s)) != PT_OK) return rc;
     if (s->rgba_cap < 4 * npix) {
         if (s->d_rgba) hipFree(s->d_rgba);
         s->d_rgba = nullptr;

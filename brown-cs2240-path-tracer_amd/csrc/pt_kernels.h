@@ -29,6 +29,8 @@ struct KernelProfiler {
     struct Rec { int kid; hipEvent_t a, b; };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
+    int only = -1;  // record only this kernel id (pt_profile_select); -1 = all
+    bool open = false;  // the last start() recorded (stop() closes it)
     hipEvent_t take();
     void start(int kid, hipStream_t s);
     void stop(hipStream_t s);
@@ -38,9 +40,11 @@ struct KernelProfiler {
 extern thread_local KernelProfiler* t_prof;
 #define PT_LAUNCH(KID, STREAM, ...)                                  \
     do {                                                             \
-        if (::pt::t_prof) ::pt::t_prof->start((KID), (STREAM));      \
+        ::pt::KernelProfiler* p_ = ::pt::t_prof;                     \
+        if (p_ && p_->only >= 0 && p_->only != (KID)) p_ = nullptr;  \
+        if (p_) p_->start((KID), (STREAM));                          \
         hipLaunchKernelGGL(__VA_ARGS__);                             \
-        if (::pt::t_prof) ::pt::t_prof->stop(STREAM);                \
+        if (p_) p_->stop(STREAM);                                    \
     } while (0)
 
 constexpr int kMegaBlock = 256;

@@ -95,13 +95,14 @@ def load_library():
     L.pt_tonemap.argtypes = [p, sz, u32, p]
     L.pt_selftest_math.argtypes = [i, i, p, p, p, sz]
     L.pt_profile_enable.argtypes = [p, i]
+    L.pt_profile_select.argtypes = [p, ctypes.c_char_p]
     L.pt_selftest_rcp.argtypes = [i, i, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
     L.pt_bvh_build.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_tonemap_async.argtypes = [p, p, sz, u32, p, p]
     L.pt_render_image.argtypes = [p, p, u32, u32, u32, i, i, p, p]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image"):
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image"):
         getattr(L, fn).restype = i
     _lib = L
     return L
@@ -207,6 +208,10 @@ class Scene:
     def profile_enable(self, enable: bool = True):
         """Bracket every kernel launch of this scene with HIP events (discards earlier records)."""
         _check(self._lib.pt_profile_enable(self._h, 1 if enable else 0))
+
+    def profile_select(self, kernel: str | None = None):
+        """Record only `kernel` ("k_wf_trace", "k_regen", ...); None = every kernel."""
+        _check(self._lib.pt_profile_select(self._h, kernel.encode() if kernel else None))
 
     def profile_read(self) -> dict:
         """{kernel name: {"launches", "total_ms", "avg_ms", "min_ms", "max_ms"}} since profile_enable()."""

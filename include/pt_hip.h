@@ -149,6 +149,9 @@ int pt_bvh_build(const double* vertices, size_t vertex_count, const int32_t* tri
  * records.  pt_profile_read waits for the recorded events and writes per-kernel totals
  * (at most max_entries; *n_out = entries written). */
 int pt_profile_enable(pt_scene* scene, int enable);
+/* Record only the launches of one kernel ("k_wf_trace", ...; NULL = all, the default): fewer
+ * events in the stream when only one kernel's duration is wanted. */
+int pt_profile_select(pt_scene* scene, const char* kernel);
 int pt_profile_read(pt_scene* scene, pt_kernel_time* out, int max_entries, int* n_out);
 
 /* Numerics self-test: out[i] = f(a[i], b[i]) evaluated ON THE DEVICE with the core's
