@@ -4,7 +4,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <array>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -53,6 +55,9 @@ struct HostLayout {
     std::vector<Tri> tris;
     std::vector<Material> mats;
     std::vector<Light> lights;
+    std::vector<uint64_t> lmask;  // mailbox scenes: uid set per leaf, indexed by first record
+    int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
+    bool mailbox = false;
     pt_scene_info info{};
     int32_t ntri = 0;
     bool fast_rcp = false;  // SceneView::fast_rcp
@@ -94,6 +99,9 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
     if (bvh[6] == 1.0f) return fail(PT_ERR_SCENE, "BVH root is a leaf (the reference never builds one)");
     struct Item { int32_t off; int32_t node; int32_t depth; };
     std::vector<Item> work;
+    // mailbox bookkeeping: each record's leaf entry (i0, i1, i2, material) and the leaves
+    std::vector<std::array<int32_t, 4>> entry;
+    std::vector<std::pair<int32_t, int32_t>> leaf_ranges;  // (first record, count)
     L.nodes.push_back(Node{});
     work.push_back({6, 0, 0});
     const size_t node_cap = bvh_len / 17 + 1;
@@ -135,8 +143,11 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                         t.e2[q] = v2[q] - v0[q];  // :7
                     }
                     t.mat = mat;
+                    t.uid = -1;
                     L.tris.push_back(t);
+                    entry.push_back({wgsl_i32(e[0]), wgsl_i32(e[1]), wgsl_i32(e[2]), mat});
                 }
+                leaf_ranges.emplace_back(refs[side], n);
                 L.info.leaves++;
                 L.info.leaf_refs += (uint32_t)n;
                 L.info.max_leaf = std::max<uint32_t>(L.info.max_leaf, (uint32_t)n);
@@ -152,6 +163,39 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
         L.nodes[(size_t)it.node] = nd;
     }
     L.info.nodes = (uint32_t)L.nodes.size();
+    // Mailboxing: a leaf entry tested twice by one query gives the same t both
+    // times and the closest-hit update is strict-<, so repeats never change the result.  With
+    // at most 64 distinct entries a query keeps the set it has tested in one 64-bit mask.
+    // uids follow first appearance (PT_MB_UID_ORDER=reverse numbers them backwards: tests
+    // use it to exercise the tie-break of the uid-ordered leaf loop).
+    {
+        std::map<std::array<int32_t, 4>, int32_t> ids;
+        std::vector<int32_t> uid(entry.size());
+        std::vector<size_t> first;
+        for (size_t r = 0; r < entry.size(); ++r) {
+            auto it = ids.find(entry[r]);
+            if (it == ids.end()) {
+                it = ids.emplace(entry[r], (int32_t)first.size()).first;
+                first.push_back(r);
+            }
+            uid[r] = it->second;
+        }
+        const int32_t U = (int32_t)first.size();
+        L.mailbox = U >= 1 && U <= 64;
+        if (L.mailbox) {
+            const char* order = std::getenv("PT_MB_UID_ORDER");
+            const bool rev = order && !std::strcmp(order, "reverse");
+            for (auto& u : uid) u = rev ? U - 1 - u : u;
+            for (size_t r = 0; r < entry.size(); ++r) L.tris[r].uid = uid[r];
+            L.mb_base = (int32_t)L.tris.size();
+            std::vector<Tri> uniq((size_t)U);
+            for (size_t k = 0; k < first.size(); ++k) uniq[(size_t)uid[first[k]]] = L.tris[first[k]];
+            L.tris.insert(L.tris.end(), uniq.begin(), uniq.end());
+            L.lmask.assign(std::max<size_t>(1, entry.size()), 0);
+            for (const auto& lr : leaf_ranges)
+                for (int32_t k = 0; k < lr.second; ++k) L.lmask[(size_t)lr.first] |= 1ull << uid[(size_t)(lr.first + k)];
+        }
+    }
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
     // a reflection/refraction of unit vectors; non-finite ones give no hit on either path)
     double emax = 0.0;
@@ -334,7 +378,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_tris = align_up(o_nodes + L.nodes.size() * sizeof(Node), 256);
     const size_t o_mats = align_up(o_tris + std::max<size_t>(1, L.tris.size()) * sizeof(Tri), 256);
     const size_t o_lights = align_up(o_mats + L.mats.size() * sizeof(Material), 256);
-    const size_t o_cnt = align_up(o_lights + L.lights.size() * sizeof(Light), 256);
+    const size_t o_lmask = align_up(o_lights + L.lights.size() * sizeof(Light), 16);
+    const size_t o_cnt = align_up(o_lmask + L.lmask.size() * sizeof(uint64_t), 256);
     const size_t total = align_up(o_cnt + sizeof(Counters), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
@@ -344,7 +389,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     if (up(o_nodes, L.nodes.data(), L.nodes.size() * sizeof(Node)) != hipSuccess ||
         up(o_tris, L.tris.data(), L.tris.size() * sizeof(Tri)) != hipSuccess ||
         up(o_mats, L.mats.data(), L.mats.size() * sizeof(Material)) != hipSuccess ||
-        up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess) {
+        up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess ||
+        up(o_lmask, L.lmask.data(), L.lmask.size() * sizeof(uint64_t)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -364,7 +410,11 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.off_tris = (uint32_t)(o_tris - o_nodes);
     s->view.off_mats = (uint32_t)(o_mats - o_nodes);
     s->view.off_lights = (uint32_t)(o_lights - o_nodes);
-    s->view.span_bytes = (uint32_t)(o_lights + L.lights.size() * sizeof(Light) - o_nodes);
+    s->view.off_lmask = (uint32_t)(o_lmask - o_nodes);
+    s->view.lmask = reinterpret_cast<const uint64_t*>(base + o_lmask);
+    s->view.mailbox = L.mailbox ? 1 : 0;
+    s->view.mb_base = L.mb_base;
+    s->view.span_bytes = (uint32_t)align_up(o_lmask + L.lmask.size() * sizeof(uint64_t) - o_nodes, 16);
     s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);
     s->info = L.info;
     s->info.device_bytes = total;
@@ -443,6 +493,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_MAILBOX")) lo.mailbox = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
     return lo;
 }

@@ -277,15 +277,17 @@ __device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r
 // lanes reject at the same step, which practically never happens), each unit is one exec
 // region and the push/pop decision is straight-line (stack[sp] is the free slot above the
 // top: max_stack = max depth + 1, pt_capi.hip).  Same units, same order, same arithmetic.
-enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8 };
+enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8, TF_BCUR = 16 };
 struct TravLean {
     int node, sp, k, na, nt, la, lb, fl, best;
     float ld, rd, best_t;
+    uint64_t tested, rem;  // mailbox flavours only: uids tested by this query / left in this pair
 };
 __device__ __forceinline__ void trav_init(TravLean& s, bool active) {
     s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1;
     s.fl = active ? 0 : TF_DONE;
     s.ld = 0.0f; s.rd = 0.0f; s.best_t = -1.0f;
+    s.tested = 0; s.rem = 0;
 }
 __device__ __forceinline__ bool trav_finished(const TravLean& s) { return (s.fl & TF_DONE) != 0; }
 __device__ __forceinline__ bool trav_finished(const TravState& s) { return s.done; }
@@ -393,10 +395,91 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     return true;
 }
 
+// Mailboxed lean step (SceneView::mailbox: at most 64 distinct leaf entries).  A query keeps
+// the set of entries (uids) it has tested; a node step takes the union of its hit leaf
+// children's uid sets minus that set, and the leaf turns test only those, one uid per test in
+// increasing uid order (ctz), against the appended per-uid records.  Exact: (1) an entry
+// tested again yields the same t, and after its first test the closest t is <= that t, so
+// the strict-< update can never take it again — skipping it changes nothing, the node
+// pruning that reads the closest t included; (2) within one leaf pair the reference keeps
+// the FIRST of equal-t hits in its leaf order (left entries, then right), so an equal-t hit
+// replaces the current best only when the best came from this pair (TF_BCUR) and the new
+// entry comes earlier in that order (mb_pairpos: rare, scanned on demand).  tri_tests counts
+// the reference's tests (every entry of every hit leaf), so counters match the oracle.
+__device__ __forceinline__ int mb_pairpos(const SceneView& sc, const TravLean& s, int uid) {
+    for (int k = 0; k < s.na; ++k)
+        if (sc.tris[s.la + k].uid == uid) return k;
+    for (int k = 0; k < s.nt - s.na; ++k)
+        if (sc.tris[s.lb + k].uid == uid) return s.na + k;
+    return 1 << 30;  // unreachable: uid was taken from this pair's masks
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool mb_node_unit(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
+    const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * s.node;
+    float4 a = np[0], b = np[1], c = np[2];
+    int4 d = reinterpret_cast<const int4*>(np)[3];
+    s.ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
+    s.rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
+    const bool li = 0.0f < s.ld, ri = 0.0f < s.rd;
+    const bool lleaf = d.z >= 0, rleaf = d.w >= 0;
+    s.na = (li & lleaf) ? d.z : 0;
+    s.nt = s.na + ((ri & rleaf) ? d.w : 0);
+    if (COUNT) { cnt.nodes++; cnt.box_tests += 2; cnt.tri_tests += s.nt; }
+    const bool lm = s.na > 0, rm = s.nt > s.na;
+    const uint64_t ml = sc.lmask[lm ? d.x : 0], mr = sc.lmask[rm ? d.y : 0];
+    const uint64_t m = (lm ? ml : 0ull) | (rm ? mr : 0ull);
+    s.rem = m & ~s.tested;
+    s.tested |= m;
+    s.la = d.x; s.lb = d.y;
+    s.fl = ((li & !lleaf) ? TF_LINT : 0) | ((ri & !rleaf) ? TF_RINT : 0) | (s.rem ? TF_LEAF : 0);  // clears TF_BCUR
+    return s.rem == 0;
+}
+
+template <int K, bool FAST_RCP>
+__device__ __forceinline__ bool mb_leaf_loop(const SceneView& sc, const Ray& r, TravLean& s) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const bool live = j == 0 || s.rem != 0;  // the first test always is
+        if (j > 0 && !__any(live)) break;
+        const int uid = live ? (int)__builtin_ctzll(s.rem) : 0;
+        s.rem &= s.rem - 1;
+        const int rec = sc.mb_base + uid;
+        float t;
+        const bool hit = tri_hit<FAST_RCP>(sc.tris, rec, r, t) & live;
+        bool take = hit & ((s.best_t < 0.0f) | (t < s.best_t));
+        if (hit & (t == s.best_t) & ((s.fl & TF_BCUR) != 0))
+            take = mb_pairpos(sc, s, uid) < mb_pairpos(sc, s, s.best - sc.mb_base);
+        s.best_t = take ? t : s.best_t;
+        s.best = take ? rec : s.best;
+        s.fl |= take ? TF_BCUR : 0;
+    }
+    const bool decide = s.rem == 0;
+    s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
+    return decide;
+}
+
+template <int K, bool COUNT, bool FAST_RCP>
+__device__ __forceinline__ bool trav_step_mb(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack, int stride,
+                                             Counters& cnt) {
+    const int state = s.fl & (TF_LEAF | TF_DONE);
+    const uint64_t want_leaf = __ballot(state == TF_LEAF);
+    const uint64_t want_node = __ballot(state == 0);
+    if ((want_leaf | want_node) == 0) return false;
+    bool decide = false;
+    if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
+        if (state == TF_LEAF) decide = mb_leaf_loop<K, FAST_RCP>(sc, r, s);
+    } else if (state == 0) {
+        decide = mb_node_unit<COUNT>(sc, r, s, cnt);
+    }
+    if (decide) lean_decide(s, stack, stride);
+    return true;
+}
+
 // Traversal flavours (LaunchOpts.trav): 0 nested loops (trace), 1 flattened with per-lane
 // branches (trav_step), 2 flattened and predicated (trav_step_pred), 3 lean (trav_step_lean),
 // 4 lean with two triangle tests per leaf turn, 5 with four, 6 with eight, 7 with sixteen; +10: the lean
-// flavours with 1/det from rcp_rn (scenes with SceneView::fast_rcp).
+// flavours with 1/det from rcp_rn (scenes with SceneView::fast_rcp); +100: mailboxed lean flavours.
 template <int TRAV, bool LEAN = (TRAV >= 3)>
 struct TravSel { using type = TravState; };
 template <int TRAV>
@@ -405,7 +488,11 @@ struct TravSel<TRAV, true> { using type = TravLean; };
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
                                              int32_t* stack, int stride, Counters& cnt) {
-    if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 20: pipelined leaf loads; + 40: if-if step
+    if constexpr (TRAV >= 100) {  // mailboxed lean<K> (SceneView::mailbox scenes); + 10: fast reciprocal
+        constexpr int K = 1 << (TRAV % 10 - 3);
+        return trav_step_mb<K, COUNT, ((TRAV / 10) & 1) != 0>(sc, r, s, stack, stride, cnt);
+    }
+    else if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 20: pipelined leaf loads; + 40: if-if step
         constexpr int B = TRAV % 10;
         constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
         return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, ((TRAV / 20) & 1) != 0, ((TRAV / 40) & 1) != 0>(

@@ -8,8 +8,11 @@
 //   nodes[]  64 B: both child AABBs + two child refs (one node = one traversal
 //            step of intersection-logic.wgsl:31-212; the root is node 0 = bvh[6])
 //   tris[]   48 B per leaf reference, leaves contiguous in traversal order:
-//            v0 | material id, e1 = v1 - v0, e2 = v2 - v0 (f32, exactly the values
-//            ray-triangle-intersection.wgsl:6-7 computes per test)
+//            v0 | material id, e1 = v1 - v0 | uid, e2 = v2 - v0 (f32, exactly the values
+//            ray-triangle-intersection.wgsl:6-7 computes per test); scenes with at most
+//            64 distinct leaf entries (mailbox scenes) append one record per distinct entry
+//   lmask[]  mailbox scenes: per leaf (indexed by its first tris[] record) the 64-bit set
+//            of the uids it holds
 //   mats[]   64 B: Ns Ni illum | Kd | Ks | Ke (program-raymarch.wgsl:87-102)
 //   lights[] 48 B: the Ntri emissive triangles in sample_area_lights' slot order,
 //            plus one extra entry k == Ntri for hash1 == 1.0 (the reference's
@@ -33,7 +36,7 @@ struct alignas(16) Tri {
     float v0[3];
     int32_t mat;
     float e1[3];
-    int32_t pad0;
+    int32_t uid;  // mailbox scenes: id of this (i0, i1, i2, material) entry, < 64; else -1
     float e2[3];
     int32_t pad1;
 };
@@ -77,7 +80,12 @@ struct SceneView {
     // (1 = plain majority; a leaf turn costs up to K triangle tests, a node turn one node
     // step, so node turns that feed lanes into their leaves pay off); 0 = pipeline default
     int32_t node_bias;
-    int32_t pad[1];
+    // mailbox (SceneView::mailbox != 0 when the scene has <= 64 distinct leaf entries): the
+    // record of uid u is tris[mb_base + u]; lmask at byte offset off_lmask (inside the span)
+    int32_t mailbox;
+    int32_t mb_base;
+    uint32_t off_lmask;
+    const uint64_t* lmask;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

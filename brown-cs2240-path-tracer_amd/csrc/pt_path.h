@@ -192,6 +192,7 @@ __device__ __forceinline__ void stage_scene_lds(SceneView& sc, char* base) {
     sc.tris = reinterpret_cast<const Tri*>(base + sc.off_tris);
     sc.mats = reinterpret_cast<const Material*>(base + sc.off_mats);
     sc.lights = reinterpret_cast<const Light*>(base + sc.off_lights);
+    sc.lmask = reinterpret_cast<const uint64_t*>(base + sc.off_lmask);
 }
 
 }  // namespace pt

@@ -69,11 +69,19 @@ VARIANTS = {
     "wf_lean4_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_IFIF": "1"},
     "wf_lean8_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_PIPE": "1"},
     "wf_lean4_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_PIPE": "1"},
+    "wf_nomb": {"PT_KERNEL": "wavefront", "PT_MAILBOX": "0"},
+    "wf_mb16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16"},
+    "wf_mb8": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8"},
+    "wf_mb4": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4"},
+    "wf_mb16_bias4": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "4"},
+    "wf_mb8_bias4": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_NODE_BIAS": "4"},
+    "wf_mb8_bias2": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_NODE_BIAS": "2"},
+    "wf_mb16_bias16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "16"},
 }
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

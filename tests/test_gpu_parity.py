@@ -46,14 +46,21 @@ KERNELS = {
     "wavefront_lean8_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_IFIF": "1"},
     "wavefront_single_stream": {"PT_KERNEL": "wavefront", "PT_DUAL": "0"},
     "wavefront_dual_1block": {"PT_KERNEL": "wavefront", "PT_DUAL": "1", "PT_WF_TRACE_BLOCKS": "1"},
+    "wavefront_nomailbox": {"PT_KERNEL": "wavefront", "PT_MAILBOX": "0"},
+    "wavefront_mailbox_rev": {"PT_KERNEL": "wavefront", "PT_MB_UID_ORDER": "reverse"},
+    "wavefront_mailbox_lean4_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_LDS": "0"},
     "wavefront_3blocks_flat1": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1", "PT_WF_TRACE_BLOCKS": "3"},
 }
+
+
+ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER")
 
 
 @pytest.fixture(params=list(KERNELS))
 def kernel(request, monkeypatch):
     """Every kernel variant must give the same bits."""
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
+    for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     for k, v in KERNELS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -240,7 +247,7 @@ def test_invalid_scene_rejected():
 # kernel timing (pt_profile_*) and the AUTO policy (megakernel below 2^20 paths per call)
 # ---------------------------------------------------------------------------------------------
 def test_profile_records_every_launch(packed, monkeypatch):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
+    for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(64, 64)
@@ -266,7 +273,7 @@ def test_profile_records_every_launch(packed, monkeypatch):
 
 
 def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
+    for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
@@ -284,7 +291,7 @@ def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
 def test_auto_large_render_matches_megakernel(packed, monkeypatch):
     """At the AUTO switch point the wavefront result equals the megakernel's bit for bit
     (both equal the oracle on the smaller cases above)."""
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF", "PT_DUAL"):
+    for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(512, 512)
@@ -292,3 +299,50 @@ def test_auto_large_render_matches_megakernel(packed, monkeypatch):
         a = s.render(meta, 0, 4, 1, 8, pt_amd.MODE_AUTO)
         m = s.render(meta, 0, 4, 1, 8, pt_amd.MODE_MEGAKERNEL)
     assert same_bits(a, m), mismatch_report(a, m)
+
+
+# ---------------------------------------------------------------------------------------------
+# mailboxed traversal: exact ties between distinct leaf entries
+# ---------------------------------------------------------------------------------------------
+@pytest.fixture(scope="session")
+def packed_tie(tmp_path_factory):
+    """CornellBox with the back wall duplicated under another material (same vertex indices,
+    so both entries give bit-identical t on every back-wall hit).  The reference keeps the
+    first of the two in leaf order; the mailboxed leaf loop tests entries in uid order and
+    must resolve the tie the same way (PT_MB_UID_ORDER=reverse puts the duplicate first)."""
+    import os
+    import shutil
+    from conftest import SCENES, pack_with_node
+    base = tmp_path_factory.mktemp("tie")
+    src = os.path.join(SCENES, "scene_assets")
+    dst = base / "scene_assets"  # the Node loader resolves '/scene_assets/...' under the web root
+    dst.mkdir()
+    shutil.copy(os.path.join(src, "CornellBox.xml"), dst / "CornellBox.xml")
+    mdir = dst / "models" / "CornellBox"
+    mdir.mkdir(parents=True)
+    shutil.copy(os.path.join(src, "models", "CornellBox", "CornellBox-Original.mtl"), mdir)
+    with open(os.path.join(src, "models", "CornellBox", "CornellBox-Original.obj")) as f:
+        obj = f.read()
+    with open(mdir / "CornellBox-Original.obj", "w") as f:
+        f.write(obj + "\ng backWallTwin\nusemtl leftWall\nf 9 10 11 12\n")
+    return pack_with_node(str(dst / "CornellBox.xml"), str(base / "packed"))
+
+
+@pytest.mark.parametrize("env", [{}, {"PT_MB_UID_ORDER": "reverse"}, {"PT_MAILBOX": "0"}],
+                         ids=["mailbox", "mailbox_reverse_uids", "no_mailbox"])
+def test_mailbox_exact_ties(packed_tie, monkeypatch, env):
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("PT_KERNEL", "wavefront")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = packed_tie
+    meta = p.meta_for(48, 40)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        gpu = s.frame(meta, 3, 8)
+        acc, gc = s.render(meta, 0, 3, 1, 8, pt_amd.MODE_WAVEFRONT, counters=True)
+    ref, _ = oracle.frame(p.triangle_data, p.bvh_data, meta, 3, 8)
+    assert same_bits(gpu, ref), mismatch_report(gpu, ref)
+    racc, rc = oracle.render(p.triangle_data, p.bvh_data, meta, 0, 3, 1, 8)
+    assert same_bits(acc, racc), mismatch_report(acc, racc)
+    assert gc == rc, (gc, rc)
