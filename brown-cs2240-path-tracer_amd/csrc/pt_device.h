@@ -404,14 +404,16 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
 // pruning that reads the closest t included; (2) within one leaf pair the reference keeps
 // the FIRST of equal-t hits in its leaf order (left entries, then right), so an equal-t hit
 // replaces the current best only when the best came from this pair (TF_BCUR) and the new
-// entry comes earlier in that order (mb_pairpos: rare, scanned on demand).  tri_tests counts
+// entry comes earlier in that order (mb_first: rare, scanned on demand).  tri_tests counts
 // the reference's tests (every entry of every hit leaf), so counters match the oracle.
-__device__ __forceinline__ int mb_pairpos(const SceneView& sc, const TravLean& s, int uid) {
-    for (int k = 0; k < s.na; ++k)
-        if (sc.tris[s.la + k].uid == uid) return k;
-    for (int k = 0; k < s.nt - s.na; ++k)
-        if (sc.tris[s.lb + k].uid == uid) return s.na + k;
-    return 1 << 30;  // unreachable: uid was taken from this pair's masks
+// true when entry uid `a` comes before entry uid `b` in this pair's reference order (left leaf
+// entries, then right); b is the current best, taken from this pair, so the scan ends
+__device__ __forceinline__ bool mb_first(const SceneView& sc, const TravLean& s, int a, int b) {
+    for (int k = 0; k < s.nt; ++k) {
+        const int u = sc.tris[k < s.na ? s.la + k : s.lb + (k - s.na)].uid;
+        if (u == a || u == b) return u == a;
+    }
+    return false;
 }
 
 template <bool COUNT>
@@ -449,7 +451,7 @@ __device__ __forceinline__ bool mb_leaf_loop(const SceneView& sc, const Ray& r, 
         const bool hit = tri_hit<FAST_RCP>(sc.tris, rec, r, t) & live;
         bool take = hit & ((s.best_t < 0.0f) | (t < s.best_t));
         if (hit & (t == s.best_t) & ((s.fl & TF_BCUR) != 0))
-            take = mb_pairpos(sc, s, uid) < mb_pairpos(sc, s, s.best - sc.mb_base);
+            take = mb_first(sc, s, uid, s.best - sc.mb_base);
         s.best_t = take ? t : s.best_t;
         s.best = take ? rec : s.best;
         s.fl |= take ? TF_BCUR : 0;

@@ -433,7 +433,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     const bool pipe = lo.pipe > 0, ifif = lo.ifif > 0;
     // mailboxed lean<K> (+100) for scenes with <= 64 distinct leaf entries, unless pipelined
     // or if-if steps were asked for (those have no mailboxed form)
-    const bool mb = lo.mailbox != 0 && sc.mailbox && base >= 5 && base <= 7 && !pipe && !ifif;
+    const bool mb = lo.mailbox != 0 && sc.mailbox && base >= 5 && base <= 8 && !pipe && !ifif;
     const int trav = mb ? 100 + base + (fast ? 10 : 0)
                         : base + ((base >= 3 && fast) ? 10 : 0) + ((base >= 3 && fast && pipe) ? 20 : 0) +
                               ((base >= 3 && fast && ifif && !pipe) ? 40 : 0);
@@ -445,11 +445,11 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     if (lds) {
         WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7) WF(true, 8)
         WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18) WF(true, 35) WF(true, 36) WF(true, 37) WF(true, 55) WF(true, 56) WF(true, 57)
-        WF(true, 105) WF(true, 106) WF(true, 107) WF(true, 115) WF(true, 116) WF(true, 117)
+        WF(true, 105) WF(true, 106) WF(true, 107) WF(true, 115) WF(true, 116) WF(true, 117) WF(true, 118)
     } else {
         WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
         WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18) WF(false, 35) WF(false, 36) WF(false, 37) WF(false, 55) WF(false, 56) WF(false, 57)
-        WF(false, 105) WF(false, 106) WF(false, 107) WF(false, 115) WF(false, 116) WF(false, 117)
+        WF(false, 105) WF(false, 106) WF(false, 107) WF(false, 115) WF(false, 116) WF(false, 117) WF(false, 118)
     }
 #undef WF
     return hipErrorInvalidValue;

@@ -71,6 +71,8 @@ VARIANTS = {
     "wf_lean4_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_PIPE": "1"},
     "wf_nomb": {"PT_KERNEL": "wavefront", "PT_MAILBOX": "0"},
     "wf_mb16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16"},
+    "wf_mb32": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean32"},
+    "wf_mb32_bias16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean32", "PT_NODE_BIAS": "16"},
     "wf_mb8": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8"},
     "wf_mb4": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4"},
     "wf_mb16_bias4": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "4"},
