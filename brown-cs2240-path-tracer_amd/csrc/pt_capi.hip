@@ -137,11 +137,12 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                     const int32_t mat = wgsl_i32(e[3]);
                     if (mat < 0 || mat >= nobj) return fail(PT_ERR_SCENE, "BVH leaf references a material out of range");
                     Tri t{};
+                    float e1[3], e2[3];
                     for (int q = 0; q < 3; ++q) {
-                        t.v0[q] = v0[q];
-                        t.e1[q] = v1[q] - v0[q];  // ray-triangle-intersection.wgsl:6
-                        t.e2[q] = v2[q] - v0[q];  // :7
+                        e1[q] = v1[q] - v0[q];  // ray-triangle-intersection.wgsl:6
+                        e2[q] = v2[q] - v0[q];  // :7
                     }
+                    tri_set(t, v0, e1, e2);
                     t.mat = mat;
                     t.uid = -1;
                     L.tris.push_back(t);
@@ -201,8 +202,9 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
     double emax = 0.0;
     bool finite = true;
     for (const Tri& t : L.tris) {
-        const double a = std::sqrt((double)t.e1[0] * t.e1[0] + (double)t.e1[1] * t.e1[1] + (double)t.e1[2] * t.e1[2]);
-        const double b = std::sqrt((double)t.e2[0] * t.e2[0] + (double)t.e2[1] * t.e2[1] + (double)t.e2[2] * t.e2[2]);
+        const double e1[3] = {t.q0[3], t.q1[0], t.q1[1]}, e2[3] = {t.q1[2], t.q1[3], t.e2z};
+        const double a = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+        const double b = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
         finite = finite && std::isfinite(a) && std::isfinite(b);
         emax = std::max(emax, a * b);
     }
@@ -493,6 +495,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_BF")) lo.bf = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_MAILBOX")) lo.mailbox = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
     return lo;

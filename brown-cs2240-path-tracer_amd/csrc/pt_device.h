@@ -38,8 +38,9 @@ __device__ __forceinline__ float ray_box(const Ray& r, float mnx, float mny, flo
 __device__ __forceinline__ void test_tri(const Tri* __restrict__ tris, int i, const Ray& r, float& best_t, int& best) {
     const float eps = 1e-8f;
     const float4* tp = reinterpret_cast<const float4*>(tris + i);
-    float4 a = tp[0], b = tp[1], c = tp[2];
-    f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
+    float4 a = tp[0], b = tp[1];
+    float c = tris[i].e2z;
+    f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c);
     f3 rce2 = cross(r.d, e2);
     float det = dot(e1, rce2);
     if (det > -eps && det < eps) return;
@@ -179,17 +180,17 @@ __device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, Tra
 // Branch-free triangle test with the exact arithmetic of test_tri: every quantity of the
 // reference's early-out chain is computed and the chain becomes one predicate (the values
 // skipped by an early return never reach `hit`, so the result is identical).
-struct TriRec { float4 a, b, c; };  // (v0, material), e1, e2
+struct TriRec { float4 a, b; float c; };  // (v0, e1.x), (e1.yz, e2.xy), e2.z
 __device__ __forceinline__ TriRec load_tri(const Tri* __restrict__ tris, int i) {
     const float4* tp = reinterpret_cast<const float4*>(tris + i);
-    return TriRec{tp[0], tp[1], tp[2]};
+    return TriRec{tp[0], tp[1], tris[i].e2z};
 }
 
 template <bool FAST_RCP = false>
 __device__ __forceinline__ bool tri_hit(const TriRec& tr, const Ray& r, float& t_out) {
     const float eps = 1e-8f;
-    const float4 a = tr.a, b = tr.b, c = tr.c;
-    f3 v0 = mk(a.x, a.y, a.z), e1 = mk(b.x, b.y, b.z), e2 = mk(c.x, c.y, c.z);
+    const float4 a = tr.a, b = tr.b;
+    f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, tr.c);
     f3 rce2 = cross(r.d, e2);
     float det = dot(e1, rce2);
     // FAST_RCP (SceneView::fast_rcp): |det| < 2^126 for this scene, where rcp_rn is the IEEE
@@ -523,12 +524,11 @@ struct Hit {
 
 // Intersection{point, normal} for the winning record (ray-triangle-intersection.wgsl:30-36)
 __device__ __forceinline__ Hit hit_data(const SceneView& sc, const Ray& r, int rec, float t) {
-    const float4* tp = reinterpret_cast<const float4*>(sc.tris + rec);
-    float4 a = tp[0], b = tp[1], c = tp[2];
+    const TriRec tr = load_tri(sc.tris, rec);
     Hit h;
     h.p = madd(r.o, r.d, t);
-    h.n = normalize(cross(mk(b.x, b.y, b.z), mk(c.x, c.y, c.z)));
-    h.mat = __builtin_bit_cast(int, a.w);
+    h.n = normalize(cross(mk(tr.a.w, tr.b.x, tr.b.y), mk(tr.b.z, tr.b.w, tr.c)));
+    h.mat = sc.tris[rec].mat;
     return h;
 }
 

@@ -62,6 +62,7 @@ struct LaunchOpts {
     int dual = -1;         // wavefront batch split in two halves on two streams: -1 default
     int stagger = -1;      // dual halves' traces alternate instead of overlapping: -1 default (off)
     int mailbox = -1;      // mailboxed lean traversal where SceneView::mailbox allows it: -1 default (on)
+    int bf = -1;           // wavefront, mailbox scenes: brute-force + replay trace kernel: -1 default (on)
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 

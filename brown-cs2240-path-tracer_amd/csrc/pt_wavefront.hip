@@ -230,6 +230,96 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     if (COUNT) flush_counters(c, cnt_out);
 }
 
+// Brute force + replay: the closest-hit kernel for mailbox scenes (SceneView::mailbox: at most
+// 64 distinct leaf entries, e.g. every Cornell box).  The reference's traversal (and the
+// mailboxed one, trav_step_mb) tests ~19 of CornellBox's 36 distinct entries per query, in an
+// order and number that differ from lane to lane, so SIMT lanes idle in each other's leaf
+// loops (~30 % of the issued test slots do work).  Here a wave takes 64 queue entries at once
+// and
+//   phase 1  runs the triangle test of EVERY distinct entry u for all 64 rays in lockstep
+//            (wave-uniform loop; the record is uniform, read through the scalar cache), keeping
+//            per ray the set of entries hit and the t of the first kBfSlots hits (LDS);
+//   phase 2  replays the reference's traversal per ray — node steps, exit-distance pruning,
+//            the mailboxed leaf pairs of trav_step_mb — where a leaf entry costs a mask test
+//            and, for entries that hit, a lookup of its t instead of a triangle test.
+// Exact: a triangle test is a pure function of (ray, record), so phase 1 computes the same t
+// (and hit predicate) the traversal would, and phase 2 applies them in the mailboxed order
+// with the same strict-< update, tie-break and pruning; tests of entries the traversal never
+// reaches have no effect.  A ray with more than `nslots` (<= kBfSlots) hits recomputes the rest on demand.
+constexpr int kBfSlots = 8;
+
+__device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
+    // uniform index: constant address space, so the record comes through s_load (no VGPRs)
+    const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(tris + i);
+    return TriRec{make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]), f[8]};
+}
+
+template <bool LDS, bool FAST_RCP, bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out, int nslots) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
+    char* slot_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
+    const uint32_t lane = lane_id();
+    float* slot = reinterpret_cast<float*>(slot_base) + (threadIdx.x / 64u) * (kBfSlots * 64) + lane;  // slot k: slot[64k]
+    if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
+    const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
+    const Tri* gtris = sc.tris;  // global records for phase 1
+    if (LDS) stage_scene_lds(sc, slot_base + (blockDim.x / 64u) * (kBfSlots * 64 * 4));
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    const uint32_t nb = (count + 63) / 64;
+    const int U = sc.n_tris - sc.mb_base;
+    const float4* q = in_q ? wb.shd.ray : wb.ext.ray;
+    Counters c = {};
+    for (uint32_t b = w; b < nb; b += nwaves) {  // batches of 64 entries, interleaved over waves
+        const uint32_t e = b * 64 + lane;
+        const bool valid = e < count;
+        uint32_t p;
+        const Ray r = unpack_ray(valid ? q[2 * (size_t)e] : make_float4(0, 0, 0, 1),
+                                 valid ? q[2 * (size_t)e + 1] : make_float4(0, 0, 0, 0), p);
+        // phase 1: every distinct entry against all 64 rays
+        uint64_t hits = 0;
+        int nh = 0;
+        for (int u = 0; u < U; ++u) {
+            float t;
+            const bool h = tri_hit<FAST_RCP>(load_tri_scalar(gtris, sc.mb_base + u), r, t) & valid;
+            if (h) {
+                if (nh < nslots) slot[64 * nh] = t;
+                ++nh;
+                hits |= 1ull << u;
+            }
+        }
+        // phase 2: the mailboxed traversal, leaf entries resolved from phase 1
+        TravLean s;
+        trav_init(s, valid);
+        while (__any(!trav_finished(s))) {
+            if (!trav_finished(s)) {
+                mb_node_unit<COUNT>(sc, r, s, c);
+                uint64_t rh = s.rem & hits;
+                while (rh) {
+                    const int u = (int)__builtin_ctzll(rh);
+                    rh &= rh - 1;
+                    const int k = __popcll(hits & ((1ull << u) - 1));
+                    const int rec = sc.mb_base + u;
+                    float t;
+                    if (k < nslots) t = slot[64 * k];
+                    else tri_hit<FAST_RCP>(sc.tris, rec, r, t);  // a hit, so the same t as phase 1
+                    bool take = (s.best_t < 0.0f) | (t < s.best_t);
+                    if ((t == s.best_t) & ((s.fl & TF_BCUR) != 0)) take = mb_first(sc, s, u, s.best - sc.mb_base);
+                    s.best_t = take ? t : s.best_t;
+                    s.best = take ? rec : s.best;
+                    s.fl |= take ? TF_BCUR : 0;
+                }
+                s.rem = 0;
+                s.fl &= ~TF_LEAF;
+                lean_decide(s, stack, blockDim.x);
+            }
+        }
+        if (valid) wb.hitq[e] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
+    }
+    if (COUNT) flush_counters(c, cnt_out);
+}
+
 // Shade blocks are 1024 threads so that compaction takes one atomicAdd per 1024 entries: all
 // atomics on the queue counter serialise at one memory channel, and one per wave (131k per
 // 8M-path batch) cost more than the shading itself.
@@ -321,6 +411,17 @@ __global__ __launch_bounds__(256) void k_wf_accum(const float* __restrict__ rad,
         const hipError_t e_ = (expr);            \
         if (e_ != hipSuccess) return e_;         \
     } while (0)
+// TRAV >= 300: the brute-force + replay kernel (k_wf_trace_bf; + 10: fast reciprocal)
+template <bool LDS, int TRAV, bool COUNT>
+constexpr const void* trace_kernel() {
+    if constexpr (TRAV >= 300) return (const void*)k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
+    else return (const void*)k_wf_trace<LDS, TRAV, COUNT>;
+}
+template <bool LDS, int TRAV, bool COUNT>
+static size_t trace_lds(const SceneView& sc) {
+    const size_t per_wave = TRAV >= 300 ? (size_t)kBfSlots * 64 * 4 : kStageBytes;
+    return (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * per_wave + (LDS ? sc.span_bytes : 0);
+}
 template <bool LDS, int TRAV, bool COUNT>
 static int trace_blocks(size_t lds_bytes) {
     static int cached = 0;
@@ -330,8 +431,7 @@ static int trace_blocks(size_t lds_bytes) {
         int per_cu = 0, dev = 0, cus = 0;
         hipGetDevice(&dev);
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_wf_trace<LDS, TRAV, COUNT>, kTraceBlock,
-                                                     lds_bytes);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<LDS, TRAV, COUNT>(), kTraceBlock, lds_bytes);
         b = std::max(1, per_cu) * std::max(1, cus);
         cached_lds = lds_bytes;
     }
@@ -362,10 +462,12 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     const bool dual = ws.aux[0] != nullptr && nframes >= 2 && wb.capacity / 2 >= npix;
     const uint32_t F = dual ? 2 * std::min<uint32_t>((nframes + 1) / 2, (uint32_t)(wb.capacity / 2 / npix))
                             : std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
-    const size_t lds = (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * kStageBytes + (LDS ? sc.span_bytes : 0);
+    const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc);
     int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
     if (const char* e = std::getenv("PT_WF_TRACE_BLOCKS")) tblocks = std::max(1, std::min(tblocks, std::atoi(e)));  // tests
     const int iters = 2 * (fp.max_depth + 1);
+    int bf_slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
+    if (const char* e = std::getenv("PT_BF_SLOTS")) bf_slots = std::max(0, std::min(kBfSlots, std::atoi(e)));
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         const uint32_t FA = dual && Fb >= 2 ? (Fb + 1) / 2 : Fb, FB = Fb - FA;
@@ -392,8 +494,12 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                 const WfBuffers& w = *hv[h].w;
                 const int sblocks = (int)((hv[h].P + kShadeBlock - 1) / kShadeBlock);
                 if (stagger && (h == 1 || it > 0)) HIP_RETURN_IF(hipStreamWaitEvent(st, ws.traced[1 - h], 0));
-                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc, w,
-                          in_q, cnt);
+                if constexpr (TRAV >= 300)
+                    PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
+                              dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
+                else
+                    PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc,
+                              w, in_q, cnt);
                 if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
                 if ((it & 1) == 0)
                     PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
@@ -434,7 +540,11 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     // mailboxed lean<K> (+100) for scenes with <= 64 distinct leaf entries, unless pipelined
     // or if-if steps were asked for (those have no mailboxed form)
     const bool mb = lo.mailbox != 0 && sc.mailbox && base >= 5 && base <= 8 && !pipe && !ifif;
-    const int trav = mb ? 100 + base + (fast ? 10 : 0)
+    // brute force + replay (k_wf_trace_bf) by default for mailbox scenes; an explicit PT_TRAV
+    // or PT_BF=0 keeps the traversal kernels
+    const bool bf = lo.bf != 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0;
+    const int trav = bf ? 300 + (fast ? 10 : 0)
+                   : mb ? 100 + base + (fast ? 10 : 0)
                         : base + ((base >= 3 && fast) ? 10 : 0) + ((base >= 3 && fast && pipe) ? 20 : 0) +
                               ((base >= 3 && fast && ifif && !pipe) ? 40 : 0);
 #define WF(L, T)                                                                                               \
@@ -445,10 +555,12 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     if (lds) {
         WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7) WF(true, 8)
         WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18) WF(true, 35) WF(true, 36) WF(true, 37) WF(true, 55) WF(true, 56) WF(true, 57)
+        WF(true, 300) WF(true, 310)
         WF(true, 105) WF(true, 106) WF(true, 107) WF(true, 115) WF(true, 116) WF(true, 117) WF(true, 118)
     } else {
         WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
         WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18) WF(false, 35) WF(false, 36) WF(false, 37) WF(false, 55) WF(false, 56) WF(false, 57)
+        WF(false, 300) WF(false, 310)
         WF(false, 105) WF(false, 106) WF(false, 107) WF(false, 115) WF(false, 116) WF(false, 117) WF(false, 118)
     }
 #undef WF

@@ -69,6 +69,8 @@ VARIANTS = {
     "wf_lean4_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_IFIF": "1"},
     "wf_lean8_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_PIPE": "1"},
     "wf_lean4_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_PIPE": "1"},
+    "wf_bf": {"PT_KERNEL": "wavefront"},
+    "wf_bf_div": {"PT_KERNEL": "wavefront", "PT_FASTRCP": "0"},
     "wf_nomb": {"PT_KERNEL": "wavefront", "PT_MAILBOX": "0"},
     "wf_mb16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16"},
     "wf_mb32": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean32"},
@@ -83,7 +85,7 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

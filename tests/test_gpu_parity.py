@@ -48,13 +48,16 @@ KERNELS = {
     "wavefront_dual_1block": {"PT_KERNEL": "wavefront", "PT_DUAL": "1", "PT_WF_TRACE_BLOCKS": "1"},
     "wavefront_nomailbox": {"PT_KERNEL": "wavefront", "PT_MAILBOX": "0"},
     "wavefront_mailbox_rev": {"PT_KERNEL": "wavefront", "PT_MB_UID_ORDER": "reverse"},
+    "wavefront_mb_lean16_rev": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
+    "wavefront_bf_global_noslots": {"PT_KERNEL": "wavefront", "PT_LDS": "0", "PT_BF_SLOTS": "0"},
+    "wavefront_bf_2slots_div": {"PT_KERNEL": "wavefront", "PT_BF_SLOTS": "2", "PT_FASTRCP": "0"},
     "wavefront_mailbox_lean4_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_LDS": "0"},
     "wavefront_3blocks_flat1": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1", "PT_WF_TRACE_BLOCKS": "3"},
 }
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
-            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER")
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -328,8 +331,10 @@ def packed_tie(tmp_path_factory):
     return pack_with_node(str(dst / "CornellBox.xml"), str(base / "packed"))
 
 
-@pytest.mark.parametrize("env", [{}, {"PT_MB_UID_ORDER": "reverse"}, {"PT_MAILBOX": "0"}],
-                         ids=["mailbox", "mailbox_reverse_uids", "no_mailbox"])
+@pytest.mark.parametrize("env", [{}, {"PT_MB_UID_ORDER": "reverse"}, {"PT_MAILBOX": "0"},
+                                 {"PT_MB_UID_ORDER": "reverse", "PT_BF_SLOTS": "1"},
+                                 {"PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"}],
+                         ids=["bf", "bf_reverse_uids", "no_mailbox", "bf_reverse_1slot", "mb_lean16_reverse"])
 def test_mailbox_exact_ties(packed_tie, monkeypatch, env):
     for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
