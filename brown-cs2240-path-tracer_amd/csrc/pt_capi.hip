@@ -495,6 +495,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_FUSE")) lo.fuse = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_BF")) lo.bf = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_MAILBOX")) lo.mailbox = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
@@ -509,12 +510,15 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     if (paths > 0x7fffffffull) return fail(PT_ERR_INVALID, "image too large for one wavefront batch");
     if (s->d_wf) { hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; }
     const size_t n = paths;
+    // queue arrays carry slack so that each half can be cut into kRegions regions of a whole
+    // number of 64-entry batches holding all its paths (k_wf_step_bf)
+    const size_t qn = n + 2 * (size_t)kRegions * 64;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
     size_t oq[6];
-    for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * n);
-    const size_t o_p0 = take(16 * n), o_p1 = take(16 * n), o_p2 = take(8 * n), o_hit = take(8 * n),
-                 o_rad = take(12 * n), o_ctl = take(4 * 2 * WF_CTL_WORDS);
+    for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * qn);
+    const size_t o_p0 = take(16 * qn), o_p1 = take(16 * qn), o_p2 = take(8 * qn), o_hit = take(8 * qn),
+                 o_rad = take(12 * n), o_ctl = take(4 * 2 * WF_CTL_WORDS), o_rcnt = take(4 * 2 * 3 * kRegions);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
     char* b = static_cast<char*>(s->d_wf);
     auto f4 = [&](size_t o) { return reinterpret_cast<float4*>(b + o); };
@@ -526,7 +530,9 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     w.hitq = reinterpret_cast<int2*>(b + o_hit);
     w.rad = reinterpret_cast<float*>(b + o_rad);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
-    if (hipMemset(w.ctl, 0, 4 * 2 * WF_CTL_WORDS) != hipSuccess) return fail(PT_ERR_HIP, "hipMemset wavefront control words");
+    w.rcnt = reinterpret_cast<uint32_t*>(b + o_rcnt);
+    if (hipMemset(w.ctl, 0, 4 * 2 * WF_CTL_WORDS) != hipSuccess || hipMemset(w.rcnt, 0, 4 * 2 * 3 * kRegions) != hipSuccess)
+        return fail(PT_ERR_HIP, "hipMemset wavefront control words");
     if (!s->ws.aux[0]) {
         if (hipStreamCreateWithFlags(&s->ws.aux[0], hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&s->ws.aux[1], hipStreamNonBlocking) != hipSuccess ||
@@ -538,6 +544,7 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
             return fail(PT_ERR_HIP, "creating the wavefront's streams");
     }
     w.capacity = (uint32_t)n;
+    w.qcap = (uint32_t)qn;
     return PT_OK;
 }
 
@@ -561,7 +568,9 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     SceneView view = s->view;
     if (const char* e = std::getenv("PT_NODE_BIAS")) view.node_bias = std::max(1, std::atoi(e));  // A/B runs
     if (lo.wavefront) {
-        const uint64_t want = std::max<uint64_t>(npix, std::min<uint64_t>(npix * (accum ? nframes : 1), kWfTargetPaths));
+        uint64_t target = kWfTargetPaths;
+        if (const char* e = std::getenv("PT_WF_PATHS")) target = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));  // A/B
+        const uint64_t want = std::max<uint64_t>(npix, std::min<uint64_t>(npix * (accum ? nframes : 1), target));
         int rc2 = ensure_wavefront(s, want);
         if (rc2 != PT_OK) return rc2;
         HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,

@@ -18,11 +18,12 @@ namespace pt {
 // calling thread, every launch is bracketed by two HIP events on its stream.
 enum KernelId : int {
     KID_MEGA = 0, KID_REGEN, KID_WF_GENERATE, KID_WF_TRACE, KID_WF_SHADE_EXT, KID_WF_SHADE_SHADOW, KID_WF_ACCUM,
-    KID_TONEMAP, KID_COUNT
+    KID_TONEMAP, KID_WF_STEP, KID_COUNT
 };
 inline const char* kernel_name(int k) {
     static const char* const n[KID_COUNT] = {"k_mega",         "k_regen",           "k_wf_generate", "k_wf_trace",
-                                             "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum",    "k_tonemap"};
+                                             "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum",    "k_tonemap",
+                                             "k_wf_step"};
     return (k >= 0 && k < KID_COUNT) ? n[k] : "?";
 }
 struct KernelProfiler {
@@ -63,6 +64,7 @@ struct LaunchOpts {
     int stagger = -1;      // dual halves' traces alternate instead of overlapping: -1 default (off)
     int mailbox = -1;      // mailboxed lean traversal where SceneView::mailbox allows it: -1 default (on)
     int bf = -1;           // wavefront, mailbox scenes: brute-force + replay trace kernel: -1 default (on)
+    int fuse = -1;         // bf trace fused with the shading (k_wf_step_bf): -1 default (on)
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 
@@ -72,7 +74,7 @@ bool scene_fits_lds(const SceneView& sc);
 // path's state travels with its ray: queue entry i holds the ray AND the path state, and
 // a shade kernel writes the surviving path to its compacted slot of the other queue, so no
 // kernel gathers by path index.  Iterations alternate extension / shadow queues.
-enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_WATCHDOG = 2, WF_SNAP_CLAIM = 3, WF_SNAP = 8, WF_SNAP_WORDS = 16, WF_CTL_WORDS = 64 };
+enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_WATCHDOG = 2, WF_SNAP_CLAIM = 3, WF_RING = 4, WF_SNAP = 8, WF_SNAP_WORDS = 16, WF_CTL_WORDS = 64 };
 // the control block holds WF_CTL_WORDS words per half of a dual-stream batch (wb_half)
 // iterations after which a trace wave gives up: it sets ctl[WF_WATCHDOG], the first such wave
 // leaves its scheduling state in ctl[WF_SNAP..], and the host reports an error
@@ -92,8 +94,16 @@ struct WfBuffers {
     int2* hitq;    // per queue entry: (leaf record, t bits)
     float* rad;    // per path: radiance when it ended [capacity][3]
     uint32_t* ctl; // queue counts
-    uint32_t capacity;
+    uint32_t capacity;  // paths per batch
+    uint32_t qcap;      // entries per queue array (capacity + slack for the region layout)
+    // region-partitioned queues of the fused kernel (k_wf_step_bf): region r of a queue holds
+    // entries [r * rstride, r * rstride + count_r); rcnt[slot * kRegions + r] = count_r for
+    // the three rotating count slots
+    uint32_t* rcnt;
+    uint32_t rstride;
+    uint32_t nreg;
 };
+constexpr uint32_t kRegions = 512;
 constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 
 // Dual-stream wavefront: two streams owned by the scene, created back to back so that HIP's

@@ -95,6 +95,15 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
         wb.ctl[WF_COUNT0] = P;
         wb.ctl[WF_COUNT1] = 0;
     }
+    // region layout (k_wf_step_bf, wb.nreg > 0): 64-path batch j goes to region j % nreg
+    const uint32_t R = wb.nreg;
+    if (R && p < R) {  // counts of region p: its batches j = p, p + R, ... < ceil(P / 64)
+        const uint32_t nbat = (P + 63) / 64;
+        const uint32_t n = p < nbat ? (nbat - p + R - 1) / R : 0u;
+        const uint32_t last = p + (n - 1) * R;
+        wb.rcnt[p] = n == 0 ? 0u : n * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
+        wb.rcnt[kRegions + p] = 0;
+    }
     Counters c = {};
     if (p < P) {
         uint32_t x, y, f;
@@ -102,7 +111,9 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
         const uint32_t t = raw_salt ? frame0 : (uint32_t)(float)(frame0 + (fbase + f) * stride);
         PathState ps;
         Ray r = path_begin(fp, x, y, t, ps);
-        store_entry(wb.ext, p, r, p, ps);
+        const uint32_t j = p / 64;
+        const uint32_t i = R ? (j % R) * wb.rstride + (j / R) * 64 + (p & 63) : p;
+        store_entry(wb.ext, i, r, p, ps);
         if (COUNT) { c.samples++; c.ext_queries++; }
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -254,21 +265,81 @@ __device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
     return TriRec{make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]), f[8]};
 }
 
+// Closest hit of the 64 rays of one batch (lane = ray; `valid` false lanes give no hit):
+// phase 1 + phase 2 above.  Returns the record (or -1) and its t in t_out.
+template <bool FAST_RCP, bool COUNT>
+__device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris, const Ray& r, bool valid, float* slot,
+                                          int nslots, int32_t* stack, int stride, Counters& c, float& t_out) {
+    const int U = sc.n_tris - sc.mb_base;
+    // phase 1: every distinct entry against all 64 rays
+    uint64_t hits = 0;
+    int nh = 0;
+    for (int u = 0; u < U; ++u) {
+        float t;
+        const bool h = tri_hit<FAST_RCP>(load_tri_scalar(gtris, sc.mb_base + u), r, t) & valid;
+        if (h) {
+            if (nh < nslots) slot[64 * nh] = t;
+            ++nh;
+            hits |= 1ull << u;
+        }
+    }
+    // phase 2: the mailboxed traversal, leaf entries resolved from phase 1
+    TravLean s;
+    trav_init(s, valid);
+    while (__any(!trav_finished(s))) {
+        if (!trav_finished(s)) {
+            mb_node_unit<COUNT>(sc, r, s, c);
+            uint64_t rh = s.rem & hits;
+            while (rh) {
+                const int u = (int)__builtin_ctzll(rh);
+                rh &= rh - 1;
+                const int k = __popcll(hits & ((1ull << u) - 1));
+                const int rec = sc.mb_base + u;
+                float t;
+                if (k < nslots) t = slot[64 * k];
+                else tri_hit<FAST_RCP>(sc.tris, rec, r, t);  // a hit, so the same t as phase 1
+                bool take = (s.best_t < 0.0f) | (t < s.best_t);
+                if ((t == s.best_t) & ((s.fl & TF_BCUR) != 0)) take = mb_first(sc, s, u, s.best - sc.mb_base);
+                s.best_t = take ? t : s.best_t;
+                s.best = take ? rec : s.best;
+                s.fl |= take ? TF_BCUR : 0;
+            }
+            s.rem = 0;
+            s.fl &= ~TF_LEAF;
+            lean_decide(s, stack, stride);
+        }
+    }
+    t_out = s.best_t;
+    return s.best;
+}
+
+// LDS of the bf kernels: per-lane stacks, then per wave kBfSlots x 64 hit slots, then the scene
+struct BfLds {
+    int32_t* stack;
+    float* slot;
+    char* scene;
+};
+__device__ __forceinline__ BfLds bf_lds(char* smem, const SceneView& sc) {
+    BfLds l;
+    l.stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
+    char* slot_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
+    l.slot = reinterpret_cast<float*>(slot_base) + (threadIdx.x / 64u) * (kBfSlots * 64) + lane_id();  // slot k: slot[64k]
+    l.scene = slot_base + (blockDim.x / 64u) * (kBfSlots * 64 * 4);
+    return l;
+}
+
 template <bool LDS, bool FAST_RCP, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out, int nslots) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
-    char* slot_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
+    const BfLds l = bf_lds(smem, sc);
     const uint32_t lane = lane_id();
-    float* slot = reinterpret_cast<float*>(slot_base) + (threadIdx.x / 64u) * (kBfSlots * 64) + lane;  // slot k: slot[64k]
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
     const Tri* gtris = sc.tris;  // global records for phase 1
-    if (LDS) stage_scene_lds(sc, slot_base + (blockDim.x / 64u) * (kBfSlots * 64 * 4));
+    if (LDS) stage_scene_lds(sc, l.scene);
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
     const uint32_t nb = (count + 63) / 64;
-    const int U = sc.n_tris - sc.mb_base;
     const float4* q = in_q ? wb.shd.ray : wb.ext.ray;
     Counters c = {};
     for (uint32_t b = w; b < nb; b += nwaves) {  // batches of 64 entries, interleaved over waves
@@ -277,45 +348,84 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
         uint32_t p;
         const Ray r = unpack_ray(valid ? q[2 * (size_t)e] : make_float4(0, 0, 0, 1),
                                  valid ? q[2 * (size_t)e + 1] : make_float4(0, 0, 0, 0), p);
-        // phase 1: every distinct entry against all 64 rays
-        uint64_t hits = 0;
-        int nh = 0;
-        for (int u = 0; u < U; ++u) {
-            float t;
-            const bool h = tri_hit<FAST_RCP>(load_tri_scalar(gtris, sc.mb_base + u), r, t) & valid;
-            if (h) {
-                if (nh < nslots) slot[64 * nh] = t;
-                ++nh;
-                hits |= 1ull << u;
+        float t;
+        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t);
+        if (valid) wb.hitq[e] = make_int2(rec, __builtin_bit_cast(int, t));
+    }
+    if (COUNT) flush_counters(c, cnt_out);
+}
+
+// Trace + shade in one launch (mailbox scenes): the wave that traced a batch of 64 queue
+// entries (bf_closest) shades them at once — the hit never goes through HBM and the ray record
+// is read once — and appends the surviving paths to the other queue.  Queues are cut into
+// wb.nreg regions (k_wf_generate deals 64-path batches round-robin); the waves w ≡ r (mod
+// nreg) serve region r of the input and append to region r of the output, one atomicAdd per
+// wave and batch on that region's counter (a counter shared by all waves serialises at one
+// memory channel, and each wave waits for its add: measured 2x slower).  A region's output
+// never exceeds its input, so every region holds its paths through all bounces.  Iteration
+// `it` reads the counts of slot it % 3, appends to slot (it + 1) % 3 and zeroes slot
+// (it + 2) % 3 for iteration it + 1 (iteration it - 1 read that slot and it - 2 wrote it, both
+// finished: stream order).  Same path logic (pt_path.h) as k_wf_shade, so the same bits.
+template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) void k_wf_step_bf(SceneView sc, FrameParams fp, WfBuffers wb, int it,
+                                                           Counters* cnt_out, int nslots) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const BfLds l = bf_lds(smem, sc);
+    const uint32_t lane = lane_id();
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    const uint32_t R = wb.nreg;  // <= nwaves (host)
+    const uint32_t rg = w % R, g = w / R, G = (nwaves - rg + R - 1) / R;
+    if (g == 0 && lane == 0) wb.rcnt[((it + 2) % 3) * kRegions + rg] = 0;
+    const uint32_t count = wb.rcnt[(it % 3) * kRegions + rg];
+    uint32_t* out_count = &wb.rcnt[((it + 1) % 3) * kRegions + rg];
+    const size_t rbase = (size_t)rg * wb.rstride;
+    const Tri* gtris = sc.tris;  // global records for phase 1
+    if (LDS) stage_scene_lds(sc, l.scene);
+    const uint32_t nb = (count + 63) / 64;
+    const WfQueue& in = EXT ? wb.ext : wb.shd;
+    const WfQueue& out = EXT ? wb.shd : wb.ext;
+    Counters c = {};
+    for (uint32_t b = g; b < nb; b += G) {  // this region's batches, interleaved over its waves
+        const bool valid = b * 64 + lane < count;
+        const size_t e = rbase + (valid ? b * 64 + lane : 0);
+        const float4 a0 = in.ray[2 * e], a1 = in.ray[2 * e + 1];
+        uint32_t p;
+        Ray r = unpack_ray(valid ? a0 : make_float4(0, 0, 0, 1), valid ? a1 : make_float4(0, 0, 0, 0), p);
+        float t;
+        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t);
+        bool more = false;
+        PathState ps;
+        if (valid) {
+            const float4 c2 = in.q2[e], d3 = in.q3[e];
+            unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
+            ps.L = mk(c2.x, c2.y, c2.z);
+            ps.seed = __builtin_bit_cast(uint32_t, c2.w);
+            ps.beta = mk(d3.x, d3.y, d3.z);
+            if (EXT) {
+                more = path_after_ext(sc, rec, t, r, ps);
+                if (more && COUNT) c.shadow_queries++;
+            } else {
+                load_shading_point(wb, (uint32_t)e, ps);
+                more = path_after_shadow(sc, fp, rec, t, r, ps);
+                if (more && COUNT) c.ext_queries++;
+            }
+            if (!more) {
+                float* o = wb.rad + 3 * (size_t)p;
+                o[0] = ps.L.x; o[1] = ps.L.y; o[2] = ps.L.z;
             }
         }
-        // phase 2: the mailboxed traversal, leaf entries resolved from phase 1
-        TravLean s;
-        trav_init(s, valid);
-        while (__any(!trav_finished(s))) {
-            if (!trav_finished(s)) {
-                mb_node_unit<COUNT>(sc, r, s, c);
-                uint64_t rh = s.rem & hits;
-                while (rh) {
-                    const int u = (int)__builtin_ctzll(rh);
-                    rh &= rh - 1;
-                    const int k = __popcll(hits & ((1ull << u) - 1));
-                    const int rec = sc.mb_base + u;
-                    float t;
-                    if (k < nslots) t = slot[64 * k];
-                    else tri_hit<FAST_RCP>(sc.tris, rec, r, t);  // a hit, so the same t as phase 1
-                    bool take = (s.best_t < 0.0f) | (t < s.best_t);
-                    if ((t == s.best_t) & ((s.fl & TF_BCUR) != 0)) take = mb_first(sc, s, u, s.best - sc.mb_base);
-                    s.best_t = take ? t : s.best_t;
-                    s.best = take ? rec : s.best;
-                    s.fl |= take ? TF_BCUR : 0;
-                }
-                s.rem = 0;
-                s.fl &= ~TF_LEAF;
-                lean_decide(s, stack, blockDim.x);
+        const uint64_t keep = __ballot(more);
+        if (keep) {  // wave-uniform
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(out_count, (uint32_t)__popcll(keep));
+            base = __shfl(base, 0, 64);
+            if (more) {
+                const uint32_t j = (uint32_t)rbase + base + rank_below(keep);
+                store_entry(out, j, r, p, ps);
+                if (EXT) store_shading_point(wb, j, ps);
             }
         }
-        if (valid) wb.hitq[e] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
     }
     if (COUNT) flush_counters(c, cnt_out);
 }
@@ -411,10 +521,12 @@ __global__ __launch_bounds__(256) void k_wf_accum(const float* __restrict__ rad,
         const hipError_t e_ = (expr);            \
         if (e_ != hipSuccess) return e_;         \
     } while (0)
-// TRAV >= 300: the brute-force + replay kernel (k_wf_trace_bf; + 10: fast reciprocal)
+// TRAV >= 300: the brute-force + replay kernel (k_wf_trace_bf; + 10: fast reciprocal); >= 400: fused
+// with the shading (k_wf_step_bf)
 template <bool LDS, int TRAV, bool COUNT>
 constexpr const void* trace_kernel() {
-    if constexpr (TRAV >= 300) return (const void*)k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
+    if constexpr (TRAV >= 400) return (const void*)k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>;
+    else if constexpr (TRAV >= 300) return (const void*)k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
     else return (const void*)k_wf_trace<LDS, TRAV, COUNT>;
 }
 template <bool LDS, int TRAV, bool COUNT>
@@ -443,12 +555,14 @@ static int trace_blocks(size_t lds_bytes) {
 // from h * WF_CTL_WORDS.
 static WfBuffers wb_half(const WfBuffers& wb, int h, size_t rad_off) {
     WfBuffers v = wb;
-    const size_t e = (size_t)h * (wb.capacity / 2);
+    const size_t e = (size_t)h * (wb.qcap / 2);
     for (WfQueue* q : {&v.ext, &v.shd}) { q->ray += 2 * e; q->q2 += e; q->q3 += e; }
     v.sp0 += e; v.sp1 += e; v.sp2 += e; v.hitq += e;
     v.rad += rad_off;
     v.ctl += h * WF_CTL_WORDS;
+    v.rcnt += h * 3 * kRegions;
     v.capacity = wb.capacity / 2;
+    v.qcap = wb.qcap / 2;
     return v;
 }
 
@@ -471,8 +585,15 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         const uint32_t FA = dual && Fb >= 2 ? (Fb + 1) / 2 : Fb, FB = Fb - FA;
-        const WfBuffers A = FB ? wb_half(wb, 0, 0) : wb;
-        const WfBuffers B = wb_half(wb, 1, (size_t)FA * npix * 3);
+        WfBuffers A = FB ? wb_half(wb, 0, 0) : wb;
+        WfBuffers B = wb_half(wb, 1, (size_t)FA * npix * 3);
+        if constexpr (TRAV >= 400) {  // region-partitioned queues (k_wf_step_bf)
+            const uint32_t R = std::min<uint32_t>(kRegions, (uint32_t)tblocks * (kTraceBlock / 64));
+            for (WfBuffers* v : {&A, &B}) {
+                v->nreg = R;
+                v->rstride = v->qcap / R / 64 * 64;  // R * rstride >= paths of the half (qcap slack)
+            }
+        }
         struct Half { const WfBuffers* w; uint32_t fbase, P; hipStream_t st; };
         const int nh = FB ? 2 : 1;
         Half hv[2] = {{&A, fb, FA * npix, FB ? ws.aux[0] : stream}, {&B, fb + FA, FB * npix, ws.aux[1]}};
@@ -481,7 +602,8 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
             for (int h = 0; h < 2; ++h) HIP_RETURN_IF(hipStreamWaitEvent(ws.aux[h], ws.fork, 0));
         }
         for (int h = 0; h < nh; ++h)
-            PT_LAUNCH(KID_WF_GENERATE, hv[h].st, (k_wf_generate<COUNT>), dim3((hv[h].P + 255) / 256), dim3(256), 0, hv[h].st,
+            PT_LAUNCH(KID_WF_GENERATE, hv[h].st, (k_wf_generate<COUNT>),
+                      dim3((std::max(hv[h].P, hv[h].w->nreg) + 255) / 256), dim3(256), 0, hv[h].st,
                       fp, *hv[h].w, frame0, stride, hv[h].fbase, hv[h].P, !accum, cnt);
         // Optional staggering (PT_STAGGER=1; measured slower: 1026 vs 1231 Msamples/s): B's trace
         // i waits for A's trace i and A's trace i+1 for B's trace i, so the persistent trace
@@ -494,7 +616,15 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                 const WfBuffers& w = *hv[h].w;
                 const int sblocks = (int)((hv[h].P + kShadeBlock - 1) / kShadeBlock);
                 if (stagger && (h == 1 || it > 0)) HIP_RETURN_IF(hipStreamWaitEvent(st, ws.traced[1 - h], 0));
-                if constexpr (TRAV >= 300)
+                if constexpr (TRAV >= 400) {  // trace + shade in one launch
+                    if ((it & 1) == 0)
+                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<true, LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
+                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
+                    else
+                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
+                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
+                    continue;
+                } else if constexpr (TRAV >= 300)
                     PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
                               dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
                 else
@@ -543,7 +673,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     // brute force + replay (k_wf_trace_bf) by default for mailbox scenes; an explicit PT_TRAV
     // or PT_BF=0 keeps the traversal kernels
     const bool bf = lo.bf != 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0;
-    const int trav = bf ? 300 + (fast ? 10 : 0)
+    const int trav = bf ? (lo.fuse != 0 ? 400 : 300) + (fast ? 10 : 0)
                    : mb ? 100 + base + (fast ? 10 : 0)
                         : base + ((base >= 3 && fast) ? 10 : 0) + ((base >= 3 && fast && pipe) ? 20 : 0) +
                               ((base >= 3 && fast && ifif && !pipe) ? 40 : 0);
@@ -555,12 +685,12 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     if (lds) {
         WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7) WF(true, 8)
         WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18) WF(true, 35) WF(true, 36) WF(true, 37) WF(true, 55) WF(true, 56) WF(true, 57)
-        WF(true, 300) WF(true, 310)
+        WF(true, 300) WF(true, 310) WF(true, 400) WF(true, 410)
         WF(true, 105) WF(true, 106) WF(true, 107) WF(true, 115) WF(true, 116) WF(true, 117) WF(true, 118)
     } else {
         WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
         WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18) WF(false, 35) WF(false, 36) WF(false, 37) WF(false, 55) WF(false, 56) WF(false, 57)
-        WF(false, 300) WF(false, 310)
+        WF(false, 300) WF(false, 310) WF(false, 400) WF(false, 410)
         WF(false, 105) WF(false, 106) WF(false, 107) WF(false, 115) WF(false, 116) WF(false, 117) WF(false, 118)
     }
 #undef WF

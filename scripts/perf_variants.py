@@ -70,6 +70,12 @@ VARIANTS = {
     "wf_lean8_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_PIPE": "1"},
     "wf_lean4_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_PIPE": "1"},
     "wf_bf": {"PT_KERNEL": "wavefront"},
+    "wf_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
+    "wf_bf_nofuse_2blk": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "512"},
+    "wf_bf_16M": {"PT_KERNEL": "wavefront", "PT_WF_PATHS": "16777216"},
+    "wf_bf_32M": {"PT_KERNEL": "wavefront", "PT_WF_PATHS": "33554432"},
+    "wf_bf_3blk": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "768"},
+    "wf_bf_2blk": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "512"},
     "wf_bf_div": {"PT_KERNEL": "wavefront", "PT_FASTRCP": "0"},
     "wf_nomb": {"PT_KERNEL": "wavefront", "PT_MAILBOX": "0"},
     "wf_mb16": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16"},
@@ -85,7 +91,7 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 
