@@ -495,6 +495,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_PERSIST")) lo.persist = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_FUSE")) lo.fuse = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_BF")) lo.bf = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_MAILBOX")) lo.mailbox = std::strcmp(e, "0") != 0 ? 1 : 0;
@@ -510,9 +511,10 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     if (paths > 0x7fffffffull) return fail(PT_ERR_INVALID, "image too large for one wavefront batch");
     if (s->d_wf) { hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; }
     const size_t n = paths;
-    // queue arrays carry slack so that each half can be cut into kRegions regions of a whole
-    // number of 64-entry batches holding all its paths (k_wf_step_bf)
-    const size_t qn = n + 2 * (size_t)kRegions * 64;
+    // queue arrays carry slack so that each half can be cut into up to kQueueSlackRegions / 1.5
+    // regions of a whole number of 64-entry batches holding all its paths (k_wf_step_bf,
+    // k_wf_persist_bf)
+    const size_t qn = n + 2 * (size_t)kQueueSlackRegions * 64;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
     size_t oq[6];

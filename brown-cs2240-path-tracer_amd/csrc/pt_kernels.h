@@ -65,6 +65,7 @@ struct LaunchOpts {
     int mailbox = -1;      // mailboxed lean traversal where SceneView::mailbox allows it: -1 default (on)
     int bf = -1;           // wavefront, mailbox scenes: brute-force + replay trace kernel: -1 default (on)
     int fuse = -1;         // bf trace fused with the shading (k_wf_step_bf): -1 default (on)
+    int persist = -1;      // fused bf as one workgroup-local launch per batch (k_wf_persist_bf): -1 default (off)
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
 
@@ -104,6 +105,10 @@ struct WfBuffers {
     uint32_t nreg;
 };
 constexpr uint32_t kRegions = 512;
+// queue slack (entries per half = 64 * this): regions of R <= 2/3 of it hold ceil(batches / R)
+// 64-entry batches each (k_wf_persist_bf uses one region per workgroup, at most kPersistMaxBlocks)
+constexpr uint32_t kQueueSlackRegions = 4096;
+constexpr uint32_t kPersistMaxBlocks = 2048;
 constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 
 // Dual-stream wavefront: two streams owned by the scene, created back to back so that HIP's

@@ -355,77 +355,153 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
     if (COUNT) flush_counters(c, cnt_out);
 }
 
-// Trace + shade in one launch (mailbox scenes): the wave that traced a batch of 64 queue
-// entries (bf_closest) shades them at once — the hit never goes through HBM and the ray record
-// is read once — and appends the surviving paths to the other queue.  Queues are cut into
-// wb.nreg regions (k_wf_generate deals 64-path batches round-robin); the waves w ≡ r (mod
+// One batch of 64 entries of queue `in` (EXT: extension rays, else shadow rays) at entries
+// rbase + b * 64 + lane (valid: b * 64 + lane < count): bf_closest, then the path logic of
+// k_wf_shade (pt_path.h, so the same bits) in the same wave — the hit never goes through HBM
+// and the ray record is read once — and the survivors appended to region rbase of the other
+// queue at offsets from `append(n)` (wave-uniform: called by lane 0, result broadcast).
+template <bool EXT, bool FAST_RCP, bool COUNT, class Append>
+__device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gtris, const FrameParams& fp,
+                                              const WfBuffers& wb, size_t rbase, uint32_t b, uint32_t count,
+                                              const BfLds& l, int nslots, Counters& c, Append append) {
+    const WfQueue& in = EXT ? wb.ext : wb.shd;
+    const WfQueue& out = EXT ? wb.shd : wb.ext;
+    const uint32_t lane = lane_id();
+    const bool valid = b * 64 + lane < count;
+    const size_t e = rbase + (valid ? b * 64 + lane : 0);
+    const float4 a0 = in.ray[2 * e], a1 = in.ray[2 * e + 1];
+    uint32_t p;
+    Ray r = unpack_ray(valid ? a0 : make_float4(0, 0, 0, 1), valid ? a1 : make_float4(0, 0, 0, 0), p);
+    float t;
+    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t);
+    bool more = false;
+    PathState ps;
+    if (valid) {
+        const float4 c2 = in.q2[e], d3 = in.q3[e];
+        unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
+        ps.L = mk(c2.x, c2.y, c2.z);
+        ps.seed = __builtin_bit_cast(uint32_t, c2.w);
+        ps.beta = mk(d3.x, d3.y, d3.z);
+        if (EXT) {
+            more = path_after_ext(sc, rec, t, r, ps);
+            if (more && COUNT) c.shadow_queries++;
+        } else {
+            load_shading_point(wb, (uint32_t)e, ps);
+            more = path_after_shadow(sc, fp, rec, t, r, ps);
+            if (more && COUNT) c.ext_queries++;
+        }
+        if (!more) {
+            float* o = wb.rad + 3 * (size_t)p;
+            o[0] = ps.L.x; o[1] = ps.L.y; o[2] = ps.L.z;
+        }
+    }
+    const uint64_t keep = __ballot(more);
+    if (keep) {  // wave-uniform
+        uint32_t base = 0;
+        if (lane == 0) base = append((uint32_t)__popcll(keep));
+        base = __shfl(base, 0, 64);
+        if (more) {
+            const uint32_t j = (uint32_t)rbase + base + rank_below(keep);
+            store_entry(out, j, r, p, ps);
+            if (EXT) store_shading_point(wb, j, ps);
+        }
+    }
+}
+
+// Trace + shade in one launch per iteration (mailbox scenes; PT_PERSIST=0): queues are cut
+// into wb.nreg regions (k_wf_generate deals 64-path batches round-robin); the waves w ≡ r (mod
 // nreg) serve region r of the input and append to region r of the output, one atomicAdd per
 // wave and batch on that region's counter (a counter shared by all waves serialises at one
 // memory channel, and each wave waits for its add: measured 2x slower).  A region's output
 // never exceeds its input, so every region holds its paths through all bounces.  Iteration
 // `it` reads the counts of slot it % 3, appends to slot (it + 1) % 3 and zeroes slot
 // (it + 2) % 3 for iteration it + 1 (iteration it - 1 read that slot and it - 2 wrote it, both
-// finished: stream order).  Same path logic (pt_path.h) as k_wf_shade, so the same bits.
+// finished: stream order).
 template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock) void k_wf_step_bf(SceneView sc, FrameParams fp, WfBuffers wb, int it,
                                                            Counters* cnt_out, int nslots) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const BfLds l = bf_lds(smem, sc);
-    const uint32_t lane = lane_id();
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
     const uint32_t R = wb.nreg;  // <= nwaves (host)
     const uint32_t rg = w % R, g = w / R, G = (nwaves - rg + R - 1) / R;
-    if (g == 0 && lane == 0) wb.rcnt[((it + 2) % 3) * kRegions + rg] = 0;
+    if (g == 0 && lane_id() == 0) wb.rcnt[((it + 2) % 3) * kRegions + rg] = 0;
     const uint32_t count = wb.rcnt[(it % 3) * kRegions + rg];
     uint32_t* out_count = &wb.rcnt[((it + 1) % 3) * kRegions + rg];
-    const size_t rbase = (size_t)rg * wb.rstride;
     const Tri* gtris = sc.tris;  // global records for phase 1
     if (LDS) stage_scene_lds(sc, l.scene);
     const uint32_t nb = (count + 63) / 64;
-    const WfQueue& in = EXT ? wb.ext : wb.shd;
-    const WfQueue& out = EXT ? wb.shd : wb.ext;
     Counters c = {};
-    for (uint32_t b = g; b < nb; b += G) {  // this region's batches, interleaved over its waves
-        const bool valid = b * 64 + lane < count;
-        const size_t e = rbase + (valid ? b * 64 + lane : 0);
-        const float4 a0 = in.ray[2 * e], a1 = in.ray[2 * e + 1];
-        uint32_t p;
-        Ray r = unpack_ray(valid ? a0 : make_float4(0, 0, 0, 1), valid ? a1 : make_float4(0, 0, 0, 0), p);
-        float t;
-        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t);
-        bool more = false;
-        PathState ps;
-        if (valid) {
-            const float4 c2 = in.q2[e], d3 = in.q3[e];
-            unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
-            ps.L = mk(c2.x, c2.y, c2.z);
-            ps.seed = __builtin_bit_cast(uint32_t, c2.w);
-            ps.beta = mk(d3.x, d3.y, d3.z);
-            if (EXT) {
-                more = path_after_ext(sc, rec, t, r, ps);
-                if (more && COUNT) c.shadow_queries++;
-            } else {
-                load_shading_point(wb, (uint32_t)e, ps);
-                more = path_after_shadow(sc, fp, rec, t, r, ps);
-                if (more && COUNT) c.ext_queries++;
-            }
-            if (!more) {
-                float* o = wb.rad + 3 * (size_t)p;
-                o[0] = ps.L.x; o[1] = ps.L.y; o[2] = ps.L.z;
-            }
+    for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves
+        bf_step_batch<EXT, FAST_RCP, COUNT>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
+                                            [&](uint32_t n) { return atomicAdd(out_count, n); });
+    if (COUNT) flush_counters(c, cnt_out);
+}
+
+// One launch per batch of paths (mailbox scenes, the default): workgroup g owns region g of the
+// queues — the 64-path batches j ≡ g (mod gridDim.x) of the batch's P paths — and runs all of
+// their bounces alone.  Its 8 waves write the camera rays, then in every iteration take the
+// region's 64-entry queue batches from an LDS counter, trace + shade them (bf_step_batch) and
+// append survivors through another LDS counter; a workgroup barrier ends the iteration (its
+// global stores are visible to the workgroup's other waves after it: one CU, one L1).  No
+// grid-wide step between bounces: no kernel boundary per bounce, no global atomics, and a
+// workgroup waiting at its barrier leaves the CU to the other resident workgroups.
+template <bool LDS, bool FAST_RCP, bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) void k_wf_persist_bf(SceneView sc, FrameParams fp, WfBuffers wb, uint32_t frame0,
+                                                              uint32_t stride, uint32_t fbase, uint32_t P, bool raw_salt,
+                                                              int iters, Counters* cnt_out, int nslots) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ uint32_t s_cnt[2], s_next;
+    const BfLds l = bf_lds(smem, sc);
+    const uint32_t lane = lane_id();
+    const uint32_t R = gridDim.x, rg = blockIdx.x;
+    const size_t rbase = (size_t)rg * wb.rstride;
+    const uint32_t nbat = (P + 63) / 64;
+    const uint32_t nmine = rg < nbat ? (nbat - rg + R - 1) / R : 0u;  // this region's 64-path batches
+    const Tri* gtris = sc.tris;  // global records for phase 1
+    if (LDS) stage_scene_lds(sc, l.scene);
+    Counters c = {};
+    const uint32_t wv = threadIdx.x / 64, nwv = blockDim.x / 64;
+    const uint32_t npix = fp.width * fp.height;
+    for (uint32_t k = wv; k < nmine; k += nwv) {  // camera rays: local batch k = global batch rg + k R
+        const uint32_t p = (rg + k * R) * 64 + lane;
+        if (p < P) {
+            uint32_t x, y, f;
+            path_pixel(p, npix, fp.width, x, y, f);
+            const uint32_t t = raw_salt ? frame0 : (uint32_t)(float)(frame0 + (fbase + f) * stride);
+            PathState ps;
+            const Ray r = path_begin(fp, x, y, t, ps);
+            store_entry(wb.ext, (uint32_t)(rbase + k * 64 + lane), r, p, ps);
+            if (COUNT) { c.samples++; c.ext_queries++; }
         }
-        const uint64_t keep = __ballot(more);
-        if (keep) {  // wave-uniform
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(out_count, (uint32_t)__popcll(keep));
-            base = __shfl(base, 0, 64);
-            if (more) {
-                const uint32_t j = (uint32_t)rbase + base + rank_below(keep);
-                store_entry(out, j, r, p, ps);
-                if (EXT) store_shading_point(wb, j, ps);
-            }
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t last = rg + (nmine - 1) * R;
+        s_cnt[0] = nmine == 0 ? 0u : nmine * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
+        s_cnt[1] = 0;
+        s_next = 0;
+    }
+    __syncthreads();
+    for (int it = 0; it < iters; ++it) {
+        const uint32_t count = s_cnt[it & 1];
+        uint32_t* out_cnt = &s_cnt[(it + 1) & 1];
+        const uint32_t nb = (count + 63) / 64;
+        while (true) {  // the region's batches, handed to the waves as they come free
+            uint32_t b = 0;
+            if (lane == 0) b = atomicAdd(&s_next, 1u);
+            b = __shfl(b, 0, 64);
+            if (b >= nb) break;
+            auto append = [&](uint32_t n) { return atomicAdd(out_cnt, n); };
+            if ((it & 1) == 0) bf_step_batch<true, FAST_RCP, COUNT>(sc, gtris, fp, wb, rbase, b, count, l, nslots, c, append);
+            else bf_step_batch<false, FAST_RCP, COUNT>(sc, gtris, fp, wb, rbase, b, count, l, nslots, c, append);
         }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // this input count becomes iteration it + 1's output count
+            s_cnt[it & 1] = 0;
+            s_next = 0;
+        }
+        __syncthreads();
     }
     if (COUNT) flush_counters(c, cnt_out);
 }
@@ -525,7 +601,8 @@ __global__ __launch_bounds__(256) void k_wf_accum(const float* __restrict__ rad,
 // with the shading (k_wf_step_bf)
 template <bool LDS, int TRAV, bool COUNT>
 constexpr const void* trace_kernel() {
-    if constexpr (TRAV >= 400) return (const void*)k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>;
+    if constexpr (TRAV >= 500) return (const void*)k_wf_persist_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
+    else if constexpr (TRAV >= 400) return (const void*)k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>;
     else if constexpr (TRAV >= 300) return (const void*)k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
     else return (const void*)k_wf_trace<LDS, TRAV, COUNT>;
 }
@@ -582,6 +659,21 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     const int iters = 2 * (fp.max_depth + 1);
     int bf_slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
     if (const char* e = std::getenv("PT_BF_SLOTS")) bf_slots = std::max(0, std::min(kBfSlots, std::atoi(e)));
+    if constexpr (TRAV >= 500) {  // one workgroup-local launch per batch (k_wf_persist_bf), one stream
+        const uint32_t Fp = std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
+        const uint32_t nblk = std::min<uint32_t>((uint32_t)tblocks, kPersistMaxBlocks);
+        WfBuffers w = wb;
+        w.rstride = w.qcap / nblk / 64 * 64;  // >= ceil(batches / nblk) * 64 (queue slack)
+        for (uint32_t fb = 0; fb < nframes; fb += Fp) {
+            const uint32_t Fb = std::min(Fp, nframes - fb);
+            PT_LAUNCH(KID_WF_STEP, stream, (k_wf_persist_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(nblk),
+                      dim3(kTraceBlock), lds, stream, sc, fp, w, frame0, stride, fb, Fb * npix, !accum, iters, cnt,
+                      bf_slots);
+            PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix,
+                      Fb, accum);
+        }
+        return hipGetLastError();
+    }
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         const uint32_t FA = dual && Fb >= 2 ? (Fb + 1) / 2 : Fb, FB = Fb - FA;
@@ -673,7 +765,9 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     // brute force + replay (k_wf_trace_bf) by default for mailbox scenes; an explicit PT_TRAV
     // or PT_BF=0 keeps the traversal kernels
     const bool bf = lo.bf != 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0;
-    const int trav = bf ? (lo.fuse != 0 ? 400 : 300) + (fast ? 10 : 0)
+    // k_wf_persist_bf (PT_PERSIST=1) measured slower: 1771 vs 2207 Msamples/s (its workgroups idle
+    // at the per-iteration barrier once a region's queue is down to a few batches)
+    const int trav = bf ? (lo.fuse == 0 ? 300 : lo.persist > 0 ? 500 : 400) + (fast ? 10 : 0)
                    : mb ? 100 + base + (fast ? 10 : 0)
                         : base + ((base >= 3 && fast) ? 10 : 0) + ((base >= 3 && fast && pipe) ? 20 : 0) +
                               ((base >= 3 && fast && ifif && !pipe) ? 40 : 0);
@@ -685,12 +779,12 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     if (lds) {
         WF(true, 1) WF(true, 2) WF(true, 3) WF(true, 4) WF(true, 5) WF(true, 6) WF(true, 7) WF(true, 8)
         WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18) WF(true, 35) WF(true, 36) WF(true, 37) WF(true, 55) WF(true, 56) WF(true, 57)
-        WF(true, 300) WF(true, 310) WF(true, 400) WF(true, 410)
+        WF(true, 300) WF(true, 310) WF(true, 400) WF(true, 410) WF(true, 500) WF(true, 510)
         WF(true, 105) WF(true, 106) WF(true, 107) WF(true, 115) WF(true, 116) WF(true, 117) WF(true, 118)
     } else {
         WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
         WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18) WF(false, 35) WF(false, 36) WF(false, 37) WF(false, 55) WF(false, 56) WF(false, 57)
-        WF(false, 300) WF(false, 310) WF(false, 400) WF(false, 410)
+        WF(false, 300) WF(false, 310) WF(false, 400) WF(false, 410) WF(false, 500) WF(false, 510)
         WF(false, 105) WF(false, 106) WF(false, 107) WF(false, 115) WF(false, 116) WF(false, 117) WF(false, 118)
     }
 #undef WF

@@ -72,6 +72,11 @@ VARIANTS = {
     "wf_bf": {"PT_KERNEL": "wavefront"},
     "wf_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
     "wf_bf_nofuse_2blk": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "512"},
+    "wf_bf_step": {"PT_KERNEL": "wavefront", "PT_PERSIST": "0"},
+    "wf_persist_2blk": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "512"},
+    "wf_persist_1024": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "1024"},
+    "wf_bf_single": {"PT_KERNEL": "wavefront", "PT_DUAL": "0"},
+    "wf_bf_32M_single": {"PT_KERNEL": "wavefront", "PT_DUAL": "0", "PT_WF_PATHS": "33554432"},
     "wf_bf_16M": {"PT_KERNEL": "wavefront", "PT_WF_PATHS": "16777216"},
     "wf_bf_32M": {"PT_KERNEL": "wavefront", "PT_WF_PATHS": "33554432"},
     "wf_bf_3blk": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "768"},
@@ -91,7 +96,7 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

@@ -50,6 +50,10 @@ KERNELS = {
     "wavefront_mailbox_rev": {"PT_KERNEL": "wavefront", "PT_MB_UID_ORDER": "reverse"},
     "wavefront_mb_lean16_rev": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
     "wavefront_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
+    "wavefront_persist": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1"},
+    "wavefront_bf_step_3blocks": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "3"},
+    "wavefront_persist_3blocks_div": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1", "PT_WF_TRACE_BLOCKS": "3",
+                                      "PT_FASTRCP": "0"},
     "wavefront_bf_nofuse_1block": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "1"},
     "wavefront_bf_global_noslots": {"PT_KERNEL": "wavefront", "PT_LDS": "0", "PT_BF_SLOTS": "0"},
     "wavefront_bf_2slots_div": {"PT_KERNEL": "wavefront", "PT_BF_SLOTS": "2", "PT_FASTRCP": "0"},
@@ -59,7 +63,7 @@ KERNELS = {
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
-            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE")
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -268,11 +272,19 @@ def test_profile_records_every_launch(packed, monkeypatch):
         s.render(meta, 0, 1, 1, depth, pt_amd.MODE_WAVEFRONT)
         assert s.profile_read() == {}
     assert set(mega) == {"k_regen"} and mega["k_regen"]["launches"] == 1
-    # CornellBox is a mailbox scene: the fused trace + shade kernel, one launch per half and step
+    # CornellBox is a mailbox scene: fused trace + shade, one launch per half and step; one batch
+    # (4 frames of 64^2 fit) in two halves on two streams (dual-stream wavefront)
     assert set(wf) == {"k_wf_generate", "k_wf_step", "k_wf_accum"}
-    # one batch (4 frames of 64^2 fit) in two halves on two streams (dual-stream wavefront)
     assert wf["k_wf_step"]["launches"] == 2 * 2 * (depth + 1)
     assert wf["k_wf_generate"]["launches"] == 2 and wf["k_wf_accum"]["launches"] == 1
+    monkeypatch.setenv("PT_PERSIST", "1")  # one workgroup-local trace + shade launch per batch
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
+        wf1 = s.profile_read()
+    assert set(wf1) == {"k_wf_step", "k_wf_accum"}
+    assert wf1["k_wf_step"]["launches"] == 1 and wf1["k_wf_accum"]["launches"] == 1
+    monkeypatch.delenv("PT_PERSIST")
     monkeypatch.setenv("PT_FUSE", "0")  # separate trace and shade kernels
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
@@ -281,7 +293,7 @@ def test_profile_records_every_launch(packed, monkeypatch):
     assert set(wf2) == {"k_wf_generate", "k_wf_trace", "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum"}
     assert wf2["k_wf_trace"]["launches"] == 2 * 2 * (depth + 1)
     assert wf2["k_wf_shade_ext"]["launches"] == wf2["k_wf_shade_shadow"]["launches"] == 2 * (depth + 1)
-    for v in list(mega.values()) + list(wf.values()) + list(wf2.values()):
+    for v in list(mega.values()) + list(wf.values()) + list(wf1.values()) + list(wf2.values()):
         assert 0.0 < v["min_ms"] <= v["avg_ms"] <= v["max_ms"] and v["total_ms"] > 0.0
 
 
@@ -344,9 +356,10 @@ def packed_tie(tmp_path_factory):
 @pytest.mark.parametrize("env", [{}, {"PT_MB_UID_ORDER": "reverse"}, {"PT_MAILBOX": "0"},
                                  {"PT_MB_UID_ORDER": "reverse", "PT_BF_SLOTS": "1"},
                                  {"PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
-                                 {"PT_FUSE": "0", "PT_MB_UID_ORDER": "reverse"}],
+                                 {"PT_FUSE": "0", "PT_MB_UID_ORDER": "reverse"},
+                                 {"PT_PERSIST": "1", "PT_MB_UID_ORDER": "reverse"}],
                          ids=["bf", "bf_reverse_uids", "no_mailbox", "bf_reverse_1slot", "mb_lean16_reverse",
-                              "bf_nofuse_reverse"])
+                              "bf_nofuse_reverse", "persist_reverse"])
 def test_mailbox_exact_ties(packed_tie, monkeypatch, env):
     for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
