@@ -13,8 +13,10 @@ dominant kernel (the one with the most HIP-event time in the timed region, recor
 library around every launch on the render stream: pt_profile_enable/pt_profile_read).
 Its algorithmic bytes per launch follow SURVEY.md §8d from the GPU's own work counters:
 k_wf_trace (wavefront) moves 48 B per ray query (32 B ray read + 16 B hit write), so a launch
-carries 48*Q / launches; the megakernel k_regen carries the whole path model
-B_alg = 48*Q + 96*Q_ext + 24 B per sample in one launch.  `pipeline` gives B_alg over the
+carries 48*Q / launches; the fused trace + shade kernel k_wf_step (the default on Cornell boxes)
+carries 48*Q + 96*Q_ext (the path model without camera rays and accumulation) / launches; the
+megakernel k_regen carries the whole path model B_alg = 48*Q + 96*Q_ext + 24 B per sample in
+one launch.  `pipeline` gives B_alg over the
 whole render.  `cpu_baseline` is the C oracle (oracle/pt_oracle.c) on the host cores, rank 0
 at N=1 only.
 """
@@ -87,10 +89,12 @@ def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world
         return None
     key = f"{W}x{H}x{spp}x{depth}x{world}"
     cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix)}
-    timed = [k for k in cands if k.endswith("false>")]  # COUNT=false: the timed (uncounted) instance
-    for k in timed or list(cands):
-        return cands[k]["hbm_bytes_per_launch"]
-    return None
+    # COUNT=false: the timed (uncounted) instances; the fused kernel has one per queue (extension /
+    # shadow), launched equally often, so their mean is the mean per launch
+    timed = [k for k in cands if k.endswith("false>")] or list(cands)
+    if not timed:
+        return None
+    return sum(cands[k]["hbm_bytes_per_launch"] for k in timed) / len(timed)
 
 
 def main():
@@ -199,6 +203,8 @@ def main():
         k_ms = prof[kernel]["avg_ms"]
         if kernel == "k_wf_trace":
             bytes_per_launch = 48.0 * (q_ext + q_sh) / launches_per_render
+        elif kernel == "k_wf_step":  # fused trace + shade: the path model minus camera rays and accumulation
+            bytes_per_launch = (48.0 * (q_ext + q_sh) + 96.0 * q_ext) / launches_per_render
         else:  # the megakernel: the whole path model in one launch
             bytes_per_launch = b_alg / launches_per_render
         achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
@@ -207,7 +213,8 @@ def main():
     pipeline = b_alg / (r_ms * 1e-3) / 1e9
 
     if rank == 0:
-        traffic = load_traffic(kernel + "<", W, H, args.spp, args.depth, world)
+        prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<", "k_wf_persist_bf<")}
+        traffic = load_traffic(prefixes.get(kernel, (kernel + "<",)), W, H, args.spp, args.depth, world)
         out = {
             "metric": "Msamples/s (paths/s) CornellBox 1024^2 depth 8",
             "value": round(value, 3),
