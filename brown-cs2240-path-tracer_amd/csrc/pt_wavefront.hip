@@ -417,8 +417,10 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
 // `it` reads the counts of slot it % 3, appends to slot (it + 1) % 3 and zeroes slot
 // (it + 2) % 3 for iteration it + 1 (iteration it - 1 read that slot and it - 2 wrote it, both
 // finished: stream order).
+// amdgpu_waves_per_eu(8): the path logic pushed the kernel to 75 VGPRs (6 waves/SIMD); capped
+// at 64 it keeps 8 waves/SIMD with no VGPR spills (a few SGPR spills to VGPR lanes): +7 %
 template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) void k_wf_step_bf(SceneView sc, FrameParams fp, WfBuffers wb, int it,
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_wf_step_bf(SceneView sc, FrameParams fp, WfBuffers wb, int it,
                                                            Counters* cnt_out, int nslots) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const BfLds l = bf_lds(smem, sc);
