@@ -56,6 +56,7 @@ struct HostLayout {
     std::vector<Material> mats;
     std::vector<Light> lights;
     std::vector<uint64_t> lmask;  // mailbox scenes: uid set per leaf, indexed by first record
+    std::vector<float4> tnorm;    // vertex-normal mode: 3 per record (SceneView::tnorm)
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -146,6 +147,15 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                     t.mat = mat;
                     t.uid = -1;
                     L.tris.push_back(t);
+                    {   // vertex normals at vn_start + i (i = (index - 1) * 3, the vertex offsets;
+                        // intersection-logic.wgsl:81-97), reads clamped as Tint's
+                        const int32_t vi[3] = {(wgsl_i32(e[0]) - 1) * 3, (wgsl_i32(e[1]) - 1) * 3, (wgsl_i32(e[2]) - 1) * 3};
+                        const int32_t vn_start = wgsl_i32(tri[5]), vn_range = wgsl_i32(tri[6]);
+                        for (int q = 0; q < 3; ++q)
+                            L.tnorm.push_back(make_float4(P.at(vn_start + vi[q]), P.at(vn_start + vi[q] + 1),
+                                                          P.at(vn_start + vi[q] + 2),
+                                                          (q == 0 && vi[2] < vn_range) ? 1.0f : 0.0f));
+                    }
                     entry.push_back({wgsl_i32(e[0]), wgsl_i32(e[1]), wgsl_i32(e[2]), mat});
                 }
                 leaf_ranges.emplace_back(refs[side], n);
@@ -192,6 +202,10 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             std::vector<Tri> uniq((size_t)U);
             for (size_t k = 0; k < first.size(); ++k) uniq[(size_t)uid[first[k]]] = L.tris[first[k]];
             L.tris.insert(L.tris.end(), uniq.begin(), uniq.end());
+            std::vector<float4> un(3 * (size_t)U);
+            for (size_t k = 0; k < first.size(); ++k)
+                for (int q = 0; q < 3; ++q) un[3 * (size_t)uid[first[k]] + q] = L.tnorm[3 * first[k] + q];
+            L.tnorm.insert(L.tnorm.end(), un.begin(), un.end());
             L.lmask.assign(std::max<size_t>(1, entry.size()), 0);
             for (const auto& lr : leaf_ranges)
                 for (int32_t k = 0; k < lr.second; ++k) L.lmask[(size_t)lr.first] |= 1ull << uid[(size_t)(lr.first + k)];
@@ -382,7 +396,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_lights = align_up(o_mats + L.mats.size() * sizeof(Material), 256);
     const size_t o_lmask = align_up(o_lights + L.lights.size() * sizeof(Light), 16);
     const size_t o_cnt = align_up(o_lmask + L.lmask.size() * sizeof(uint64_t), 256);
-    const size_t total = align_up(o_cnt + sizeof(Counters), 256);
+    const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
+    const size_t total = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -392,7 +407,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_tris, L.tris.data(), L.tris.size() * sizeof(Tri)) != hipSuccess ||
         up(o_mats, L.mats.data(), L.mats.size() * sizeof(Material)) != hipSuccess ||
         up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess ||
-        up(o_lmask, L.lmask.data(), L.lmask.size() * sizeof(uint64_t)) != hipSuccess) {
+        up(o_lmask, L.lmask.data(), L.lmask.size() * sizeof(uint64_t)) != hipSuccess ||
+        up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -415,6 +431,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.off_lmask = (uint32_t)(o_lmask - o_nodes);
     s->view.lmask = reinterpret_cast<const uint64_t*>(base + o_lmask);
     s->view.mailbox = L.mailbox ? 1 : 0;
+    s->view.tnorm = reinterpret_cast<const float4*>(base + o_tn);
+    s->view.vnormals = 0;
     s->view.mb_base = L.mb_base;
     s->view.span_bytes = (uint32_t)align_up(o_lmask + L.lmask.size() * sizeof(uint64_t) - o_nodes, 16);
     s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);
@@ -440,6 +458,12 @@ void pt_scene_destroy(pt_scene* s) {
     if (s->d_mem) hipFree(s->d_mem);
     s->prof.destroy();
     delete s;
+}
+
+int pt_scene_set_vertex_normals(pt_scene* s, int enable) {
+    if (!s) return fail(PT_ERR_INVALID, "null scene");
+    s->view.vnormals = enable ? 1 : 0;
+    return PT_OK;
 }
 
 int pt_scene_get_info(const pt_scene* s, pt_scene_info* out) {

@@ -527,8 +527,24 @@ __device__ __forceinline__ Hit hit_data(const SceneView& sc, const Ray& r, int r
     const TriRec tr = load_tri(sc.tris, rec);
     Hit h;
     h.p = madd(r.o, r.d, t);
-    h.n = normalize(cross(mk(tr.a.w, tr.b.x, tr.b.y), mk(tr.b.z, tr.b.w, tr.c)));
+    const f3 e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
+    h.n = normalize(cross(e1, e2));
     h.mat = sc.tris[rec].mat;
+    if (sc.vnormals) {
+        const float4 n0 = sc.tnorm[3 * rec];
+        if (n0.w != 0.0f) {  // ray-triangle-intersection.wgsl:44-87: the test's u, v, then the blend
+            const float4 n1 = sc.tnorm[3 * rec + 1], n2 = sc.tnorm[3 * rec + 2];
+            const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z);
+            const f3 rce2 = cross(r.d, e2);
+            const float inv_det = 1.0f / dot(e1, rce2);
+            const f3 s = r.o - v0;
+            const float u = inv_det * dot(s, rce2);
+            const float v = inv_det * dot(r.d, cross(s, e1));
+            const float w = (1.0f - u) - v;
+            h.n = normalize(mk(fmaf(v, n2.x, fmaf(u, n1.x, w * n0.x)), fmaf(v, n2.y, fmaf(u, n1.y, w * n0.y)),
+                               fmaf(v, n2.z, fmaf(u, n1.z, w * n0.z))));
+        }
+    }
     return h;
 }
 

@@ -94,6 +94,11 @@ struct SceneView {
     int32_t mb_base;
     uint32_t off_lmask;
     const uint64_t* lmask;
+    // vertex-normal mode (pt_scene_set_vertex_normals; the reference's commented-out branch,
+    // intersection-logic.wgsl:81-108): per record (v0n, v1n, v2n) as 3 float4, v0n.w = 1 where
+    // i2 < vn_range (the branch applies); global memory, read for the winning record only
+    const float4* tnorm;
+    int32_t vnormals;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

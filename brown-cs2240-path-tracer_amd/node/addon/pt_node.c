@@ -353,6 +353,22 @@ static napi_value js_profile_enable(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
+/* sceneSetVertexNormals(scene, enable): vertex-normal shading (pt_scene_set_vertex_normals) */
+static napi_value js_scene_set_vertex_normals(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
+    bool on = true;
+    if (!s || (argc > 1 && napi_get_value_bool(env, argv[1], &on) != napi_ok)) {
+        napi_throw_type_error(env, NULL, "sceneSetVertexNormals(scene, enable)");
+        return NULL;
+    }
+    int rc = pt_scene_set_vertex_normals(s, on ? 1 : 0);
+    if (rc) return throw_pt(env, rc);
+    return NULL;
+}
+
 /* profileRead(scene) -> {kernel: {launches, totalMs, minMs, maxMs}} */
 static napi_value js_profile_read(napi_env env, napi_callback_info info) {
     size_t argc = 1;
@@ -391,6 +407,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"profileEnable", NULL, js_profile_enable, NULL, NULL, NULL, napi_enumerable, NULL},
         {"profileRead", NULL, js_profile_read, NULL, NULL, NULL, napi_enumerable, NULL},
         {"bvhBuild", NULL, js_bvh_build, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"sceneSetVertexNormals", NULL, js_scene_set_vertex_normals, NULL, NULL, NULL, napi_enumerable, NULL},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

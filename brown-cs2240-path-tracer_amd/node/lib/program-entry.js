@@ -32,7 +32,8 @@ function make_meta(screenDimension, camera_data, scene_description, time_elapsed
 /**
  * programEntry(screenDimension, primitive_data, camera_data, scene_description, options?)
  *   -> Promise<{accum: Float32Array(W*H*3), sample_runs, rgba: Uint8ClampedArray(W*H*4), counters, scene_info}>
- * options: {device=0, maxDepth=16, mode='auto', frame0=0, chunk=spp, onFrames(done, total), imageOnly=false}
+ * options: {device=0, maxDepth=16, mode='auto', frame0=0, chunk=spp, onFrames(done, total), imageOnly=false,
+ *           vertexNormals=false (the reference's commented-out smooth-normal branch; changes results)}
  * imageOnly: render and tone-map on the device in one call and return only {rgba, counters, ...}
  * (no accumulator crosses PCIe; pt_render_image).
  * As in the reference only primitive_data[0] is rendered (program-raymarch.wgsl:31,33).
@@ -43,6 +44,7 @@ async function programEntry(screenDimension, primitive_data, camera_data, scene_
     const [W, H] = screenDimension;
     const meta = make_meta(screenDimension, camera_data, scene_description, 0);
     const scene = pt.sceneCreate(primitive_data[0].triangle_data, primitive_data[0].bvh_data, o.device);
+    if (o.vertexNormals) pt.sceneSetVertexNormals(scene, true);
     const spp = scene_description.Settings.samplesPerPixel;
     const chunk = Math.max(1, o.chunk || spp);
     const accum = new Float32Array(W * H * 3);

@@ -101,8 +101,10 @@ def load_library():
     L.pt_tonemap_async.argtypes = [p, p, sz, u32, p, p]
     L.pt_render_image.argtypes = [p, p, u32, u32, u32, i, i, p, p]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
+    L.pt_scene_set_vertex_normals.argtypes = [p, i]
     for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image"):
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
+               "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
     _lib = L
     return L
@@ -160,6 +162,10 @@ class Scene:
 
     def __exit__(self, *a):
         self.close()
+
+    def set_vertex_normals(self, enable: bool = True):
+        """Vertex-normal shading (pt_scene_set_vertex_normals; off = the reference's behaviour)."""
+        _check(self._lib.pt_scene_set_vertex_normals(self._h, 1 if enable else 0))
 
     @property
     def info(self) -> dict:

@@ -99,6 +99,15 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
 void pt_scene_destroy(pt_scene* scene);
 int pt_scene_get_info(const pt_scene* scene, pt_scene_info* info_out);
 
+/* Vertex-normal shading (off by default = the reference's behaviour): the
+ * hit normal of a triangle whose third index i2 = (idx2 - 1) * 3 < vn_range (triangle_data[6])
+ * becomes normalize(w*n0 + u*n1 + v*n2) with the test's barycentrics and the normals at
+ * vn_start + (idx - 1) * 3 (triangle_data[5]) — ray_triangle_intersection_vertex_normals
+ * (src/wgsl-util/ray-triangle-intersection.wgsl:44-87), which the reference calls only from
+ * commented-out code (src/wgsl-util/intersection-logic.wgsl:81-108).  Changes results on scenes
+ * with vertex normals.  Applies to later renders of the scene. */
+int pt_scene_set_vertex_normals(pt_scene* scene, int enable);
+
 /* Render frames k = frame0 + i*frame_stride, i < nframes, each 1 spp per pixel, and add
  * clamp(L) (v >= 0 ? v : 0, NaN -> 0) into accum in frame order — the render_loop of
  * program-raymarch.ts:226-335 without the per-frame readback.  accum: host f32

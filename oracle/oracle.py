@@ -50,6 +50,7 @@ def lib():
         L.po_ray_bbox.restype = f; L.po_ray_bbox.argtypes = [p, p, p, p]
         L.po_intersect.restype = i32; L.po_intersect.argtypes = [p, u32, p, u32, p, p, p, p]
         L.po_tonemap.restype = None; L.po_tonemap.argtypes = [p, ctypes.c_uint64, u32, p]
+        L.po_set_vertex_normals.restype = None; L.po_set_vertex_normals.argtypes = [i32]
         _lib = L
     return _lib
 
@@ -129,3 +130,9 @@ def math_fn(name: str, x):
     """Vectorised access to the pinned f32 transcendentals (po_sinf, po_acosf, ...)."""
     fn = getattr(lib(), "po_" + name + "f")
     return np.array([fn(float(v)) for v in np.asarray(x, np.float32)], np.float32)
+
+
+def set_vertex_normals(on: bool):
+    """Vertex-normal mode (the reference's commented-out branch, intersection-logic.wgsl:81-108):
+    process-wide switch of the oracle library."""
+    lib().po_set_vertex_normals(1 if on else 0)

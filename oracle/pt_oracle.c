@@ -261,6 +261,43 @@ static isect_t ray_tri(const ray_t *r, v3 v0, v3 v1, v3 v2) {
     return null_isect();
 }
 
+/* ray-triangle-intersection.wgsl:44-87 (ray_triangle_intersection_vertex_normals): the same test,
+ * normal = normalize(w*v0n + u*v1n + v*v2n), w = 1 - u - v.  The reference calls it only from
+ * commented-out code (intersection-logic.wgsl:81-108); vertex-normal mode (po_set_vertex_normals)
+ * enables that branch.  The a*b+c sites are FMAs, as everywhere in the contract. */
+static isect_t ray_tri_vn(const ray_t *r, v3 v0, v3 v1, v3 v2, v3 n0, v3 n1, v3 n2) {
+    v3 rd = xyz(r->d), ro = xyz(r->p);
+    const float eps = 1e-8f;
+    v3 e1 = sub3(v1, v0), e2 = sub3(v2, v0);
+    v3 rce2 = cross3(rd, e2);
+    float det = dot3(e1, rce2);
+    if (det > -eps && det < eps) return null_isect();
+    float inv_det = 1.0f / det;
+    v3 s = sub3(ro, v0);
+    float u = inv_det * dot3(s, rce2);
+    if (u < 0.0f || u > 1.0f) return null_isect();
+    v3 sce1 = cross3(s, e1);
+    float v = inv_det * dot3(rd, sce1);
+    if (v < 0.0f || u + v > 1.0f) return null_isect();
+    float w = (1.0f - u) - v;
+    float t = inv_det * dot3(e2, sce1);
+    if (t > eps) {
+        isect_t h;
+        v3 p = madd3(ro, rd, t);
+        v3 nn = V3(fmaf(v, n2.x, fmaf(u, n1.x, w * n0.x)), fmaf(v, n2.y, fmaf(u, n1.y, w * n0.y)),
+                   fmaf(v, n2.z, fmaf(u, n1.z, w * n0.z)));
+        v3 n = normalize3(nn);
+        h.point = V4(p.x, p.y, p.z, 1.0f);
+        h.normal = V4(n.x, n.y, n.z, 0.0f);
+        h.intersected = 1; h.t = t; h.material_id = 0;
+        return h;
+    }
+    return null_isect();
+}
+
+static int g_vertex_normals; /* po_set_vertex_normals */
+EXPORT void po_set_vertex_normals(int on) { g_vertex_normals = on != 0; }
+
 static inline v3 vert(const scene_t *s, int32_t v_start, int32_t i) {
     return V3(P(s, v_start + i), P(s, v_start + i + 1), P(s, v_start + i + 2));
 }
@@ -270,9 +307,13 @@ static void test_leaf(const scene_t *s, const ray_t *ray, int32_t lp, isect_t *c
     int32_t o_start = lp + 5 + 12;
     int32_t o_end = o_start + (int32_t)num_triangles;
     int32_t v_start = (int32_t)P(s, 2);
+    int32_t vn_start = (int32_t)P(s, 5), vn_range = (int32_t)P(s, 6);
     for (int32_t i = o_start; i < o_end; i += 4) {
         int32_t i0 = ((int32_t)B(s, i) - 1) * 3, i1 = ((int32_t)B(s, i + 1) - 1) * 3, i2 = ((int32_t)B(s, i + 2) - 1) * 3;
-        isect_t h = ray_tri(ray, vert(s, v_start, i0), vert(s, v_start, i1), vert(s, v_start, i2));
+        isect_t h = (g_vertex_normals && i2 < vn_range)
+                        ? ray_tri_vn(ray, vert(s, v_start, i0), vert(s, v_start, i1), vert(s, v_start, i2),
+                                     vert(s, vn_start, i0), vert(s, vn_start, i1), vert(s, vn_start, i2))
+                        : ray_tri(ray, vert(s, v_start, i0), vert(s, v_start, i1), vert(s, v_start, i2));
         if (c) c->tri_tests++;
         if (h.intersected && (*closest_t < 0.0f || h.t < *closest_t)) {
             *closest = h;

@@ -376,3 +376,37 @@ def test_mailbox_exact_ties(packed_tie, monkeypatch, env):
     racc, rc = oracle.render(p.triangle_data, p.bvh_data, meta, 0, 3, 1, 8)
     assert same_bits(acc, racc), mismatch_report(acc, racc)
     assert gc == rc, (gc, rc)
+
+
+# ---------------------------------------------------------------------------------------------
+# vertex-normal mode: the reference's commented-out smooth-normal branch
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("scene,W,H", [("CornellBox-Glossy", 40, 32), ("CornellBox-Sphere", 40, 32),
+                                       ("MedievalBoat", 24, 16), ("CornellBox", 32, 24)])
+@pytest.mark.parametrize("env", [{"PT_KERNEL": "mega"}, {"PT_KERNEL": "wavefront"},
+                                 {"PT_KERNEL": "wavefront", "PT_FUSE": "0"}], ids=["mega", "wavefront", "wf_nofuse"])
+def test_vertex_normals_bitexact(packed, monkeypatch, scene, W, H, env):
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = packed[scene]
+    meta = p.meta_for(W, H)
+    oracle.set_vertex_normals(True)
+    try:
+        ref, _ = oracle.frame(p.triangle_data, p.bvh_data, meta, 5, 16)
+        racc, _ = oracle.render(p.triangle_data, p.bvh_data, meta, 0, 3, 1, 8)
+    finally:
+        oracle.set_vertex_normals(False)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.set_vertex_normals(True)
+        gpu = s.frame(meta, 5, 16)
+        acc = s.render(meta, 0, 3, 1, 8, pt_amd.MODE_AUTO)
+        s.set_vertex_normals(False)
+        flat = s.frame(meta, 5, 16)
+    assert same_bits(gpu, ref), mismatch_report(gpu, ref)
+    assert same_bits(acc, racc), mismatch_report(acc, racc)
+    plain, _ = oracle.frame(p.triangle_data, p.bvh_data, meta, 5, 16)
+    assert same_bits(flat, plain)  # switching back restores the reference's normals
+    if scene != "CornellBox":  # scenes with vertex normals shade differently
+        assert not same_bits(gpu, plain)

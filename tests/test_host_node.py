@@ -163,7 +163,8 @@ try { pt.render(1, 2); } catch (e) { terr = e.constructor.name; }
 console.log(JSON.stringify({abi: pt.abiVersion(), keys: Object.keys(pt).sort(), err, terr}));''')
     assert r["abi"] == 1
     assert r["keys"] == sorted(["abiVersion", "deviceCount", "sceneCreate", "sceneInfo", "render", "renderSync", "frame",
-                                "tonemap", "profileEnable", "profileRead", "bvhBuild", "renderImage"])
+                                "tonemap", "profileEnable", "profileRead", "bvhBuild", "renderImage",
+                                "sceneSetVertexNormals"])
     assert r["terr"] == "TypeError"
     assert r["err"] and "pt_hip error" in r["err"]
 

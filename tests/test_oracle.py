@@ -175,3 +175,23 @@ def test_render_equals_sum_of_frames():
         ref = ref + np.where(r >= 0, r, np.float32(0)).astype(np.float32)
     assert np.array_equal(acc.view(np.uint32), ref.view(np.uint32))
     assert c["samples"] == 32 * 32 * 4
+
+
+def test_oracle_vertex_normal_mode_only_where_normals_exist():
+    """Vertex-normal mode (the reference's commented-out branch) leaves scenes without `vn` data
+    unchanged (i2 < vn_range never holds with vn_range = 0) and changes those with it."""
+    import conftest
+    out = {}
+    for name in ("CornellBox", "CornellBox-Glossy"):
+        import tempfile
+        d = tempfile.mkdtemp()
+        p = conftest.pack_with_node(os.path.join(conftest.SCENES, "scene_assets", name + ".xml"), d)
+        m = p.meta_for(16, 12)
+        a, _ = oracle.frame(p.triangle_data, p.bvh_data, m, 2, 8)
+        oracle.set_vertex_normals(True)
+        try:
+            b, _ = oracle.frame(p.triangle_data, p.bvh_data, m, 2, 8)
+        finally:
+            oracle.set_vertex_normals(False)
+        out[name] = np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert out == {"CornellBox": True, "CornellBox-Glossy": False}
