@@ -271,12 +271,25 @@ template <bool FAST_RCP, bool COUNT>
 __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris, const Ray& r, bool valid, float* slot,
                                           int nslots, int32_t* stack, int stride, Counters& c, float& t_out) {
     const int U = sc.n_tris - sc.mb_base;
-    // phase 1: every distinct entry against all 64 rays
+    // phase 1: every distinct entry against all 64 rays.  The test is tri_hit's arithmetic cut
+    // after u: when no lane passes the det and u tests (the early-out chain of
+    // ray-triangle-intersection.wgsl:15-24) the rest cannot make a hit and is skipped for the wave
     uint64_t hits = 0;
     int nh = 0;
     for (int u = 0; u < U; ++u) {
-        float t;
-        const bool h = tri_hit<FAST_RCP>(load_tri_scalar(gtris, sc.mb_base + u), r, t) & valid;
+        const TriRec tr = load_tri_scalar(gtris, sc.mb_base + u);
+        const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
+        const f3 rce2 = cross(r.d, e2);
+        const float det = dot(e1, rce2);
+        const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
+        const f3 sv = r.o - v0;
+        const float bu = inv_det * dot(sv, rce2);
+        const bool ok_u = valid & !(det > -1e-8f && det < 1e-8f) & !(bu < 0.0f) & !(bu > 1.0f);
+        if (!__any(ok_u)) continue;  // wave-uniform
+        const f3 sce1 = cross(sv, e1);
+        const float bv = inv_det * dot(r.d, sce1);
+        const float t = inv_det * dot(e2, sce1);
+        const bool h = ok_u & !(bv < 0.0f) & !(bu + bv > 1.0f) & (t > 1e-8f);
         if (h) {
             if (nh < nslots) slot[64 * nh] = t;
             ++nh;
