@@ -276,6 +276,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     // ray-triangle-intersection.wgsl:15-24) the rest cannot make a hit and is skipped for the wave
     uint64_t hits = 0;
     int nh = 0;
+    float tmin = 3.0e38f;  // smallest t of any entry this ray hits
     for (int u = 0; u < U; ++u) {
         const TriRec tr = load_tri_scalar(gtris, sc.mb_base + u);
         const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
@@ -294,11 +295,16 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
             if (nh < nslots) slot[64 * nh] = t;
             ++nh;
             hits |= 1ull << u;
+            tmin = fminf(tmin, t);
         }
     }
-    // phase 2: the mailboxed traversal, leaf entries resolved from phase 1
+    // phase 2: the mailboxed traversal, leaf entries resolved from phase 1.  Without counters a
+    // ray stops as soon as its closest t equals tmin: no later entry has a smaller t, and an
+    // equal one can only win inside the pair just resolved (strict-< across pairs) — so the
+    // result is final; a ray that hits nothing at all is final at once.  The counting build
+    // (COUNT) walks on, to count the reference's work.
     TravLean s;
-    trav_init(s, valid);
+    trav_init(s, valid && (COUNT || hits != 0));
     while (__any(!trav_finished(s))) {
         if (!trav_finished(s)) {
             mb_node_unit<COUNT>(sc, r, s, c);
@@ -319,7 +325,8 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
             }
             s.rem = 0;
             s.fl &= ~TF_LEAF;
-            lean_decide(s, stack, stride);
+            if (!COUNT && s.best_t == tmin) s.fl |= TF_DONE;
+            else lean_decide(s, stack, stride);
         }
     }
     t_out = s.best_t;
