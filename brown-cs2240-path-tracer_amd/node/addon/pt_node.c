@@ -150,6 +150,7 @@ typedef struct {
     float* accum;
     uint8_t* rgba; /* renderImage: the displayed image instead of the accumulator */
     pt_counters counters;
+    int want_counters; /* optional last argument (default true): counting builds of the kernels */
     int rc;
     char err[512];
 } render_job;
@@ -157,17 +158,18 @@ typedef struct {
 static void render_execute(napi_env env, void* data) {
     (void)env;
     render_job* j = (render_job*)data;
-    j->rc = j->rgba ? pt_render_image(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->rgba,
-                                      &j->counters)
-                    : pt_render(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->accum,
-                                &j->counters);
+    pt_counters* c = j->want_counters ? &j->counters : NULL;
+    j->rc = j->rgba ? pt_render_image(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->rgba, c)
+                    : pt_render(j->scene, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->accum, c);
     if (j->rc) snprintf(j->err, sizeof j->err, "pt_hip error %d: %s", j->rc, pt_last_error());
 }
 
 static void render_complete(napi_env env, napi_status status, void* data) {
     render_job* j = (render_job*)data;
     if (status == napi_ok && j->rc == 0) {
-        napi_resolve_deferred(env, j->deferred, counters_obj(env, &j->counters));
+        napi_value none;
+        napi_get_null(env, &none);
+        napi_resolve_deferred(env, j->deferred, j->want_counters ? counters_obj(env, &j->counters) : none);
     } else {
         napi_value msg, e;
         napi_create_string_utf8(env, j->rc ? j->err : "render cancelled", NAPI_AUTO_LENGTH, &msg);
@@ -179,10 +181,23 @@ static void render_complete(napi_env env, napi_status status, void* data) {
     free(j);
 }
 
-/* parse (scene, meta, frame0, nframes, stride, maxDepth, mode, accum) */
-static int parse_render_args(napi_env env, napi_callback_info info, render_job* j, napi_value argv[8]) {
-    size_t argc = 8;
+/* optional boolean argv[8]: work counters wanted (default true) */
+static int parse_want_counters(napi_env env, size_t argc, napi_value* argv, render_job* j) {
+    bool want = true;
+    if (argc > 8) {
+        napi_valuetype t;
+        if (napi_typeof(env, argv[8], &t) != napi_ok) return 0;
+        if (t != napi_undefined && napi_get_value_bool(env, argv[8], &want) != napi_ok) return 0;
+    }
+    j->want_counters = want ? 1 : 0;
+    return 1;
+}
+
+/* parse (scene, meta, frame0, nframes, stride, maxDepth, mode, accum[, counters]) */
+static int parse_render_args(napi_env env, napi_callback_info info, render_job* j, napi_value argv[9]) {
+    size_t argc = 9;
     if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 8) return 0;
+    if (!parse_want_counters(env, argc, argv, j)) return 0;
     float* meta;
     size_t ml, al;
     j->scene = get_scene(env, argv[0]);
@@ -195,16 +210,16 @@ static int parse_render_args(napi_env env, napi_callback_info info, render_job* 
     return 1;
 }
 
-/* render(scene, meta, frame0, nframes, stride, maxDepth, mode, accum) -> Promise<counters> */
+/* render(scene, meta, frame0, nframes, stride, maxDepth, mode, accum[, counters=true]) -> Promise<counters|null> */
 static napi_value js_render(napi_env env, napi_callback_info info) {
-    napi_value argv[8];
+    napi_value argv[9];
     render_job* j = (render_job*)calloc(1, sizeof(render_job));
     if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
     if (!parse_render_args(env, info, j, argv)) {
         free(j);
         napi_throw_type_error(env, NULL,
                               "render(scene, Float32Array meta[48], frame0, nframes, stride, maxDepth, mode, "
-                              "Float32Array accum[W*H*3])");
+                              "Float32Array accum[W*H*3], counters?)");
         return NULL;
     }
     napi_value promise, name;
@@ -218,16 +233,18 @@ static napi_value js_render(napi_env env, napi_callback_info info) {
     return promise;
 }
 
-/* renderImage(scene, meta, frame0, nframes, stride, maxDepth, mode, Uint8Array rgba[W*H*4]) -> Promise<counters>:
+/* renderImage(scene, meta, frame0, nframes, stride, maxDepth, mode, Uint8Array rgba[W*H*4][, counters=true])
+ * -> Promise<counters|null>:
  * programEntry's displayed image, tone-mapped on the device (pt_render_image) */
 static napi_value js_render_image(napi_env env, napi_callback_info info) {
-    size_t argc = 8;
-    napi_value argv[8];
+    size_t argc = 9;
+    napi_value argv[9];
     render_job* j = (render_job*)calloc(1, sizeof(render_job));
     if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
     float* meta;
     size_t ml = 0, il = 0;
-    int ok = napi_get_cb_info(env, info, &argc, argv, NULL, NULL) == napi_ok && argc >= 8;
+    int ok = napi_get_cb_info(env, info, &argc, argv, NULL, NULL) == napi_ok && argc >= 8 &&
+             parse_want_counters(env, argc, argv, j);
     if (ok) {
         j->scene = get_scene(env, argv[0]);
         ok = j->scene && get_f32(env, argv[1], &meta, &ml) && ml >= 48;
@@ -258,16 +275,19 @@ static napi_value js_render_image(napi_env env, napi_callback_info info) {
 
 /* renderSync(...same...) -> counters */
 static napi_value js_render_sync(napi_env env, napi_callback_info info) {
-    napi_value argv[8];
+    napi_value argv[9];
     render_job j;
     memset(&j, 0, sizeof j);
     if (!parse_render_args(env, info, &j, argv)) {
         napi_throw_type_error(env, NULL, "renderSync(scene, meta, frame0, nframes, stride, maxDepth, mode, accum)");
         return NULL;
     }
-    int rc = pt_render(j.scene, j.meta, j.frame0, j.nframes, j.stride, j.max_depth, j.mode, j.accum, &j.counters);
+    int rc = pt_render(j.scene, j.meta, j.frame0, j.nframes, j.stride, j.max_depth, j.mode, j.accum,
+                       j.want_counters ? &j.counters : NULL);
     if (rc) return throw_pt(env, rc);
-    return counters_obj(env, &j.counters);
+    napi_value none;
+    napi_get_null(env, &none);
+    return j.want_counters ? counters_obj(env, &j.counters) : none;
 }
 
 /* frame(scene, meta, t, maxDepth, out Float32Array[W*H*3]) */

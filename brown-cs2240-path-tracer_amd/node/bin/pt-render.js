@@ -5,6 +5,7 @@
 // (relative to --out-root, default cwd).  Usage: pt-render.js <scene.ini> [--web-root DIR]
 // [--out-root DIR] [--max-depth D] [--mode auto|megakernel|wavefront] [--device N] [--spp N]
 // [--vertex-normals 1] (smooth shading from the OBJ normals: the reference's commented-out branch)
+// [--counters 1] (work counters in the JSON line; runs the kernels' counting builds)
 const fs = require('fs');
 const path = require('path');
 const host = require('..');
@@ -22,7 +23,7 @@ async function main(argv) {
     const t1 = Date.now();
     const r = await host.programEntry(s.screenDimension, s.primitive_data, s.camera_data, s.scene_description, {
         device: parseInt(args.device || '0'), maxDepth: parseInt(args.max_depth || '16'), mode: args.mode || 'auto',
-        vertexNormals: args.vertex_normals === '1',
+        vertexNormals: args.vertex_normals === '1', counters: args.counters === '1',
     });
     const t2 = Date.now();
     const [W, H] = s.screenDimension;

@@ -33,7 +33,8 @@ function make_meta(screenDimension, camera_data, scene_description, time_elapsed
  * programEntry(screenDimension, primitive_data, camera_data, scene_description, options?)
  *   -> Promise<{accum: Float32Array(W*H*3), sample_runs, rgba: Uint8ClampedArray(W*H*4), counters, scene_info}>
  * options: {device=0, maxDepth=16, mode='auto', frame0=0, chunk=spp, onFrames(done, total), imageOnly=false,
- *           vertexNormals=false (the reference's commented-out smooth-normal branch; changes results)}
+ *           vertexNormals=false (the reference's commented-out smooth-normal branch; changes results),
+ *           counters=false (work counters: the kernels' counting builds, slower; counters is null without)}
  * imageOnly: render and tone-map on the device in one call and return only {rgba, counters, ...}
  * (no accumulator crosses PCIe; pt_render_image).
  * As in the reference only primitive_data[0] is rendered (program-raymarch.wgsl:31,33).
@@ -53,18 +54,19 @@ async function programEntry(screenDimension, primitive_data, camera_data, scene_
     if (mode === undefined) throw Error(`unknown mode ${o.mode}`);
     if (o.imageOnly) {
         const rgba = new Uint8ClampedArray(W * H * 4);
-        const c = await pt.renderImage(scene, meta, o.frame0, spp, 1, o.maxDepth, mode, new Uint8Array(rgba.buffer));
+        const c = await pt.renderImage(scene, meta, o.frame0, spp, 1, o.maxDepth, mode, new Uint8Array(rgba.buffer),
+                                       !!o.counters);
         return { accum: null, sample_runs: spp, rgba, counters: c, scene_info: pt.sceneInfo(scene) };
     }
     for (let done = 0; done < spp; done += chunk) {
         const n = Math.min(chunk, spp - done);
-        const c = await pt.render(scene, meta, o.frame0 + done, n, 1, o.maxDepth, mode, accum);
-        for (const k of Object.keys(counters)) counters[k] += c[k];
+        const c = await pt.render(scene, meta, o.frame0 + done, n, 1, o.maxDepth, mode, accum, !!o.counters);
+        if (c) for (const k of Object.keys(counters)) counters[k] += c[k];
         if (o.onFrames) o.onFrames(done + n, spp);
     }
     const rgba = new Uint8ClampedArray(W * H * 4);
     pt.tonemap(accum, spp, rgba);
-    return { accum, sample_runs: spp, rgba, counters, scene_info: pt.sceneInfo(scene) };
+    return { accum, sample_runs: spp, rgba, counters: o.counters ? counters : null, scene_info: pt.sceneInfo(scene) };
 }
 
 module.exports = { programEntry, make_meta, MODE };

@@ -55,9 +55,15 @@ def load_scene(src: str, width: int | None = None, height: int | None = None, sp
 
 
 def program_entry(packed: PackedScene, device: int = 0, max_depth: int = 16, mode: int = MODE_AUTO, frame0: int = 0,
-                  spp: int | None = None) -> dict:
-    """Render spp (default samplesPerPixel) frames; returns accum [H,W,3] f32, rgba [H,W,4] u8, counters."""
+                  spp: int | None = None, counters: bool = False, vertex_normals: bool = False) -> dict:
+    """Render spp (default samplesPerPixel) frames; returns accum [H,W,3] f32, rgba [H,W,4] u8 and the work
+    counters (None unless asked for: they run the kernels' counting builds)."""
     n = int(spp if spp is not None else packed.settings["samplesPerPixel"])
     with Scene(packed.triangle_data, packed.bvh_data, device=device) as s:
-        accum, counters = s.render(packed.meta, frame0, n, 1, max_depth, mode, counters=True)
-    return {"accum": accum, "sample_runs": n, "rgba": tonemap(accum, n), "counters": counters}
+        if vertex_normals:
+            s.set_vertex_normals(True)
+        if counters:
+            accum, cnt = s.render(packed.meta, frame0, n, 1, max_depth, mode, counters=True)
+        else:
+            accum, cnt = s.render(packed.meta, frame0, n, 1, max_depth, mode), None
+    return {"accum": accum, "sample_runs": n, "rgba": tonemap(accum, n), "counters": cnt}

@@ -24,13 +24,17 @@ const host = require(process.argv[1]);
     S.imageWidth = %d; S.imageHeight = %d; S.samplesPerPixel = %d;
     const dim = host.screen_dimension(S);
     const a = await host.programEntry(dim, s.primitive_data, s.camera_data, s.scene_description,
-                                      { maxDepth: 8, mode: 'megakernel', chunk: 4 });
+                                      { maxDepth: 8, mode: 'megakernel', chunk: 4, counters: true });
     const b = await host.programEntry(dim, s.primitive_data, s.camera_data, s.scene_description,
-                                      { maxDepth: 8, mode: 'wavefront', imageOnly: true });
+                                      { maxDepth: 8, mode: 'wavefront', imageOnly: true, counters: true });
+    const c = await host.programEntry(dim, s.primitive_data, s.camera_data, s.scene_description,
+                                      { maxDepth: 8, mode: 'wavefront' });
     const out = process.argv[4];
     fs.writeFileSync(out + '/accum.f32', Buffer.from(a.accum.buffer));
     fs.writeFileSync(out + '/rgba.u8', Buffer.from(a.rgba.buffer));
     fs.writeFileSync(out + '/rgba_image.u8', Buffer.from(b.rgba.buffer));
+    fs.writeFileSync(out + '/accum_fast.f32', Buffer.from(c.accum.buffer));
+    if (c.counters !== null) throw Error('counters without asking');
     fs.writeFileSync(out + '/counters.json', JSON.stringify([a.counters, b.counters]));
 })().catch((e) => { console.error(e.stack || String(e)); process.exit(1); });
 """ % (W, H, SPP)
@@ -43,12 +47,14 @@ def test_node_program_entry_matches_python_path():
         acc = np.fromfile(os.path.join(td, "accum.f32"), np.float32).reshape(H, W, 3)
         rgba = np.fromfile(os.path.join(td, "rgba.u8"), np.uint8).reshape(H, W, 4)
         rgba_img = np.fromfile(os.path.join(td, "rgba_image.u8"), np.uint8).reshape(H, W, 4)
+        acc_fast = np.fromfile(os.path.join(td, "accum_fast.f32"), np.float32).reshape(H, W, 3)
         c_node = json.load(open(os.path.join(td, "counters.json")))
         p = pack_with_node(INI, os.path.join(td, "packed"), "--web-root", SCENES, "--width", str(W), "--height", str(H),
                            "--spp", str(SPP))
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         ref, c = s.render(p.meta, 0, SPP, 1, 8, pt_amd.MODE_MEGAKERNEL, counters=True)
     assert acc.tobytes() == ref.tobytes()                       # chunked (4 + 2 frames) == one call
+    assert acc_fast.tobytes() == ref.tobytes()                  # uncounted wavefront build, same bits
     assert np.array_equal(rgba, pt_amd.tonemap(ref, SPP))
     assert np.array_equal(rgba_img, rgba)                        # device tone map, wavefront pipeline
     assert c_node[0] == c and c_node[1] == c
