@@ -448,10 +448,10 @@ void pt_scene_destroy(pt_scene* s) {
     if (s->stream) { hipStreamSynchronize(s->stream); hipStreamDestroy(s->stream); }
     if (s->d_accum) hipFree(s->d_accum);
     if (s->d_wf) hipFree(s->d_wf);
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kMaxParts; ++h) {
         if (s->ws.aux[h]) { hipStreamSynchronize(s->ws.aux[h]); hipStreamDestroy(s->ws.aux[h]); }
         if (s->ws.join[h]) hipEventDestroy(s->ws.join[h]);
-        if (s->ws.traced[h]) hipEventDestroy(s->ws.traced[h]);
+        if (h < 2 && s->ws.traced[h]) hipEventDestroy(s->ws.traced[h]);
     }
     if (s->ws.fork) hipEventDestroy(s->ws.fork);
     if (s->d_rgba) hipFree(s->d_rgba);
@@ -517,6 +517,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_FASTRCP")) lo.fast_rcp = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_PIPE")) lo.pipe = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_PARTS")) lo.parts = std::atoi(e);
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_PERSIST")) lo.persist = std::strcmp(e, "0") != 0 ? 1 : 0;
@@ -544,7 +545,8 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     size_t oq[6];
     for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * qn);
     const size_t o_p0 = take(16 * qn), o_p1 = take(16 * qn), o_p2 = take(8 * qn), o_hit = take(8 * qn),
-                 o_rad = take(12 * n), o_ctl = take(4 * 2 * WF_CTL_WORDS), o_rcnt = take(4 * 2 * 3 * kRegions);
+                 o_rad = take(12 * n), o_ctl = take(4 * kMaxParts * WF_CTL_WORDS),
+                 o_rcnt = take(4 * kMaxParts * 3 * kRegions);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
     char* b = static_cast<char*>(s->d_wf);
     auto f4 = [&](size_t o) { return reinterpret_cast<float4*>(b + o); };
@@ -557,17 +559,16 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     w.rad = reinterpret_cast<float*>(b + o_rad);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
     w.rcnt = reinterpret_cast<uint32_t*>(b + o_rcnt);
-    if (hipMemset(w.ctl, 0, 4 * 2 * WF_CTL_WORDS) != hipSuccess || hipMemset(w.rcnt, 0, 4 * 2 * 3 * kRegions) != hipSuccess)
+    if (hipMemset(w.ctl, 0, 4 * kMaxParts * WF_CTL_WORDS) != hipSuccess ||
+        hipMemset(w.rcnt, 0, 4 * kMaxParts * 3 * kRegions) != hipSuccess)
         return fail(PT_ERR_HIP, "hipMemset wavefront control words");
     if (!s->ws.aux[0]) {
-        if (hipStreamCreateWithFlags(&s->ws.aux[0], hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&s->ws.aux[1], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ws.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ws.join[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ws.join[1], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ws.traced[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ws.traced[1], hipEventDisableTiming) != hipSuccess)
-            return fail(PT_ERR_HIP, "creating the wavefront's streams");
+        bool ok = hipEventCreateWithFlags(&s->ws.fork, hipEventDisableTiming) == hipSuccess;
+        for (int h = 0; h < kMaxParts && ok; ++h)
+            ok = hipStreamCreateWithFlags(&s->ws.aux[h], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&s->ws.join[h], hipEventDisableTiming) == hipSuccess;
+        for (int h = 0; h < 2 && ok; ++h) ok = hipEventCreateWithFlags(&s->ws.traced[h], hipEventDisableTiming) == hipSuccess;
+        if (!ok) return fail(PT_ERR_HIP, "creating the wavefront's streams");
     }
     w.capacity = (uint32_t)n;
     w.qcap = (uint32_t)qn;
@@ -632,7 +633,7 @@ int pt_render_async(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t
 static int check_watchdog(pt_scene* s) {
     if (!s->d_wf) return PT_OK;
     uint32_t flag = 0, h = 0;
-    for (; h < 2; ++h) {  // one control block per half of a dual-stream batch
+    for (; h < kMaxParts; ++h) {  // one control block per part of a batch
         HIP_TRY(hipMemcpy(&flag, s->wf.ctl + h * WF_CTL_WORDS + WF_WATCHDOG, sizeof(flag), hipMemcpyDeviceToHost));
         if (flag) break;
     }

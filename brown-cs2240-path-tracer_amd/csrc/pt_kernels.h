@@ -62,6 +62,7 @@ struct LaunchOpts {
     int ifif = -1;         // lean step = node step for all lanes that want one, then leaf loop: -1 default
     int dual = -1;         // wavefront batch split in two halves on two streams: -1 default
     int stagger = -1;      // dual halves' traces alternate instead of overlapping: -1 default (off)
+    int parts = -1;        // parts of a wavefront batch on their own streams (1..kMaxParts): -1 default (2)
     int mailbox = -1;      // mailboxed lean traversal where SceneView::mailbox allows it: -1 default (on)
     int bf = -1;           // wavefront, mailbox scenes: brute-force + replay trace kernel: -1 default (on)
     int fuse = -1;         // bf trace fused with the shading (k_wf_step_bf): -1 default (on)
@@ -114,11 +115,13 @@ constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 // Dual-stream wavefront: two streams owned by the scene, created back to back so that HIP's
 // round-robin stream -> hardware-queue mapping puts them on different queues (a shared queue
 // serialises the halves), plus fork/join events with the caller's stream.  Null = one stream.
+constexpr int kMaxParts = 4;  // parts of a wavefront batch on their own streams (LaunchOpts::parts)
 struct WfStreams {
-    hipStream_t aux[2] = {nullptr, nullptr};
-    hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
-    hipEvent_t traced[2] = {nullptr, nullptr};  // "half h finished its trace i" (staggering)
+    hipStream_t aux[kMaxParts] = {};
+    hipEvent_t fork = nullptr, join[kMaxParts] = {};
+    hipEvent_t traced[2] = {nullptr, nullptr};  // "part h finished its trace i" (staggering, two parts)
     bool stagger = false;
+    int nparts = 2;
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

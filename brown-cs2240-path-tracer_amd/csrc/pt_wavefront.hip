@@ -649,19 +649,19 @@ static int trace_blocks(size_t lds_bytes) {
     return b;
 }
 
-// Paths [0, P) of half h of a batch: queue entries from h * capacity/2, radiance from
-// `rad_off` floats (so the two halves' radiance is contiguous in frame order), control words
-// from h * WF_CTL_WORDS.
-static WfBuffers wb_half(const WfBuffers& wb, int h, size_t rad_off) {
+// Paths [0, P) of part h of nparts of a batch: queue entries from h * qcap/nparts, radiance from
+// `rad_off` floats (so the parts' radiance is contiguous in frame order), control words from
+// h * WF_CTL_WORDS, region counts from h * 3 * kRegions.
+static WfBuffers wb_part(const WfBuffers& wb, int h, int nparts, size_t rad_off) {
     WfBuffers v = wb;
-    const size_t e = (size_t)h * (wb.qcap / 2);
+    const size_t e = (size_t)h * (wb.qcap / nparts);
     for (WfQueue* q : {&v.ext, &v.shd}) { q->ray += 2 * e; q->q2 += e; q->q3 += e; }
     v.sp0 += e; v.sp1 += e; v.sp2 += e; v.hitq += e;
     v.rad += rad_off;
     v.ctl += h * WF_CTL_WORDS;
     v.rcnt += h * 3 * kRegions;
-    v.capacity = wb.capacity / 2;
-    v.qcap = wb.qcap / 2;
+    v.capacity = wb.capacity / nparts;
+    v.qcap = wb.qcap / nparts;
     return v;
 }
 
@@ -670,11 +670,12 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                               uint32_t nframes, uint32_t stride, bool accum, float* out, Counters* cnt,
                               hipStream_t stream, const WfStreams& ws) {
     const uint32_t npix = fp.width * fp.height;
-    // two halves on two streams when a half holds at least a frame: the trace of one half
-    // (VALU/LDS-bound) runs beside the shading of the other (HBM-bound)
-    const bool dual = ws.aux[0] != nullptr && nframes >= 2 && wb.capacity / 2 >= npix;
-    const uint32_t F = dual ? 2 * std::min<uint32_t>((nframes + 1) / 2, (uint32_t)(wb.capacity / 2 / npix))
-                            : std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
+    // the batch in ws.nparts parts on as many streams when a part holds at least a frame: one
+    // part's kernel fills the others' launch tails and boundaries (and, with separate trace and
+    // shade kernels, a VALU-bound trace runs beside an HBM-bound shade)
+    int np = ws.aux[0] != nullptr ? ws.nparts : 1;
+    while (np > 1 && (nframes < (uint32_t)np || wb.capacity / np < npix)) np /= 2;
+    const uint32_t F = np * std::max<uint32_t>(1, std::min<uint32_t>((nframes + np - 1) / np, (uint32_t)(wb.capacity / np / npix)));
     const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc);
     int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
     if (const char* e = std::getenv("PT_WF_TRACE_BLOCKS")) tblocks = std::max(1, std::min(tblocks, std::atoi(e)));  // tests
@@ -698,37 +699,45 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     }
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
-        const uint32_t FA = dual && Fb >= 2 ? (Fb + 1) / 2 : Fb, FB = Fb - FA;
-        WfBuffers A = FB ? wb_half(wb, 0, 0) : wb;
-        WfBuffers B = wb_half(wb, 1, (size_t)FA * npix * 3);
+        // frames of the batch dealt to the parts in contiguous runs (part h: frames fb + f0[h] ..)
+        struct Part { WfBuffers w; uint32_t fbase, P; hipStream_t st; };
+        Part pv[kMaxParts];
+        int nh = 0;
+        uint32_t f0 = 0;
+        for (int h = 0; h < np && f0 < Fb; ++h) {
+            const uint32_t fh = std::min<uint32_t>((Fb + np - 1) / np, Fb - f0);
+            pv[nh].w = np > 1 ? wb_part(wb, h, np, (size_t)f0 * npix * 3) : wb;
+            pv[nh].fbase = fb + f0;
+            pv[nh].P = fh * npix;
+            pv[nh].st = np > 1 ? ws.aux[h] : stream;
+            f0 += fh;
+            ++nh;
+        }
         if constexpr (TRAV >= 400) {  // region-partitioned queues (k_wf_step_bf)
             const uint32_t R = std::min<uint32_t>(kRegions, (uint32_t)tblocks * (kTraceBlock / 64));
-            for (WfBuffers* v : {&A, &B}) {
-                v->nreg = R;
-                v->rstride = v->qcap / R / 64 * 64;  // R * rstride >= paths of the half (qcap slack)
+            for (int h = 0; h < nh; ++h) {
+                pv[h].w.nreg = R;
+                pv[h].w.rstride = pv[h].w.qcap / R / 64 * 64;  // R * rstride >= paths of the part (qcap slack)
             }
         }
-        struct Half { const WfBuffers* w; uint32_t fbase, P; hipStream_t st; };
-        const int nh = FB ? 2 : 1;
-        Half hv[2] = {{&A, fb, FA * npix, FB ? ws.aux[0] : stream}, {&B, fb + FA, FB * npix, ws.aux[1]}};
-        if (FB) {
+        if (np > 1) {
             HIP_RETURN_IF(hipEventRecord(ws.fork, stream));
-            for (int h = 0; h < 2; ++h) HIP_RETURN_IF(hipStreamWaitEvent(ws.aux[h], ws.fork, 0));
+            for (int h = 0; h < nh; ++h) HIP_RETURN_IF(hipStreamWaitEvent(pv[h].st, ws.fork, 0));
         }
         for (int h = 0; h < nh; ++h)
-            PT_LAUNCH(KID_WF_GENERATE, hv[h].st, (k_wf_generate<COUNT>),
-                      dim3((std::max(hv[h].P, hv[h].w->nreg) + 255) / 256), dim3(256), 0, hv[h].st,
-                      fp, *hv[h].w, frame0, stride, hv[h].fbase, hv[h].P, !accum, cnt);
-        // Optional staggering (PT_STAGGER=1; measured slower: 1026 vs 1231 Msamples/s): B's trace
-        // i waits for A's trace i and A's trace i+1 for B's trace i, so the persistent trace
-        // kernels never share the machine.  Default: the halves' kernels overlap freely.
+            PT_LAUNCH(KID_WF_GENERATE, pv[h].st, (k_wf_generate<COUNT>),
+                      dim3((std::max(pv[h].P, pv[h].w.nreg) + 255) / 256), dim3(256), 0, pv[h].st,
+                      fp, pv[h].w, frame0, stride, pv[h].fbase, pv[h].P, !accum, cnt);
+        // Optional staggering (PT_STAGGER=1, two parts; measured slower: 1026 vs 1231 Msamples/s):
+        // part 1's trace i waits for part 0's trace i and part 0's trace i+1 for part 1's trace i,
+        // so the persistent trace kernels never share the machine.  Default: parts overlap freely.
         const bool stagger = nh == 2 && ws.stagger;
         int in_q = 0;
         for (int it = 0; it < iters; ++it) {
             for (int h = 0; h < nh; ++h) {
-                const hipStream_t st = hv[h].st;
-                const WfBuffers& w = *hv[h].w;
-                const int sblocks = (int)((hv[h].P + kShadeBlock - 1) / kShadeBlock);
+                const hipStream_t st = pv[h].st;
+                const WfBuffers& w = pv[h].w;
+                const int sblocks = (int)((pv[h].P + kShadeBlock - 1) / kShadeBlock);
                 if (stagger && (h == 1 || it > 0)) HIP_RETURN_IF(hipStreamWaitEvent(st, ws.traced[1 - h], 0));
                 if constexpr (TRAV >= 400) {  // trace + shade in one launch
                     if ((it & 1) == 0)
@@ -754,9 +763,9 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
             }
             in_q ^= 1;
         }
-        if (FB) {
-            for (int h = 0; h < 2; ++h) {
-                HIP_RETURN_IF(hipEventRecord(ws.join[h], ws.aux[h]));
+        if (np > 1) {
+            for (int h = 0; h < nh; ++h) {
+                HIP_RETURN_IF(hipEventRecord(ws.join[h], pv[h].st));
                 HIP_RETURN_IF(hipStreamWaitEvent(stream, ws.join[h], 0));
             }
         }
@@ -769,7 +778,8 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
                             Counters* cnt, hipStream_t stream, const WfStreams& ws_in) {
-    WfStreams ws = lo.dual != 0 ? ws_in : WfStreams{};  // dual by default: +15 % measured (in-process A/B)
+    WfStreams ws = lo.dual != 0 ? ws_in : WfStreams{};  // parts on streams by default: +15 % measured (in-process A/B)
+    ws.nparts = std::max(1, std::min(kMaxParts, lo.parts > 0 ? lo.parts : 2));
     ws.stagger = lo.stagger > 0;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;

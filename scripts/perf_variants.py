@@ -72,6 +72,9 @@ VARIANTS = {
     "wf_bf": {"PT_KERNEL": "wavefront"},
     "wf_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
     "wf_bf_nofuse_2blk": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "512"},
+    "wf_parts4": {"PT_KERNEL": "wavefront", "PT_PARTS": "4"},
+    "wf_parts3": {"PT_KERNEL": "wavefront", "PT_PARTS": "3"},
+    "wf_parts4_16M": {"PT_KERNEL": "wavefront", "PT_PARTS": "4", "PT_WF_PATHS": "16777216"},
     "wf_bf_step": {"PT_KERNEL": "wavefront", "PT_PERSIST": "0"},
     "wf_persist_2blk": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "512"},
     "wf_persist_1024": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "1024"},
@@ -96,7 +99,7 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST", "PT_PARTS"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

@@ -51,6 +51,8 @@ KERNELS = {
     "wavefront_mb_lean16_rev": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
     "wavefront_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
     "wavefront_persist": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1"},
+    "wavefront_4parts": {"PT_KERNEL": "wavefront", "PT_PARTS": "4"},
+    "wavefront_3parts_nofuse": {"PT_KERNEL": "wavefront", "PT_PARTS": "3", "PT_FUSE": "0"},
     "wavefront_bf_step_3blocks": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "3"},
     "wavefront_persist_3blocks_div": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1", "PT_WF_TRACE_BLOCKS": "3",
                                       "PT_FASTRCP": "0"},
@@ -63,7 +65,7 @@ KERNELS = {
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
-            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST")
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS")
 
 
 @pytest.fixture(params=list(KERNELS))
