@@ -258,6 +258,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
 // with the same strict-< update, tie-break and pruning; tests of entries the traversal never
 // reaches have no effect.  A ray with more than `nslots` (<= kBfSlots) hits recomputes the rest on demand.
 constexpr int kBfSlots = 8;
+constexpr bool kBfPrefetch = true;  // bf_step_batch loads q2/q3 before the trace
 
 __device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
     // uniform index: constant address space, so the record comes through s_load (no VGPRs)
@@ -392,12 +393,15 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     const float4 a0 = in.ray[2 * e], a1 = in.ray[2 * e + 1];
     uint32_t p;
     Ray r = unpack_ray(valid ? a0 : make_float4(0, 0, 0, 1), valid ? a1 : make_float4(0, 0, 0, 0), p);
+    // the path state is loaded before the trace and arrives while it runs (kBfPrefetch)
+    float4 c2 = make_float4(0, 0, 0, 0), d3 = c2;
+    if (kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
     float t;
     const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t);
     bool more = false;
     PathState ps;
     if (valid) {
-        const float4 c2 = in.q2[e], d3 = in.q3[e];
+        if (!kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
         unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
         ps.L = mk(c2.x, c2.y, c2.z);
         ps.seed = __builtin_bit_cast(uint32_t, c2.w);
