@@ -520,6 +520,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_PARTS")) lo.parts = std::atoi(e);
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_REGEN_BF")) lo.regen_bf = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_PERSIST")) lo.persist = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_FUSE")) lo.fuse = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_BF")) lo.bf = std::strcmp(e, "0") != 0 ? 1 : 0;

@@ -66,6 +66,7 @@ struct LaunchOpts {
     int mailbox = -1;      // mailboxed lean traversal where SceneView::mailbox allows it: -1 default (on)
     int bf = -1;           // wavefront, mailbox scenes: brute-force + replay trace kernel: -1 default (on)
     int fuse = -1;         // bf trace fused with the shading (k_wf_step_bf): -1 default (on)
+    int regen_bf = -1;     // megakernel with brute-force + replay on mailbox scenes: -1 default (off)
     int persist = -1;      // fused bf as one workgroup-local launch per batch (k_wf_persist_bf): -1 default (off)
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
 };
@@ -132,6 +133,11 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
 hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
                              uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
                              hipStream_t stream);
+
+// megakernel with brute-force + replay closest hits (mailbox scenes; pt_wavefront.hip)
+hipError_t launch_regen_bf(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
+                           uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
+                           hipStream_t stream);
 
 // display transform of program-raymarch.ts:295-316 on device (pt_image.hip)
 hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t* rgba, hipStream_t stream);

@@ -231,6 +231,8 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& scene, const
 #undef LIT
         return hipGetLastError();
     }
+    if (lo.regen_bf > 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0)
+        return launch_regen_bf(lo, sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream);
     const bool lds = lo.lds && scene_fits_lds(sc);
     // lean4 + node bias 8 + fast reciprocal by default (measured at 1024^2 64 spp: 848 vs 611
     // for lean2 with majority turns and the division; scripts/perf_variants.py)

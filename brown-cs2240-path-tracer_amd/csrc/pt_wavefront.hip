@@ -532,6 +532,86 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_persist_bf(SceneView sc, Fra
     if (COUNT) flush_counters(c, cnt_out);
 }
 
+// Megakernel with brute force + replay (mailbox scenes, PT_KERNEL=mega with PT_REGEN_BF=1): the
+// layout of k_regen — lane = pixel of an 8x8 tile, the pixel's frames in order, a lane whose
+// path ended starts its next frame at once, clamp(L) accumulated in registers — with every
+// query of the wave resolved by bf_closest.  Extension and shadow rays of different lanes share
+// one phase 1 (a triangle test does not care which kind of ray it serves), so there are no
+// queues, no compaction and no kernel boundary between bounces.
+constexpr int kRegenBfBlock = 256;
+template <bool LDS, bool FAST_RCP, bool ACCUM, bool COUNT>
+__global__ __launch_bounds__(kRegenBfBlock) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void k_regen_bf(SceneView sc, FrameParams fp, uint32_t frame0, uint32_t nframes, uint32_t stride, float* __restrict__ out,
+                Counters* cnt_out, int nslots) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const BfLds l = bf_lds(smem, sc);
+    const Tri* gtris = sc.tris;
+    if (LDS) stage_scene_lds(sc, l.scene);
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7), y = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
+    Counters c = {};
+    const bool valid = x < fp.width && y < fp.height;
+    float* o = out + 3 * ((size_t)(valid ? y : 0) * fp.width + (valid ? x : 0));
+    f3 acc = (ACCUM && valid) ? mk(o[0], o[1], o[2]) : mk(0.0f, 0.0f, 0.0f);
+    enum { kIdle = 0, kExt = 1, kShadow = 2 };
+    int phase = kIdle;
+    uint32_t next = 0;  // next frame of this pixel to start
+    Ray ray;
+    ray.o = ray.d = ray.inv = mk(0.0f, 0.0f, 0.0f);
+    PathState ps;
+    while (true) {
+        if (phase == kIdle && valid && next < nframes) {
+            const uint32_t t = ACCUM ? (uint32_t)(float)(frame0 + next * stride) : frame0;
+            ++next;
+            ray = path_begin(fp, x, y, t, ps);
+            phase = kExt;
+            if (COUNT) { c.samples++; c.ext_queries++; }
+        }
+        const bool live = phase != kIdle;
+        if (!__any(live)) break;  // wave-uniform: every lane's frames are done
+        float t;
+        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, ray, live, l.slot, nslots, l.stack, blockDim.x, c, t);
+        if (live) {
+            bool more;
+            if (phase == kExt) {
+                more = path_after_ext(sc, rec, t, ray, ps);
+                if (more) { phase = kShadow; if (COUNT) c.shadow_queries++; }
+            } else {
+                more = path_after_shadow(sc, fp, rec, t, ray, ps);
+                if (more) { phase = kExt; if (COUNT) c.ext_queries++; }
+            }
+            if (!more) {
+                acc = ACCUM ? add_clamped(acc, ps.L) : ps.L;
+                phase = kIdle;
+            }
+        }
+    }
+    if (valid) { o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; }
+    if (COUNT) flush_counters(c, cnt_out);
+}
+
+hipError_t launch_regen_bf(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
+                           uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
+                           hipStream_t stream) {
+    const bool lds = lo.lds && scene_fits_lds(sc);
+    const bool fast = lo.fast_rcp != 0 && sc.fast_rcp;
+    int slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
+    if (const char* e = std::getenv("PT_BF_SLOTS")) slots = std::max(0, std::min(kBfSlots, std::atoi(e)));
+    dim3 grid((fp.width + 15) / 16, (fp.height + 15) / 16), block(kRegenBfBlock);
+    const size_t shm = (size_t)sc.max_stack * kRegenBfBlock * 4 + (kRegenBfBlock / 64) * (kBfSlots * 64 * 4) +
+                       (lds ? sc.span_bytes : 0);
+#define RB(L, F, A, C)                                                                                          \
+    PT_LAUNCH(KID_REGEN, stream, (k_regen_bf<L, F, A, C>), grid, block, shm, stream, sc, fp, frame0, nframes, stride, \
+              out, cnt, slots)
+#define RB_AC(L, F) \
+    if (accum) { if (count) RB(L, F, true, true); else RB(L, F, true, false); } else { if (count) RB(L, F, false, true); else RB(L, F, false, false); }
+    if (lds) { if (fast) { RB_AC(true, true) } else { RB_AC(true, false) } }
+    else { if (fast) { RB_AC(false, true) } else { RB_AC(false, false) } }
+#undef RB_AC
+#undef RB
+    return hipGetLastError();
+}
+
 // Shade blocks are 1024 threads so that compaction takes one atomicAdd per 1024 entries: all
 // atomics on the queue counter serialise at one memory channel, and one per wave (131k per
 // 8M-path batch) cost more than the shading itself.

@@ -72,6 +72,7 @@ VARIANTS = {
     "wf_bf": {"PT_KERNEL": "wavefront"},
     "wf_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
     "wf_bf_nofuse_2blk": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "512"},
+    "mega_bf": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1"},
     "wf_parts4": {"PT_KERNEL": "wavefront", "PT_PARTS": "4"},
     "wf_parts3": {"PT_KERNEL": "wavefront", "PT_PARTS": "3"},
     "wf_parts4_16M": {"PT_KERNEL": "wavefront", "PT_PARTS": "4", "PT_WF_PATHS": "16777216"},
@@ -99,7 +100,7 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST", "PT_PARTS"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

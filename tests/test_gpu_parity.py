@@ -51,6 +51,8 @@ KERNELS = {
     "wavefront_mb_lean16_rev": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
     "wavefront_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
     "wavefront_persist": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1"},
+    "mega_bf": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1"},
+    "mega_bf_global_1slot": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1", "PT_LDS": "0", "PT_BF_SLOTS": "1"},
     "wavefront_4parts": {"PT_KERNEL": "wavefront", "PT_PARTS": "4"},
     "wavefront_3parts_nofuse": {"PT_KERNEL": "wavefront", "PT_PARTS": "3", "PT_FUSE": "0"},
     "wavefront_bf_step_3blocks": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "3"},
@@ -65,7 +67,7 @@ KERNELS = {
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
-            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS")
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF")
 
 
 @pytest.fixture(params=list(KERNELS))
