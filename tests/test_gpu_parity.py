@@ -417,3 +417,17 @@ def test_vertex_normals_bitexact(packed, monkeypatch, scene, W, H, env):
     assert same_bits(flat, plain)  # switching back restores the reference's normals
     if scene != "CornellBox":  # scenes with vertex normals shade differently
         assert not same_bits(gpu, plain)
+
+
+def test_large_image_single_part_matches_megakernel(packed, monkeypatch):
+    """4096^2 (config 5's image): more pixels than the default batch capacity, so the batch holds
+    one frame and runs as a single part on one stream; the fused wavefront still equals the
+    megakernel bit for bit (both equal the oracle on the small cases)."""
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    p = packed["CornellBox"]
+    meta = p.meta_for(4096, 4096)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        a = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_WAVEFRONT)
+        m = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_MEGAKERNEL)
+    assert same_bits(a, m), mismatch_report(a, m)
