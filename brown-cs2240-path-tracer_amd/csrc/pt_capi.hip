@@ -57,6 +57,7 @@ struct HostLayout {
     std::vector<Light> lights;
     std::vector<uint64_t> lmask;  // mailbox scenes: uid set per leaf, indexed by first record
     std::vector<float4> tnorm;    // vertex-normal mode: 3 per record (SceneView::tnorm)
+    std::vector<float4> cull;     // mailbox scenes: 3 per distinct entry (SceneView::cull)
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -206,6 +207,32 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             for (size_t k = 0; k < first.size(); ++k)
                 for (int q = 0; q < 3; ++q) un[3 * (size_t)uid[first[k]] + q] = L.tnorm[3 * first[k] + q];
             L.tnorm.insert(L.tnorm.end(), un.begin(), un.end());
+            // entry cull records (bf_cull_mask): the box of the triangle the test sees (v0, v0 + e1,
+            // v0 + e2 of the stored record), tau = 1e-2 |e1| |e2| (the bundle's |det| floor, per
+            // unit |d|), the margin factor and w = 2 |v0| + |e1| + |e2| (margin = factor *
+            // (2 sqrt(3) max|o| + w), the bound on the test's rounding), e1 x e2
+            L.cull.resize(3 * (size_t)U);
+            for (int32_t u = 0; u < U; ++u) {
+                const Tri& t = L.tris[(size_t)(L.mb_base + u)];
+                const double v0[3] = {t.q0[0], t.q0[1], t.q0[2]}, e1[3] = {t.q0[3], t.q1[0], t.q1[1]},
+                             e2[3] = {t.q1[2], t.q1[3], t.e2z};
+                double lo[3], hi[3], n[3];
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = std::min({v0[a], v0[a] + e1[a], v0[a] + e2[a]});
+                    hi[a] = std::max({v0[a], v0[a] + e1[a], v0[a] + e2[a]});
+                }
+                n[0] = e1[1] * e2[2] - e1[2] * e2[1];
+                n[1] = e1[2] * e2[0] - e1[0] * e2[2];
+                n[2] = e1[0] * e2[1] - e1[1] * e2[0];
+                const double l1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+                const double l2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+                const double lv = std::sqrt(v0[0] * v0[0] + v0[1] * v0[1] + v0[2] * v0[2]);
+                auto dn = [](double x) { return std::nextafter((float)x, -INFINITY); };
+                auto upf = [](double x) { return std::nextafter((float)x, INFINITY); };
+                L.cull[3 * (size_t)u + 0] = make_float4(dn(lo[0]), dn(lo[1]), dn(lo[2]), upf(1e-2 * l1 * l2));
+                L.cull[3 * (size_t)u + 1] = make_float4(upf(hi[0]), upf(hi[1]), upf(hi[2]), 4e-3f);
+                L.cull[3 * (size_t)u + 2] = make_float4((float)n[0], (float)n[1], (float)n[2], upf(2.0 * lv + l1 + l2));
+            }
             L.lmask.assign(std::max<size_t>(1, entry.size()), 0);
             for (const auto& lr : leaf_ranges)
                 for (int32_t k = 0; k < lr.second; ++k) L.lmask[(size_t)lr.first] |= 1ull << uid[(size_t)(lr.first + k)];
@@ -397,7 +424,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_lmask = align_up(o_lights + L.lights.size() * sizeof(Light), 16);
     const size_t o_cnt = align_up(o_lmask + L.lmask.size() * sizeof(uint64_t), 256);
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
-    const size_t total = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
+    const size_t o_cull = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
+    const size_t total = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -408,7 +436,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_mats, L.mats.data(), L.mats.size() * sizeof(Material)) != hipSuccess ||
         up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess ||
         up(o_lmask, L.lmask.data(), L.lmask.size() * sizeof(uint64_t)) != hipSuccess ||
-        up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess) {
+        up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
+        up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -433,6 +462,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.mailbox = L.mailbox ? 1 : 0;
     s->view.tnorm = reinterpret_cast<const float4*>(base + o_tn);
     s->view.vnormals = 0;
+    s->view.cull = reinterpret_cast<const float4*>(base + o_cull);
+    s->view.cull_its = 0;  // per launch (launch_wavefront)
     s->view.mb_base = L.mb_base;
     s->view.span_bytes = (uint32_t)align_up(o_lmask + L.lmask.size() * sizeof(uint64_t) - o_nodes, 16);
     s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);
@@ -518,6 +549,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_PIPE")) lo.pipe = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_PARTS")) lo.parts = std::atoi(e);
+    if (const char* e = std::getenv("PT_CULL")) lo.cull = std::atoi(e);
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_REGEN_BF")) lo.regen_bf = std::strcmp(e, "0") != 0 ? 1 : 0;

@@ -99,6 +99,11 @@ struct SceneView {
     // i2 < vn_range (the branch applies); global memory, read for the winning record only
     const float4* tnorm;
     int32_t vnormals;
+    // entry cull of the brute-force kernels (mailbox scenes; pt_wavefront.hip bf_cull_mask): per
+    // distinct entry u, cull[3u..3u+2] = {box lo, tau}, {box hi, margin factor}, {e1 x e2, w}
+    // (pt_capi.hip build_layout); cull_its = the wavefront launches that use it (it < cull_its)
+    const float4* cull;
+    int32_t cull_its;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

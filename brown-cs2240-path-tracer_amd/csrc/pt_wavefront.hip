@@ -266,11 +266,81 @@ __device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
     return TriRec{make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]), f[8]};
 }
 
+// Entry cull (SceneView::cull; camera rays and their shadow rays, whose batches are coherent):
+// lane u tests distinct entry u against the bundle of the wave's valid rays — origins in the box
+// [olo, ohi], directions in [dlo, dhi], each axis on its own (a superset of the rays) — and the
+// entry is dropped from phase 1 when (a) no ray of the bundle reaches the entry's box grown by
+// the margin for t >= 0 and (b) every ray of the bundle has |det| >= tau (|e1 . (d x e2)| =
+// |d . (e1 x e2)| bounded by interval arithmetic).  (b) bounds the rounding of the test: a ray
+// whose |det| >= 1e-2 |e1| |e2| and whose test reports a hit passes within 2.4e-4 S + 6e-5
+// (|e1| + |e2|) of the triangle (S = 2 (|o| + |v0|)); the margin is 4e-3 (S + |e1| + |e2|),
+// ~16x that bound, so a ray that the test would report hitting always reaches the grown box, and
+// an entry dropped here has no hit for any ray of the wave: the result is unchanged.  Exact, like
+// the skipped det/u early-out (phase 1), for every entry the test would not hit.
+__device__ __forceinline__ float uniformf(float x) {  // to an SGPR (the value is wave-uniform)
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+}
+__device__ __forceinline__ float wave_minf(float x) {
+    for (int s = 1; s < 64; s <<= 1) x = fminf(x, __shfl_xor(x, s, 64));
+    return uniformf(x);
+}
+__device__ __forceinline__ float wave_maxf(float x) {
+    for (int s = 1; s < 64; s <<= 1) x = fmaxf(x, __shfl_xor(x, s, 64));
+    return uniformf(x);
+}
+__device__ __forceinline__ uint64_t bf_cull_mask(const SceneView& sc, const Ray& r, bool valid, int U) {
+    const uint64_t all = U >= 64 ? ~0ull : (1ull << U) - 1;
+    if (__ballot(valid) == 0) return 0;  // no ray: nothing can hit
+    const float inf = __builtin_inff();
+    const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    float olo[3], ohi[3], dlo[3], dhi[3];
+    for (int a = 0; a < 3; ++a) {
+        olo[a] = wave_minf(valid ? o[a] : inf);
+        ohi[a] = wave_maxf(valid ? o[a] : -inf);
+        dlo[a] = wave_minf(valid ? d[a] : inf);
+        dhi[a] = wave_maxf(valid ? d[a] : -inf);
+    }
+    const int u = (int)lane_id();
+    bool keep = true;
+    if (u < U) {
+        const float4 c0 = sc.cull[3 * u], c1 = sc.cull[3 * u + 1], c2 = sc.cull[3 * u + 2];
+        float omax = 0.0f, dm2 = 0.0f;
+        for (int a = 0; a < 3; ++a) {
+            omax = fmaxf(omax, fmaxf(fabsf(olo[a]), fabsf(ohi[a])));
+            const float dm = fmaxf(fabsf(dlo[a]), fabsf(dhi[a]));
+            dm2 += dm * dm;
+        }
+        const float m = c1.w * (3.4641017f * omax + c2.w);
+        const float blo[3] = {c0.x - m, c0.y - m, c0.z - m}, bhi[3] = {c1.x + m, c1.y + m, c1.z + m};
+        const float n[3] = {c2.x, c2.y, c2.z};
+        float tlo = 0.0f, thi = inf, dlo_n = 0.0f, dhi_n = 0.0f;
+        bool ok = true;
+        for (int a = 0; a < 3; ++a) {
+            // some o + t d inside [blo, bhi] on axis a needs olo + t dlo <= bhi and ohi + t dhi >= blo
+            const float A = bhi[a] - olo[a], B = blo[a] - ohi[a];
+            if (dlo[a] > 0.0f) thi = fminf(thi, A / dlo[a]);
+            else if (dlo[a] < 0.0f) tlo = fmaxf(tlo, A / dlo[a]);
+            else ok &= A >= 0.0f;
+            if (dhi[a] > 0.0f) tlo = fmaxf(tlo, B / dhi[a]);
+            else if (dhi[a] < 0.0f) thi = fminf(thi, B / dhi[a]);
+            else ok &= B <= 0.0f;
+            dlo_n += fminf(n[a] * dlo[a], n[a] * dhi[a]);
+            dhi_n += fmaxf(n[a] * dlo[a], n[a] * dhi[a]);
+        }
+        const bool reach = ok && tlo <= thi;
+        const float tau = c0.w * sqrtf(dm2);
+        const bool steady = dlo_n >= tau || dhi_n <= -tau;
+        keep = reach || !steady || !(m < inf);
+    }
+    return __ballot(keep) & all;
+}
+
 // Closest hit of the 64 rays of one batch (lane = ray; `valid` false lanes give no hit):
 // phase 1 + phase 2 above.  Returns the record (or -1) and its t in t_out.
 template <bool FAST_RCP, bool COUNT>
 __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris, const Ray& r, bool valid, float* slot,
-                                          int nslots, int32_t* stack, int stride, Counters& c, float& t_out) {
+                                          int nslots, int32_t* stack, int stride, Counters& c, float& t_out,
+                                          uint64_t todo = ~0ull) {  // todo: entries phase 1 tests (bf_cull_mask)
     const int U = sc.n_tris - sc.mb_base;
     // phase 1: every distinct entry against all 64 rays.  The test is tri_hit's arithmetic cut
     // after u: when no lane passes the det and u tests (the early-out chain of
@@ -278,7 +348,10 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     uint64_t hits = 0;
     int nh = 0;
     float tmin = 3.0e38f;  // smallest t of any entry this ray hits
-    for (int u = 0; u < U; ++u) {
+    todo &= U >= 64 ? ~0ull : (1ull << U) - 1;  // wave-uniform
+    while (todo) {
+        const int u = (int)__builtin_ctzll(todo);
+        todo &= todo - 1;
         const TriRec tr = load_tri_scalar(gtris, sc.mb_base + u);
         const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
         const f3 rce2 = cross(r.d, e2);
@@ -384,7 +457,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
 template <bool EXT, bool FAST_RCP, bool COUNT, class Append>
 __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gtris, const FrameParams& fp,
                                               const WfBuffers& wb, size_t rbase, uint32_t b, uint32_t count,
-                                              const BfLds& l, int nslots, Counters& c, Append append) {
+                                              const BfLds& l, int nslots, Counters& c, Append append,
+                                              bool cull = false) {  // cull: wave-uniform (bf_cull_mask)
     const WfQueue& in = EXT ? wb.ext : wb.shd;
     const WfQueue& out = EXT ? wb.shd : wb.ext;
     const uint32_t lane = lane_id();
@@ -393,11 +467,12 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     const float4 a0 = in.ray[2 * e], a1 = in.ray[2 * e + 1];
     uint32_t p;
     Ray r = unpack_ray(valid ? a0 : make_float4(0, 0, 0, 1), valid ? a1 : make_float4(0, 0, 0, 0), p);
+    const uint64_t todo = cull ? bf_cull_mask(sc, r, valid, sc.n_tris - sc.mb_base) : ~0ull;  // before the prefetch: fewer live VGPRs
     // the path state is loaded before the trace and arrives while it runs (kBfPrefetch)
     float4 c2 = make_float4(0, 0, 0, 0), d3 = c2;
     if (kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
     float t;
-    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t);
+    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t, todo);
     bool more = false;
     PathState ps;
     if (valid) {
@@ -443,7 +518,9 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
 // finished: stream order).
 // amdgpu_waves_per_eu(8): the path logic pushed the kernel to 75 VGPRs (6 waves/SIMD); capped
 // at 64 it keeps 8 waves/SIMD with no VGPR spills (a few SGPR spills to VGPR lanes): +7 %
-template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT>
+// CULL: the entry cull (bf_cull_mask) — its own instance, so the launches without it keep
+// their register allocation (the cull code costs VGPR spills at the 64-VGPR cap)
+template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT, bool CULL = false>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_wf_step_bf(SceneView sc, FrameParams fp, WfBuffers wb, int it,
                                                            Counters* cnt_out, int nslots) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -461,7 +538,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     Counters c = {};
     for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves
         bf_step_batch<EXT, FAST_RCP, COUNT>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
-                                            [&](uint32_t n) { return atomicAdd(out_count, n); });
+                                            [&](uint32_t n) { return atomicAdd(out_count, n); }, CULL);
     if (COUNT) flush_counters(c, cnt_out);
 }
 
@@ -824,11 +901,19 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                 const int sblocks = (int)((pv[h].P + kShadeBlock - 1) / kShadeBlock);
                 if (stagger && (h == 1 || it > 0)) HIP_RETURN_IF(hipStreamWaitEvent(st, ws.traced[1 - h], 0));
                 if constexpr (TRAV >= 400) {  // trace + shade in one launch
-                    if ((it & 1) == 0)
-                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<true, LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
+                    constexpr bool rcp = ((TRAV / 10) & 1) != 0;
+                    const bool cull = it < sc.cull_its;
+                    if ((it & 1) == 0 && cull)
+                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<true, LDS, rcp, COUNT, true>), dim3(tblocks),
+                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
+                    else if ((it & 1) == 0)
+                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<true, LDS, rcp, COUNT>), dim3(tblocks),
+                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
+                    else if (cull)
+                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<false, LDS, rcp, COUNT, true>), dim3(tblocks),
                                   dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
                     else
-                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
+                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<false, LDS, rcp, COUNT>), dim3(tblocks),
                                   dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
                     continue;
                 } else if constexpr (TRAV >= 300)
@@ -868,6 +953,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     if (sc.node_bias <= 0) sc.node_bias = 8;  // measured best with lean16 (1 = majority: -13 %)
+    sc.cull_its = lo.cull >= 0 ? lo.cull : 0;  // launches 0 (camera rays) and 1 (their shadow rays)
     const bool lds = lo.lds && scene_fits_lds(sc);
     // lean16 with the fast reciprocal by default (measured best on gfx950, scripts/perf_variants.py);
     // the wavefront always uses a flattened traversal; lean flavours take the fast reciprocal

@@ -63,11 +63,17 @@ KERNELS = {
     "wavefront_bf_2slots_div": {"PT_KERNEL": "wavefront", "PT_BF_SLOTS": "2", "PT_FASTRCP": "0"},
     "wavefront_mailbox_lean4_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_LDS": "0"},
     "wavefront_3blocks_flat1": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1", "PT_WF_TRACE_BLOCKS": "3"},
+    # entry cull of the fused kernel: on its default launches, on every launch (incoherent
+    # bundles: mostly nothing culled, all paths through the cull code), with the division
+    "wavefront_cull": {"PT_KERNEL": "wavefront", "PT_CULL": "2"},
+    "wavefront_cull_all": {"PT_KERNEL": "wavefront", "PT_CULL": "99"},
+    "wavefront_cull_all_div_global": {"PT_KERNEL": "wavefront", "PT_CULL": "99", "PT_FASTRCP": "0", "PT_LDS": "0"},
 }
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
-            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF")
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
+            "PT_CULL")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -431,3 +437,21 @@ def test_large_image_single_part_matches_megakernel(packed, monkeypatch):
         a = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_WAVEFRONT)
         m = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_MEGAKERNEL)
     assert same_bits(a, m), mismatch_report(a, m)
+
+
+@pytest.mark.parametrize("scene", ["CornellBox", "CornellBox-Mirror"])
+def test_entry_cull_full_size(packed, monkeypatch, scene):
+    """The entry cull (bf_cull_mask) at the bench's image size: every launch culled, the default
+    launches culled and none culled give the same bits (1024^2, 2 frames, the full depth)."""
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("PT_KERNEL", "wavefront")
+    p = packed[scene]
+    meta = p.meta_for(1024, 1024)
+    out = {}
+    for cull in ("0", "2", "99"):
+        monkeypatch.setenv("PT_CULL", cull)
+        with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+            out[cull] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
+    assert same_bits(out["2"], out["0"]), mismatch_report(out["2"], out["0"])
+    assert same_bits(out["99"], out["0"]), mismatch_report(out["99"], out["0"])
