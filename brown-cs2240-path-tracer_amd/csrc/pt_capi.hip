@@ -58,6 +58,7 @@ struct HostLayout {
     std::vector<uint64_t> lmask;  // mailbox scenes: uid set per leaf, indexed by first record
     std::vector<float4> tnorm;    // vertex-normal mode: 3 per record (SceneView::tnorm)
     std::vector<float4> cull;     // mailbox scenes: 3 per distinct entry (SceneView::cull)
+    std::vector<float> bfpair;    // mailbox scenes: 20 per pair of distinct entries (SceneView::bfpair)
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -232,6 +233,12 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                 L.cull[3 * (size_t)u + 0] = make_float4(dn(lo[0]), dn(lo[1]), dn(lo[2]), upf(1e-2 * l1 * l2));
                 L.cull[3 * (size_t)u + 1] = make_float4(upf(hi[0]), upf(hi[1]), upf(hi[2]), 4e-3f);
                 L.cull[3 * (size_t)u + 2] = make_float4((float)n[0], (float)n[1], (float)n[2], upf(2.0 * lv + l1 + l2));
+            }
+            L.bfpair.assign(20 * (size_t)((U + 1) / 2), 0.0f);
+            for (int32_t u = 0; u < U; ++u) {
+                const Tri& t = L.tris[(size_t)(L.mb_base + u)];
+                const float c[9] = {t.q0[0], t.q0[1], t.q0[2], t.q0[3], t.q1[0], t.q1[1], t.q1[2], t.q1[3], t.e2z};
+                for (int k = 0; k < 9; ++k) L.bfpair[20 * (size_t)(u / 2) + 2 * k + (u & 1)] = c[k];
             }
             L.lmask.assign(std::max<size_t>(1, entry.size()), 0);
             for (const auto& lr : leaf_ranges)
@@ -425,7 +432,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_cnt = align_up(o_lmask + L.lmask.size() * sizeof(uint64_t), 256);
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
     const size_t o_cull = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
-    const size_t total = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
+    const size_t o_pair = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
+    const size_t total = align_up(o_pair + std::max<size_t>(1, L.bfpair.size()) * sizeof(float), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -437,7 +445,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess ||
         up(o_lmask, L.lmask.data(), L.lmask.size() * sizeof(uint64_t)) != hipSuccess ||
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
-        up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess) {
+        up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess ||
+        up(o_pair, L.bfpair.data(), L.bfpair.size() * sizeof(float)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -464,6 +473,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.vnormals = 0;
     s->view.cull = reinterpret_cast<const float4*>(base + o_cull);
     s->view.cull_its = 0;  // per launch (launch_wavefront)
+    s->view.bfpair = reinterpret_cast<const float*>(base + o_pair);
     s->view.mb_base = L.mb_base;
     s->view.span_bytes = (uint32_t)align_up(o_lmask + L.lmask.size() * sizeof(uint64_t) - o_nodes, 16);
     s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);

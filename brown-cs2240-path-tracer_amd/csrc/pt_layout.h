@@ -104,6 +104,10 @@ struct SceneView {
     // (pt_capi.hip build_layout); cull_its = the wavefront launches that use it (it < cull_its)
     const float4* cull;
     int32_t cull_its;
+    // the distinct entries in pairs for phase 1's packed-f32 test (mailbox scenes): pair j =
+    // entries 2j, 2j+1 as 20 floats {v0.x of 2j, v0.x of 2j+1, v0.y, v0.y, ..., e2.z, e2.z, 0, 0};
+    // an odd count ends with an all-zero entry (det = 0: never a hit)
+    const float* bfpair;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

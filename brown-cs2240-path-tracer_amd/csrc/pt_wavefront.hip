@@ -258,6 +258,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
 // with the same strict-< update, tie-break and pruning; tests of entries the traversal never
 // reaches have no effect.  A ray with more than `nslots` (<= kBfSlots) hits recomputes the rest on demand.
 constexpr int kBfSlots = 8;
+// phase 1 in entry pairs with packed f32 (bf_pairs): bit-exact, measured no faster (fused kernel,
+// extension rays only: 2598 vs 2607 Msamples/s; both queues: 2446, VGPR spills in the shadow instance)
+constexpr bool kBfPacked = false;  // (k_regen_bf, itself opt-in, uses bf_pairs: tests cover it)
 constexpr bool kBfPrefetch = true;  // bf_step_batch loads q2/q3 before the trace
 
 __device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
@@ -335,9 +338,62 @@ __device__ __forceinline__ uint64_t bf_cull_mask(const SceneView& sc, const Ray&
     return __ballot(keep) & all;
 }
 
+// Phase 1 over pairs of entries (SceneView::bfpair) with packed f32 arithmetic: each
+// v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 does one operation of the test for both entries of
+// the pair — the same IEEE operations, in the same order, as tri_hit's (dot/cross of pt_math.h,
+// rcp_rn with kRcpSteps = 1), so the same bits at half the VALU issue.  Hits are recorded in
+// entry order, as the one-entry loop does.
+typedef float fv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fv2 fma2(fv2 a, fv2 b, fv2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ fv2 sp2(float x) { return fv2{x, x}; }
+static_assert(kRcpSteps == 1, "bf_pairs restates rcp_rn with one Newton step");
+template <bool FAST_RCP>
+__device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool valid, float* slot, int nslots,
+                                         uint64_t& hits, int& nh, float& tmin) {
+    const int NP = (sc.n_tris - sc.mb_base + 1) >> 1;
+    for (int j = 0; j < NP; ++j) {
+        const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(sc.bfpair + 20 * j);
+        const fv2 v0x = {f[0], f[1]}, v0y = {f[2], f[3]}, v0z = {f[4], f[5]};
+        const fv2 e1x = {f[6], f[7]}, e1y = {f[8], f[9]}, e1z = {f[10], f[11]};
+        const fv2 e2x = {f[12], f[13]}, e2y = {f[14], f[15]}, e2z = {f[16], f[17]};
+        const fv2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
+        const fv2 rx = fma2(dy, e2z, -(dz * e2y)), ry = fma2(dz, e2x, -(dx * e2z)), rz = fma2(dx, e2y, -(dy * e2x));
+        const fv2 det = fma2(e1z, rz, fma2(e1y, ry, e1x * rx));
+        fv2 inv;
+        if (FAST_RCP) {
+            const fv2 y = {__builtin_amdgcn_rcpf(det.x), __builtin_amdgcn_rcpf(det.y)};
+            inv = fma2(fma2(-det, y, sp2(1.0f)), y, y);
+        } else {
+            inv = fv2{1.0f / det.x, 1.0f / det.y};
+        }
+        const fv2 sx = sp2(r.o.x) - v0x, sy = sp2(r.o.y) - v0y, sz = sp2(r.o.z) - v0z;
+        const fv2 bu = inv * fma2(sz, rz, fma2(sy, ry, sx * rx));
+        const bool ok0 = valid & !(det.x > -1e-8f && det.x < 1e-8f) & !(bu.x < 0.0f) & !(bu.x > 1.0f);
+        const bool ok1 = valid & !(det.y > -1e-8f && det.y < 1e-8f) & !(bu.y < 0.0f) & !(bu.y > 1.0f);
+        if (!__any(ok0 | ok1)) continue;  // wave-uniform
+        const fv2 cx = fma2(sy, e1z, -(sz * e1y)), cy = fma2(sz, e1x, -(sx * e1z)), cz = fma2(sx, e1y, -(sy * e1x));
+        const fv2 bv = inv * fma2(dz, cz, fma2(dy, cy, dx * cx));
+        const fv2 t = inv * fma2(e2z, cz, fma2(e2y, cy, e2x * cx));
+        const bool h0 = ok0 & !(bv.x < 0.0f) & !(bu.x + bv.x > 1.0f) & (t.x > 1e-8f);
+        const bool h1 = ok1 & !(bv.y < 0.0f) & !(bu.y + bv.y > 1.0f) & (t.y > 1e-8f);
+        if (h0) {
+            if (nh < nslots) slot[64 * nh] = t.x;
+            ++nh;
+            hits |= 1ull << (2 * j);
+            tmin = fminf(tmin, t.x);
+        }
+        if (h1) {
+            if (nh < nslots) slot[64 * nh] = t.y;
+            ++nh;
+            hits |= 1ull << (2 * j + 1);
+            tmin = fminf(tmin, t.y);
+        }
+    }
+}
+
 // Closest hit of the 64 rays of one batch (lane = ray; `valid` false lanes give no hit):
 // phase 1 + phase 2 above.  Returns the record (or -1) and its t in t_out.
-template <bool FAST_RCP, bool COUNT>
+template <bool FAST_RCP, bool COUNT, bool PK = kBfPacked>
 __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris, const Ray& r, bool valid, float* slot,
                                           int nslots, int32_t* stack, int stride, Counters& c, float& t_out,
                                           uint64_t todo = ~0ull) {  // todo: entries phase 1 tests (bf_cull_mask)
@@ -348,6 +404,10 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     uint64_t hits = 0;
     int nh = 0;
     float tmin = 3.0e38f;  // smallest t of any entry this ray hits
+    if (PK && todo == ~0ull) {  // every entry: in pairs, packed f32 (bf_pairs)
+        bf_pairs<FAST_RCP>(sc, r, valid, slot, nslots, hits, nh, tmin);
+        todo = 0;
+    }
     todo &= U >= 64 ? ~0ull : (1ull << U) - 1;  // wave-uniform
     while (todo) {
         const int u = (int)__builtin_ctzll(todo);
@@ -647,7 +707,7 @@ void k_regen_bf(SceneView sc, FrameParams fp, uint32_t frame0, uint32_t nframes,
         const bool live = phase != kIdle;
         if (!__any(live)) break;  // wave-uniform: every lane's frames are done
         float t;
-        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, ray, live, l.slot, nslots, l.stack, blockDim.x, c, t);
+        const int rec = bf_closest<FAST_RCP, COUNT, true>(sc, gtris, ray, live, l.slot, nslots, l.stack, blockDim.x, c, t);
         if (live) {
             bool more;
             if (phase == kExt) {
