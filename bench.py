@@ -89,9 +89,15 @@ def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world
         return None
     key = f"{W}x{H}x{spp}x{depth}x{world}"
     cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix)}
-    # COUNT=false: the timed (uncounted) instances; the fused kernel has one per queue (extension /
-    # shadow), launched equally often, so their mean is the mean per launch
-    timed = [k for k in cands if k.endswith("false>")] or list(cands)
+    # the timed instances: COUNT=false (template argument 4 of k_wf_step_bf<EXT, LDS, rcp, COUNT,
+    # CULL>, the last one of the others) and no opt-in CULL; the fused kernel has one per queue
+    # (extension / shadow), launched equally often, so their mean is the mean per launch
+    def timed_instance(name):
+        args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")]
+        i = 3 if name.startswith("k_wf_step_bf<") else len(args) - 1
+        return 0 <= i < len(args) and all(a == "false" for a in args[i:])
+
+    timed = [k for k in cands if timed_instance(k)] or list(cands)
     if not timed:
         return None
     return sum(cands[k]["hbm_bytes_per_launch"] for k in timed) / len(timed)

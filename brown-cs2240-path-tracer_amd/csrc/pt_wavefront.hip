@@ -408,10 +408,8 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         bf_pairs<FAST_RCP>(sc, r, valid, slot, nslots, hits, nh, tmin);
         todo = 0;
     }
-    todo &= U >= 64 ? ~0ull : (1ull << U) - 1;  // wave-uniform
-    while (todo) {
-        const int u = (int)__builtin_ctzll(todo);
-        todo &= todo - 1;
+    // one entry of phase 1 against the wave's 64 rays
+    auto entry = [&](int u) __attribute__((always_inline)) {
         const TriRec tr = load_tri_scalar(gtris, sc.mb_base + u);
         const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
         const f3 rce2 = cross(r.d, e2);
@@ -420,7 +418,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         const f3 sv = r.o - v0;
         const float bu = inv_det * dot(sv, rce2);
         const bool ok_u = valid & !(det > -1e-8f && det < 1e-8f) & !(bu < 0.0f) & !(bu > 1.0f);
-        if (!__any(ok_u)) continue;  // wave-uniform
+        if (!__any(ok_u)) return;  // wave-uniform
         const f3 sce1 = cross(sv, e1);
         const float bv = inv_det * dot(r.d, sce1);
         const float t = inv_det * dot(e2, sce1);
@@ -430,6 +428,16 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
             ++nh;
             hits |= 1ull << u;
             tmin = fminf(tmin, t);
+        }
+    };
+    if (todo == ~0ull) {  // every entry (a constant in the instances without the cull)
+        for (int u = 0; u < U; ++u) entry(u);
+    } else {
+        todo &= U >= 64 ? ~0ull : (1ull << U) - 1;  // wave-uniform
+        while (todo) {
+            const int u = (int)__builtin_ctzll(todo);
+            todo &= todo - 1;
+            entry(u);
         }
     }
     // phase 2: the mailboxed traversal, leaf entries resolved from phase 1.  Without counters a
