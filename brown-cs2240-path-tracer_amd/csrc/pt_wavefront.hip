@@ -261,6 +261,23 @@ constexpr int kBfSlots = 8;
 // phase 1 in entry pairs with packed f32 (bf_pairs): bit-exact, measured no faster (fused kernel,
 // extension rays only: 2598 vs 2607 Msamples/s; both queues: 2446, VGPR spills in the shadow instance)
 constexpr bool kBfPacked = false;  // (k_regen_bf, itself opt-in, uses bf_pairs: tests cover it)
+// Diagnostic build only (EXTRA=-DPT_PHASE_TIMING=1, scripts/phase_timing.py): shader-clock
+// cycles per phase of bf_step_batch, summed per wave slot (8 phases x {extension, shadow}).
+#ifndef PT_PHASE_TIMING
+#define PT_PHASE_TIMING 0
+#endif
+constexpr int kPhaseSlots = 16;
+constexpr int kPhaseWaves = 16384;
+#if PT_PHASE_TIMING
+__device__ unsigned long long g_phase[kPhaseWaves * kPhaseSlots];
+#endif
+__device__ __forceinline__ uint64_t phase_clock() {
+#if PT_PHASE_TIMING
+    return __builtin_amdgcn_s_memtime();
+#else
+    return 0;
+#endif
+}
 constexpr bool kBfPrefetch = true;  // bf_step_batch loads q2/q3 before the trace
 
 __device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
@@ -396,7 +413,8 @@ __device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool
 template <bool FAST_RCP, bool COUNT, bool PK = kBfPacked>
 __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris, const Ray& r, bool valid, float* slot,
                                           int nslots, int32_t* stack, int stride, Counters& c, float& t_out,
-                                          uint64_t todo = ~0ull) {  // todo: entries phase 1 tests (bf_cull_mask)
+                                          uint64_t todo = ~0ull,  // todo: entries phase 1 tests (bf_cull_mask)
+                                          uint64_t* tmark = nullptr) {  // PT_PHASE_TIMING: end of phase 1
     const int U = sc.n_tris - sc.mb_base;
     // phase 1: every distinct entry against all 64 rays.  The test is tri_hit's arithmetic cut
     // after u: when no lane passes the det and u tests (the early-out chain of
@@ -440,6 +458,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
             entry(u);
         }
     }
+    if (PT_PHASE_TIMING && tmark) *tmark = phase_clock();
     // phase 2: the mailboxed traversal, leaf entries resolved from phase 1.  Without counters a
     // ray stops as soon as its closest t equals tmin: no later entry has a smaller t, and an
     // equal one can only win inside the pair just resolved (strict-< across pairs) — so the
@@ -530,6 +549,8 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     const WfQueue& in = EXT ? wb.ext : wb.shd;
     const WfQueue& out = EXT ? wb.shd : wb.ext;
     const uint32_t lane = lane_id();
+    uint64_t tm[6];
+    if (PT_PHASE_TIMING) tm[0] = phase_clock();
     const bool valid = b * 64 + lane < count;
     const size_t e = rbase + (valid ? b * 64 + lane : 0);
     const float4 a0 = in.ray[2 * e], a1 = in.ray[2 * e + 1];
@@ -540,7 +561,10 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     float4 c2 = make_float4(0, 0, 0, 0), d3 = c2;
     if (kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
     float t;
-    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t, todo);
+    if (PT_PHASE_TIMING) tm[1] = phase_clock();
+    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t, todo,
+                                                PT_PHASE_TIMING ? &tm[2] : nullptr);
+    if (PT_PHASE_TIMING) tm[3] = phase_clock();
     bool more = false;
     PathState ps;
     if (valid) {
@@ -563,6 +587,7 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
         }
     }
     const uint64_t keep = __ballot(more);
+    if (PT_PHASE_TIMING) tm[4] = phase_clock();
     if (keep) {  // wave-uniform
         uint32_t base = 0;
         if (lane == 0) base = append((uint32_t)__popcll(keep));
@@ -573,6 +598,16 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
             if (EXT) store_shading_point(wb, j, ps);
         }
     }
+#if PT_PHASE_TIMING
+    // slots: 0 load + cull, 1 phase 1, 2 phase 2, 3 shading, 4 append + stores, 5 batches
+    tm[5] = phase_clock();
+    const uint32_t wv = (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) % kPhaseWaves;
+    if (lane == 0) {
+        unsigned long long* g = g_phase + (size_t)wv * kPhaseSlots + (EXT ? 0 : 8);
+        for (int k = 0; k < 5; ++k) atomicAdd(g + k, (unsigned long long)(tm[k + 1] - tm[k]));
+        atomicAdd(g + 5, 1ull);
+    }
+#endif
 }
 
 // Trace + shade in one launch per iteration (mailbox scenes; PT_PERSIST=0): queues are cut
@@ -1062,3 +1097,15 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
 }
 
 }  // namespace pt
+
+#if PT_PHASE_TIMING
+// diagnostic build only: the phase cycle sums per wave slot (kPhaseWaves x kPhaseSlots u64),
+// zeroed after the read
+extern "C" __attribute__((visibility("default"))) int pt_debug_phase_read(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pt::g_phase), sizeof(unsigned long long) * pt::kPhaseWaves * pt::kPhaseSlots) != hipSuccess) return -1;
+    static unsigned long long zero[pt::kPhaseWaves * pt::kPhaseSlots];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(pt::g_phase), zero, sizeof(zero)) != hipSuccess) return -1;
+    return pt::kPhaseWaves * pt::kPhaseSlots;
+}
+#endif
