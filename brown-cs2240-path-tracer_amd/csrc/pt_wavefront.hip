@@ -278,6 +278,7 @@ __device__ __forceinline__ uint64_t phase_clock() {
     return 0;
 #endif
 }
+constexpr bool kBfScalarPrefetch = false;  // phase 1: next record's s_load in flight during a test (measured -2 %)
 constexpr bool kBfPrefetch = true;  // bf_step_batch loads q2/q3 before the trace
 
 __device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
@@ -427,8 +428,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         todo = 0;
     }
     // one entry of phase 1 against the wave's 64 rays
-    auto entry = [&](int u) __attribute__((always_inline)) {
-        const TriRec tr = load_tri_scalar(gtris, sc.mb_base + u);
+    auto entry = [&](int u, const TriRec& tr) __attribute__((always_inline)) {
         const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
         const f3 rce2 = cross(r.d, e2);
         const float det = dot(e1, rce2);
@@ -449,13 +449,27 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         }
     };
     if (todo == ~0ull) {  // every entry (a constant in the instances without the cull)
-        for (int u = 0; u < U; ++u) entry(u);
+        if (kBfScalarPrefetch) {
+            // the next record's s_load is issued after this record's wait, so it is in flight
+            // while this entry is tested (scalar loads return out of order: lgkmcnt(0) would
+            // otherwise wait for both)
+            TriRec nxt = load_tri_scalar(gtris, sc.mb_base);
+            for (int u = 0; u < U; ++u) {
+                const TriRec tr = nxt;
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): tr is here
+                __asm__ volatile("" ::: "memory");
+                nxt = load_tri_scalar(gtris, sc.mb_base + min(u + 1, U - 1));
+                entry(u, tr);
+            }
+        } else {
+            for (int u = 0; u < U; ++u) entry(u, load_tri_scalar(gtris, sc.mb_base + u));
+        }
     } else {
         todo &= U >= 64 ? ~0ull : (1ull << U) - 1;  // wave-uniform
         while (todo) {
             const int u = (int)__builtin_ctzll(todo);
             todo &= todo - 1;
-            entry(u);
+            entry(u, load_tri_scalar(gtris, sc.mb_base + u));
         }
     }
     if (PT_PHASE_TIMING && tmark) *tmark = phase_clock();
