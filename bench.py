@@ -90,8 +90,9 @@ def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world
     key = f"{W}x{H}x{spp}x{depth}x{world}"
     cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix)}
     # the timed instances: COUNT=false (template argument 4 of k_wf_step_bf<EXT, LDS, rcp, COUNT,
-    # CULL>, the last one of the others) and no opt-in CULL; the fused kernel has one per queue
-    # (extension / shadow), launched equally often, so their mean is the mean per launch
+    # CULL, GEN>, the last one of the others), no opt-in CULL, and not the one GEN launch per
+    # batch (it reads no queue); the fused kernel has one per queue (extension / shadow),
+    # launched equally often, so their mean is the mean per launch
     def timed_instance(name):
         args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")]
         i = 3 if name.startswith("k_wf_step_bf<") else len(args) - 1

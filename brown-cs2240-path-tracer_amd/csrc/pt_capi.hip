@@ -560,6 +560,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_PARTS")) lo.parts = std::atoi(e);
     if (const char* e = std::getenv("PT_CULL")) lo.cull = std::atoi(e);
+    if (const char* e = std::getenv("PT_FUSE_GEN")) lo.fuse_gen = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_REGEN_BF")) lo.regen_bf = std::strcmp(e, "0") != 0 ? 1 : 0;

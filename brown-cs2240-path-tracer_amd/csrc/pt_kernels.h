@@ -62,6 +62,7 @@ struct LaunchOpts {
     int ifif = -1;         // lean step = node step for all lanes that want one, then leaf loop: -1 default
     int dual = -1;         // wavefront batch split in two halves on two streams: -1 default
     int stagger = -1;      // dual halves' traces alternate instead of overlapping: -1 default (off)
+    int fuse_gen = 1;      // fused kernel: the first launch makes the camera paths (0: k_wf_generate)
     int cull = -1;         // entry cull for the first `cull` wavefront launches (bf kernels): -1 default
     int parts = -1;        // parts of a wavefront batch on their own streams (1..kMaxParts): -1 default (2)
     int mailbox = -1;      // mailboxed lean traversal where SceneView::mailbox allows it: -1 default (on)
@@ -123,6 +124,7 @@ struct WfStreams {
     hipEvent_t fork = nullptr, join[kMaxParts] = {};
     hipEvent_t traced[2] = {nullptr, nullptr};  // "part h finished its trace i" (staggering, two parts)
     bool stagger = false;
+    bool fuse_gen = true;  // LaunchOpts::fuse_gen
     int nparts = 2;
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,

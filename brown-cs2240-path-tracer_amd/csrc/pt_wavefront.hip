@@ -555,11 +555,20 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
 // k_wf_shade (pt_path.h, so the same bits) in the same wave — the hit never goes through HBM
 // and the ray record is read once — and the survivors appended to region rbase of the other
 // queue at offsets from `append(n)` (wave-uniform: called by lane 0, result broadcast).
-template <bool EXT, bool FAST_RCP, bool COUNT, class Append>
+// GEN (the first extension launch, k_wf_step_bf's GEN): the batch's camera paths are made here
+// instead of read from the queue — path p = (b * R + region) * 64 + lane, k_wf_generate's
+// layout — and packed into the very words store_entry would have written, so everything after
+// reads the same bits as from the queue (the queue write and read of the camera rays saved).
+struct GenArgs {
+    uint32_t frame0, stride, fbase, R, rg;
+    bool raw_salt;
+};
+template <bool EXT, bool FAST_RCP, bool COUNT, bool GEN = false, class Append>
 __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gtris, const FrameParams& fp,
                                               const WfBuffers& wb, size_t rbase, uint32_t b, uint32_t count,
                                               const BfLds& l, int nslots, Counters& c, Append append,
-                                              bool cull = false) {  // cull: wave-uniform (bf_cull_mask)
+                                              bool cull = false,  // cull: wave-uniform (bf_cull_mask)
+                                              const GenArgs& gen = GenArgs{}) {
     const WfQueue& in = EXT ? wb.ext : wb.shd;
     const WfQueue& out = EXT ? wb.shd : wb.ext;
     const uint32_t lane = lane_id();
@@ -567,13 +576,32 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     if (PT_PHASE_TIMING) tm[0] = phase_clock();
     const bool valid = b * 64 + lane < count;
     const size_t e = rbase + (valid ? b * 64 + lane : 0);
-    const float4 a0 = in.ray[2 * e], a1 = in.ray[2 * e + 1];
+    float4 a0 = make_float4(0, 0, 0, 1), a1 = make_float4(0, 0, 0, 0);
+    float4 c2 = make_float4(0, 0, 0, 0), d3 = c2;
+    if constexpr (GEN) {
+        if (valid) {
+            const uint32_t pg = (b * gen.R + gen.rg) * 64 + lane;
+            uint32_t x, y, f;
+            path_pixel(pg, fp.width * fp.height, fp.width, x, y, f);
+            const uint32_t tt = gen.raw_salt ? gen.frame0 : (uint32_t)(float)(gen.frame0 + (gen.fbase + f) * gen.stride);
+            PathState g;
+            const Ray gr = path_begin(fp, x, y, tt, g);
+            a0 = make_float4(gr.o.x, gr.o.y, gr.o.z, gr.d.x);
+            a1 = make_float4(gr.d.y, gr.d.z, __builtin_bit_cast(float, pg), __builtin_bit_cast(float, pack_dspec(g)));
+            c2 = make_float4(g.L.x, g.L.y, g.L.z, __builtin_bit_cast(float, g.seed));
+            d3 = make_float4(g.beta.x, g.beta.y, g.beta.z, 0.0f);
+            if (COUNT) { c.samples++; c.ext_queries++; }
+        }
+    } else {
+        a0 = in.ray[2 * e];
+        a1 = in.ray[2 * e + 1];
+        if (!valid) { a0 = make_float4(0, 0, 0, 1); a1 = make_float4(0, 0, 0, 0); }
+    }
     uint32_t p;
-    Ray r = unpack_ray(valid ? a0 : make_float4(0, 0, 0, 1), valid ? a1 : make_float4(0, 0, 0, 0), p);
+    Ray r = unpack_ray(a0, a1, p);
     const uint64_t todo = cull ? bf_cull_mask(sc, r, valid, sc.n_tris - sc.mb_base) : ~0ull;  // before the prefetch: fewer live VGPRs
     // the path state is loaded before the trace and arrives while it runs (kBfPrefetch)
-    float4 c2 = make_float4(0, 0, 0, 0), d3 = c2;
-    if (kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
+    if (!GEN && kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
     float t;
     if (PT_PHASE_TIMING) tm[1] = phase_clock();
     const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t, todo,
@@ -582,7 +610,7 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     bool more = false;
     PathState ps;
     if (valid) {
-        if (!kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
+        if (!GEN && !kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
         unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
         ps.L = mk(c2.x, c2.y, c2.z);
         ps.seed = __builtin_bit_cast(uint32_t, c2.w);
@@ -637,9 +665,12 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
 // at 64 it keeps 8 waves/SIMD with no VGPR spills (a few SGPR spills to VGPR lanes): +7 %
 // CULL: the entry cull (bf_cull_mask) — its own instance, so the launches without it keep
 // their register allocation (the cull code costs VGPR spills at the 64-VGPR cap)
-template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT, bool CULL = false>
+// GEN: the first launch makes the camera paths itself (bf_step_batch GEN; replaces
+// k_wf_generate): region counts in closed form, the output counts zeroed by the host.
+template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT, bool CULL = false, bool GEN = false>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_wf_step_bf(SceneView sc, FrameParams fp, WfBuffers wb, int it,
-                                                           Counters* cnt_out, int nslots) {
+                                                           Counters* cnt_out, int nslots, uint32_t frame0,
+                                                           uint32_t stride, uint32_t fbase, uint32_t P, bool raw_salt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const BfLds l = bf_lds(smem, sc);
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
@@ -647,15 +678,25 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     const uint32_t R = wb.nreg;  // <= nwaves (host)
     const uint32_t rg = w % R, g = w / R, G = (nwaves - rg + R - 1) / R;
     if (g == 0 && lane_id() == 0) wb.rcnt[((it + 2) % 3) * kRegions + rg] = 0;
-    const uint32_t count = wb.rcnt[(it % 3) * kRegions + rg];
+    uint32_t count;
+    if constexpr (GEN) {  // k_wf_generate's closed-form count of region rg
+        const uint32_t nbat = (P + 63) / 64;
+        const uint32_t n = rg < nbat ? (nbat - rg + R - 1) / R : 0u;
+        const uint32_t last = rg + (n - 1) * R;
+        count = n == 0 ? 0u : n * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
+        if (w == 0 && lane_id() == 0) { wb.ctl[WF_COUNT0] = P; wb.ctl[WF_COUNT1] = 0; }
+    } else {
+        count = wb.rcnt[(it % 3) * kRegions + rg];
+    }
     uint32_t* out_count = &wb.rcnt[((it + 1) % 3) * kRegions + rg];
     const Tri* gtris = sc.tris;  // global records for phase 1
     if (LDS) stage_scene_lds(sc, l.scene);
     const uint32_t nb = (count + 63) / 64;
+    const GenArgs ga{frame0, stride, fbase, R, rg, raw_salt};
     Counters c = {};
     for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves
-        bf_step_batch<EXT, FAST_RCP, COUNT>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
-                                            [&](uint32_t n) { return atomicAdd(out_count, n); }, CULL);
+        bf_step_batch<EXT, FAST_RCP, COUNT, GEN>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
+                                                 [&](uint32_t n) { return atomicAdd(out_count, n); }, CULL, ga);
     if (COUNT) flush_counters(c, cnt_out);
 }
 
@@ -1002,10 +1043,17 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
             HIP_RETURN_IF(hipEventRecord(ws.fork, stream));
             for (int h = 0; h < nh; ++h) HIP_RETURN_IF(hipStreamWaitEvent(pv[h].st, ws.fork, 0));
         }
-        for (int h = 0; h < nh; ++h)
-            PT_LAUNCH(KID_WF_GENERATE, pv[h].st, (k_wf_generate<COUNT>),
-                      dim3((std::max(pv[h].P, pv[h].w.nreg) + 255) / 256), dim3(256), 0, pv[h].st,
-                      fp, pv[h].w, frame0, stride, pv[h].fbase, pv[h].P, !accum, cnt);
+        // the fused kernel's first launch makes the camera paths itself (GEN); it appends into
+        // count slot 1, zeroed here (k_wf_generate zeroes it otherwise)
+        const bool fgen = TRAV >= 400 && TRAV < 500 && ws.fuse_gen;
+        for (int h = 0; h < nh; ++h) {
+            if (fgen)
+                HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rcnt + kRegions, 0, kRegions * sizeof(uint32_t), pv[h].st));
+            else
+                PT_LAUNCH(KID_WF_GENERATE, pv[h].st, (k_wf_generate<COUNT>),
+                          dim3((std::max(pv[h].P, pv[h].w.nreg) + 255) / 256), dim3(256), 0, pv[h].st,
+                          fp, pv[h].w, frame0, stride, pv[h].fbase, pv[h].P, !accum, cnt);
+        }
         // Optional staggering (PT_STAGGER=1, two parts; measured slower: 1026 vs 1231 Msamples/s):
         // part 1's trace i waits for part 0's trace i and part 0's trace i+1 for part 1's trace i,
         // so the persistent trace kernels never share the machine.  Default: parts overlap freely.
@@ -1020,18 +1068,17 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                 if constexpr (TRAV >= 400) {  // trace + shade in one launch
                     constexpr bool rcp = ((TRAV / 10) & 1) != 0;
                     const bool cull = it < sc.cull_its;
-                    if ((it & 1) == 0 && cull)
-                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<true, LDS, rcp, COUNT, true>), dim3(tblocks),
-                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
-                    else if ((it & 1) == 0)
-                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<true, LDS, rcp, COUNT>), dim3(tblocks),
-                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
-                    else if (cull)
-                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<false, LDS, rcp, COUNT, true>), dim3(tblocks),
-                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
-                    else
-                        PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<false, LDS, rcp, COUNT>), dim3(tblocks),
-                                  dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots);
+                    const bool g0 = fgen && it == 0;
+#define PT_STEP(E, C, G) PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<E, LDS, rcp, COUNT, C, G>), dim3(tblocks), \
+                                   dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots, frame0, stride,   \
+                                   pv[h].fbase, pv[h].P, !accum)
+                    if (g0 && cull) PT_STEP(true, true, true);
+                    else if (g0) PT_STEP(true, false, true);
+                    else if ((it & 1) == 0 && cull) PT_STEP(true, true, false);
+                    else if ((it & 1) == 0) PT_STEP(true, false, false);
+                    else if (cull) PT_STEP(false, true, false);
+                    else PT_STEP(false, false, false);
+#undef PT_STEP
                     continue;
                 } else if constexpr (TRAV >= 300)
                     PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
@@ -1067,6 +1114,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     WfStreams ws = lo.dual != 0 ? ws_in : WfStreams{};  // parts on streams by default: +15 % measured (in-process A/B)
     ws.nparts = std::max(1, std::min(kMaxParts, lo.parts > 0 ? lo.parts : 2));
     ws.stagger = lo.stagger > 0;
+    ws.fuse_gen = lo.fuse_gen != 0;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     if (sc.node_bias <= 0) sc.node_bias = 8;  // measured best with lean16 (1 = majority: -13 %)

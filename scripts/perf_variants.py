@@ -73,6 +73,8 @@ VARIANTS = {
     "wf_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
     "wf_bf_nofuse_2blk": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "512"},
     "mega_bf": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1"},
+    "wf_gen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1"},
+    "wf_nogen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "0"},
     "wf_cull0": {"PT_KERNEL": "wavefront", "PT_CULL": "0"},
     "wf_cull1": {"PT_KERNEL": "wavefront", "PT_CULL": "1"},
     "wf_cull2": {"PT_KERNEL": "wavefront", "PT_CULL": "2"},
@@ -105,7 +107,7 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF", "PT_CULL"):
+    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF", "PT_CULL", "PT_FUSE_GEN"):
         os.environ.pop(k, None)
     os.environ.update(VARIANTS[v])
 

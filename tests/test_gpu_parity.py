@@ -68,12 +68,16 @@ KERNELS = {
     "wavefront_cull": {"PT_KERNEL": "wavefront", "PT_CULL": "2"},
     "wavefront_cull_all": {"PT_KERNEL": "wavefront", "PT_CULL": "99"},
     "wavefront_cull_all_div_global": {"PT_KERNEL": "wavefront", "PT_CULL": "99", "PT_FASTRCP": "0", "PT_LDS": "0"},
+    # camera paths made in the first fused launch (GEN) or by k_wf_generate
+    "wavefront_gen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1"},
+    "wavefront_nogen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "0"},
+    "wavefront_gen_cull_1block": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1", "PT_CULL": "2", "PT_WF_TRACE_BLOCKS": "1"},
 }
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
-            "PT_CULL")
+            "PT_CULL", "PT_FUSE_GEN")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -271,6 +275,7 @@ def test_invalid_scene_rejected():
 def test_profile_records_every_launch(packed, monkeypatch):
     for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("PT_FUSE_GEN", "0")  # camera paths from k_wf_generate (the GEN form: below)
     p = packed["CornellBox"]
     meta = p.meta_for(64, 64)
     depth = 8
@@ -290,6 +295,13 @@ def test_profile_records_every_launch(packed, monkeypatch):
     assert set(wf) == {"k_wf_generate", "k_wf_step", "k_wf_accum"}
     assert wf["k_wf_step"]["launches"] == 2 * 2 * (depth + 1)
     assert wf["k_wf_generate"]["launches"] == 2 and wf["k_wf_accum"]["launches"] == 1
+    monkeypatch.setenv("PT_FUSE_GEN", "1")  # the first step launch makes the camera paths
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
+        wfg = s.profile_read()
+    assert set(wfg) == {"k_wf_step", "k_wf_accum"}
+    assert wfg["k_wf_step"]["launches"] == 2 * 2 * (depth + 1) and wfg["k_wf_accum"]["launches"] == 1
     monkeypatch.setenv("PT_PERSIST", "1")  # one workgroup-local trace + shade launch per batch
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
@@ -453,5 +465,11 @@ def test_entry_cull_full_size(packed, monkeypatch, scene):
         monkeypatch.setenv("PT_CULL", cull)
         with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
             out[cull] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
+    monkeypatch.setenv("PT_CULL", "0")
+    for gen in ("0", "1"):  # camera paths from k_wf_generate / made in the first fused launch
+        monkeypatch.setenv("PT_FUSE_GEN", gen)
+        with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+            out["gen" + gen] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
     assert same_bits(out["2"], out["0"]), mismatch_report(out["2"], out["0"])
     assert same_bits(out["99"], out["0"]), mismatch_report(out["99"], out["0"])
+    assert same_bits(out["gen0"], out["gen1"]), mismatch_report(out["gen0"], out["gen1"])
