@@ -56,3 +56,21 @@ def test_region_layout_fits_and_counts(capacity, dual, R):
         for r in {0, R - 1}:
             mine = np.sort(off[region == r])
             assert np.array_equal(mine, np.arange(counts[r]))
+
+
+@pytest.mark.parametrize("R", [1, 3, 64, K_REGIONS])
+@pytest.mark.parametrize("P", [1, 63, 64, 65, 4096 + 17, 2 * 1024 * 1024])
+def test_gen_path_index_inverts_the_layout(P, R):
+    """k_wf_step_bf's GEN launch makes path p = (b * R + rg) * 64 + lane for in-region batch b,
+    lane < count_rg - b * 64: exactly the path k_wf_generate would have stored at region rg,
+    offset b * 64 + lane — every path once, in the same slot."""
+    region, off, _ = layout(P, R, 1 << 40)
+    b, lane = off // 64, off % 64
+    p = np.arange(P, dtype=np.int64)
+    assert np.array_equal((b * R + region) * 64 + lane, p)
+    for rg in {0, R - 1, min(R - 1, 5)}:
+        n = closed_form_count(rg, P, R)
+        slots = np.arange(n)
+        made = (slots // 64 * R + rg) * 64 + slots % 64
+        assert np.array_equal(np.sort(p[region == rg]), made)
+        assert made.size == 0 or made.max() < P
