@@ -90,17 +90,22 @@ def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world
     key = f"{W}x{H}x{spp}x{depth}x{world}"
     cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix)}
     # the timed instances: COUNT=false (template argument 4 of k_wf_step_bf<EXT, LDS, rcp, COUNT,
-    # CULL, GEN>, the last one of the others), no opt-in CULL, and not the one GEN launch per
-    # batch (it reads no queue); the fused kernel has one per queue (extension / shadow),
-    # launched equally often, so their mean is the mean per launch
+    # CULL, GEN>, the last one of the others) and no opt-in CULL; averaged per launch, weighted
+    # by their dispatch counts when the summary has them (extension, shadow and the one camera
+    # GEN launch per batch), else the plain mean of the instances
     def timed_instance(name):
         args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")]
-        i = 3 if name.startswith("k_wf_step_bf<") else len(args) - 1
-        return 0 <= i < len(args) and all(a == "false" for a in args[i:])
+        if name.startswith("k_wf_step_bf<"):
+            return len(args) >= 4 and args[3] == "false" and (len(args) < 5 or args[4] == "false")
+        return bool(args) and args[-1] == "false"
 
     timed = [k for k in cands if timed_instance(k)] or list(cands)
     if not timed:
         return None
+    wts = [cands[k].get("dispatches") for k in timed]
+    if all(wts):
+        return sum(cands[k]["hbm_bytes_per_launch"] * w for k, w in zip(timed, wts)) / sum(wts)
+    timed = [k for k in timed if not k.endswith("true>")] or timed  # no counts: leave GEN out
     return sum(cands[k]["hbm_bytes_per_launch"] for k in timed) / len(timed)
 
 

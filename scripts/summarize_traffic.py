@@ -11,8 +11,8 @@ def load(tag, counter):
     per = collections.defaultdict(list)
     for (k, d), v in agg.items():
         per[k].append(sum(v))
-    return {k: sum(v) / len(v) for k, v in per.items()}
-fetch, write = load("fetch", "FETCH_SIZE"), load("write", "WRITE_SIZE")
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+(fetch, ndisp), (write, _) = load("fetch", "FETCH_SIZE"), load("write", "WRITE_SIZE")
 line = [json.loads(l) for l in open("gpurun_out/traffic/fetch.log") if l.startswith("{")][0]
 cfg = line["config"]
 W, H = 1024, 1024
@@ -26,6 +26,7 @@ for k in fetch:
     short = k.split("::")[-1]
     fb, wb = fetch[k] * 1024 * 2, write.get(k, 0.0) * 1024
     t[key][short] = {"fetch_kb_raw": fetch[k], "write_kb": write.get(k, 0.0), "hbm_bytes_per_launch": fb + wb,
+                     "dispatches": ndisp[k],
                      "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KB -> bytes, mean per dispatch"}
 json.dump(t, open(path, "w"), indent=1)
 print(json.dumps(t[key], indent=1))

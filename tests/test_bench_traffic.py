@@ -1,0 +1,41 @@
+"""bench.py's roofline traffic: the PMC bytes per launch of the timed k_wf_step instances
+(COUNT=false, no opt-in CULL), weighted by their dispatch counts (scripts/summarize_traffic.py)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def _write(tmp_path, entries):
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "traffic.json").write_text(json.dumps({"64x64x4x8x1": entries}))
+
+
+def test_weighted_by_dispatches(tmp_path, monkeypatch):
+    _write(tmp_path, {
+        "k_wf_step_bf<true, true, true, false, false, false>": {"hbm_bytes_per_launch": 200.0, "dispatches": 8},
+        "k_wf_step_bf<false, true, true, false, false, false>": {"hbm_bytes_per_launch": 100.0, "dispatches": 9},
+        "k_wf_step_bf<true, true, true, false, false, true>": {"hbm_bytes_per_launch": 1000.0, "dispatches": 1},
+        "k_wf_step_bf<true, true, true, true, false, false>": {"hbm_bytes_per_launch": 9e9, "dispatches": 8},   # COUNT
+        "k_wf_step_bf<true, true, true, false, true, false>": {"hbm_bytes_per_launch": 9e9, "dispatches": 1},   # CULL
+        "k_wf_accum": {"hbm_bytes_per_launch": 9e9, "dispatches": 1},
+    })
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    got = bench.load_traffic(("k_wf_step_bf<", "k_wf_persist_bf<"), 64, 64, 4, 8, 1)
+    assert got == (200.0 * 8 + 100.0 * 9 + 1000.0) / 18
+
+
+def test_unweighted_without_counts(tmp_path, monkeypatch):
+    _write(tmp_path, {
+        "k_wf_step_bf<true, true, true, false, false>": {"hbm_bytes_per_launch": 200.0},
+        "k_wf_step_bf<false, true, true, false, false>": {"hbm_bytes_per_launch": 100.0},
+        "k_wf_step_bf<true, true, true, true, false>": {"hbm_bytes_per_launch": 9e9},
+        "k_wf_trace<true, 17, false>": {"hbm_bytes_per_launch": 7.0},
+        "k_wf_trace<true, 17, true>": {"hbm_bytes_per_launch": 9e9},
+    })
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.load_traffic("k_wf_step_bf<", 64, 64, 4, 8, 1) == 150.0
+    assert bench.load_traffic("k_wf_trace", 64, 64, 4, 8, 1) == 7.0
+    assert bench.load_traffic("k_wf_trace", 32, 32, 4, 8, 1) is None
