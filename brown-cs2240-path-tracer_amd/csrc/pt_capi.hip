@@ -641,7 +641,11 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     if (lo.wavefront) {
         uint64_t target = kWfTargetPaths;
         if (const char* e = std::getenv("PT_WF_PATHS")) target = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));  // A/B
-        const uint64_t want = std::max<uint64_t>(npix, std::min<uint64_t>(npix * (accum ? nframes : 1), target));
+        // at least two frames per batch when the call has two (images above the target, e.g.
+        // 4096^2): the batch's parts run on their own streams and overlap (+29 % at 4096^2)
+        const uint64_t all = npix * (accum ? nframes : 1);
+        const uint64_t two = 2 * npix <= 0x7fffffffull ? 2 * npix : npix;
+        const uint64_t want = std::max<uint64_t>(std::min<uint64_t>(all, two), std::min<uint64_t>(all, target));
         int rc2 = ensure_wavefront(s, want);
         if (rc2 != PT_OK) return rc2;
         HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,

@@ -438,17 +438,22 @@ def test_vertex_normals_bitexact(packed, monkeypatch, scene, W, H, env):
 
 
 def test_large_image_single_part_matches_megakernel(packed, monkeypatch):
-    """4096^2 (config 5's image): more pixels than the default batch capacity, so the batch holds
-    one frame and runs as a single part on one stream; the fused wavefront still equals the
-    megakernel bit for bit (both equal the oracle on the small cases)."""
+    """4096^2 (config 5's image): more pixels than the default batch target, so the batch holds
+    two frames, one per part on its own stream (and with PT_PARTS=1 one part holding both); the
+    fused wavefront still equals the megakernel bit for bit (both equal the oracle on the small
+    cases)."""
     for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(4096, 4096)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         a = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_WAVEFRONT)
+        monkeypatch.setenv("PT_PARTS", "1")
+        a1 = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_WAVEFRONT)
+        monkeypatch.delenv("PT_PARTS")
         m = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_MEGAKERNEL)
     assert same_bits(a, m), mismatch_report(a, m)
+    assert same_bits(a1, m), mismatch_report(a1, m)
 
 
 @pytest.mark.parametrize("scene", ["CornellBox", "CornellBox-Mirror"])
