@@ -78,9 +78,10 @@ def cpu_baseline(tri, bvh, meta, depth, target_s=12.0):
                       f"{threads} OpenMP threads, {c['samples']} samples in {dt:.2f} s"}
 
 
-def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world: int):
-    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC passes
-    (scripts/collect_traffic.sh -> profiles/traffic.json), when they match this configuration."""
+def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int, field: str = "hbm_bytes_per_launch"):
+    """Per-launch PMC figure of the render kernel (HBM bytes, or `valu_issue`) from the committed
+    rocprofv3 passes (scripts/collect_traffic.sh -> profiles/traffic.json), when they match this
+    configuration: (value, source) or None."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
@@ -88,7 +89,7 @@ def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world
     except (OSError, ValueError):
         return None
     key = f"{W}x{H}x{spp}x{depth}x{world}"
-    cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix)}
+    cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix) and field in v}
     # the timed instances: COUNT=false (template argument 4 of k_wf_step_bf<EXT, LDS, rcp, COUNT,
     # CULL, GEN>, the last one of the others) and no opt-in CULL; averaged per launch, weighted
     # by their dispatch counts when the summary has them (extension, shadow and the one camera
@@ -102,11 +103,17 @@ def load_traffic(kernel_prefix: str, W: int, H: int, spp: int, depth: int, world
     timed = [k for k in cands if timed_instance(k)] or list(cands)
     if not timed:
         return None
+    src = "profiles/traffic.json[" + key + "]: " + t[key].get("_source", "rocprofv3 PMC passes (scripts/collect_traffic.sh)")
     wts = [cands[k].get("dispatches") for k in timed]
     if all(wts):
-        return sum(cands[k]["hbm_bytes_per_launch"] * w for k, w in zip(timed, wts)) / sum(wts)
+        return sum(cands[k][field] * w for k, w in zip(timed, wts)) / sum(wts), src
     timed = [k for k in timed if not k.endswith("true>")] or timed  # no counts: leave GEN out
-    return sum(cands[k]["hbm_bytes_per_launch"] for k in timed) / len(timed)
+    return sum(cands[k][field] for k in timed) / len(timed), src
+
+
+def metric_name(scene: str, W: int, H: int, depth: int) -> str:
+    """BASELINE.json's metric, for the workload actually run (its headline is CornellBox 1024^2 depth 8)."""
+    return f"Msamples/s (paths/s) {scene} {W}x{H} depth {depth}"
 
 
 def main():
@@ -204,6 +211,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    scene.check()  # a device-side failure of any timed render (pt_scene_check) fails the bench
     total_samples = W * H * args.spp
     ms_per_step = elapsed / args.steps * 1e3
     value = total_samples / (elapsed / args.steps) / 1e6
@@ -213,22 +221,28 @@ def main():
         kernel = max(prof, key=lambda k: prof[k]["total_ms"])
         launches_per_render = prof[kernel]["launches"] / args.steps
         k_ms = prof[kernel]["avg_ms"]
+        busy_ms = prof[kernel]["busy_ms"] / args.steps  # union of the launches' intervals, per step
         if kernel == "k_wf_trace":
             bytes_per_launch = 48.0 * (q_ext + q_sh) / launches_per_render
         elif kernel == "k_wf_step":  # fused trace + shade: the path model minus camera rays and accumulation
             bytes_per_launch = (48.0 * (q_ext + q_sh) + 96.0 * q_ext) / launches_per_render
         else:  # the megakernel: the whole path model in one launch
             bytes_per_launch = b_alg / launches_per_render
-        achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
+        # achieved = the algorithmic bytes of all of a step's launches over the time the kernel
+        # is busy in that step (launches of the batch's parts overlap on their streams, so the
+        # per-launch event time over-counts: it is reported, not used)
+        achieved = bytes_per_launch * launches_per_render / (busy_ms * 1e-3) / 1e9
     else:  # --no-kernel-timing (diagnostic)
-        kernel, launches_per_render, k_ms, bytes_per_launch, achieved = "n/a", 0, 0.0, 0.0, 0.0
+        kernel, launches_per_render, k_ms, busy_ms, bytes_per_launch, achieved = "n/a", 0, 0.0, 0.0, 0.0, 0.0
     pipeline = b_alg / (r_ms * 1e-3) / 1e9
 
     if rank == 0:
         prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<", "k_wf_persist_bf<")}
-        traffic = load_traffic(prefixes.get(kernel, (kernel + "<",)), W, H, args.spp, args.depth, world)
+        pre = prefixes.get(kernel, (kernel + "<",))
+        traffic = load_traffic(pre, W, H, args.spp, args.depth, world)
+        valu = load_traffic(pre, W, H, args.spp, args.depth, world, field="valu_issue")
         out = {
-            "metric": "Msamples/s (paths/s) CornellBox 1024^2 depth 8",
+            "metric": metric_name(args.scene, W, H, args.depth),
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -239,18 +253,30 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (reference CornellBox.xml scene packed by the Node host; RNG salts t_k = k)",
+            "data": f"synthetic (reference {args.scene}.xml scene packed by the Node host; RNG salts t_k = k)",
             "config": {"workload": f"{args.scene}.xml {W}x{H} {args.spp}spp depth {args.depth}, rr 0.9, "
                                    f"frames sharded k mod {world}" + (", RCCL sum-reduce of the f32 accumulator"
                                                                         if world > 1 else ""),
                        "mode": args.mode, "samples_per_step": total_samples},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic[0] * launches_per_render / (busy_ms * 1e-3) / 1e9 if traffic and busy_ms else None,
+                         "traffic_unit": "GB/s (PMC HBM bytes per launch x launches / busy time)",
+                         "traffic_bytes_per_launch": round(traffic[0]) if traffic else None,
+                         "traffic_source": traffic[1] if traffic else None,
                          "kernel": kernel, "kernel_avg_ms": round(k_ms, 4),
+                         "kernel_busy_ms_per_step": round(busy_ms, 3),
+                         "achieved_def": "algorithmic bytes per launch (SURVEY.md 8d model from the GPU's work counters) x "
+                                         "launches per step / the kernel's busy time per step (union of its launches' "
+                                         "HIP-event intervals on every part stream)",
                          "launches_per_step": launches_per_render, "bytes_per_launch": round(bytes_per_launch),
                          "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3),
                          "pipeline": {"bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
                                       "achieved": round(pipeline, 2), "frac": round(pipeline / HBM_PEAK_GBS, 4)},
+                         "valu_issue": ({"bound": "valu_issue", "frac": round(valu[0], 4),
+                                         "def": "4 x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE): SIMD issue cycles "
+                                                "of VALU over all SIMD cycles, kernel alone (PMC pass)",
+                                         "source": valu[1]} if valu else None),
                          "kernels_ms_warmup_step": {k: round(v["total_ms"] / max(args.warmup, 1), 3)
                                                     for k, v in prof_warm.items()},
                          "render_ms_steps": [round(x, 2) for x in render_ms]},

@@ -4,7 +4,10 @@
 // host as node/lib/bvh.js + packer.js: pack_bvh), in IEEE double exactly as the JS numbers
 // are, so the packed buffer is byte-identical and the traversal (whose order and exit-distance
 // pruning depend on the topology) returns the same hits:
-//   * node split axis = longest extent of the node box (ties x > y > z);
+//   * node split axis = longest of the node's strides (ties x > y > z) — js-geometry's Bounds fixes
+//     its strides when constructed and bvh.ts builds a child box from its PARENT's min/max before
+//     moving the split face, so a node's strides are its parent's extent (the root's its own);
+//     the reference's own renders decide this semantics;
 //   * 18 candidate split fractions s = 0.05, 0.05+0.05, ... accumulated in double while
 //     s <= 0.95 (the last is 0.9000000000000002); cost |nL - avg| + |nR - avg| with
 //     inclusive box overlap counts, first minimum wins;
@@ -32,6 +35,7 @@ struct BNode {
     bool leaf = false;
     int axis = -1;
     Box box{};
+    double stride[3] = {0, 0, 0};  // js-geometry Bounds.stride_* as constructed: the parent's extent
     std::vector<int32_t> objs;  // indices into the triangle list
     std::unique_ptr<BNode> l, r;
 };
@@ -57,7 +61,7 @@ struct Builder {
     void recurse(BNode& n, int depth) {
         if (depth >= kMaxDepth) { n.leaf = true; return; }
         const Box& nb = n.box;
-        const double sx = nb.mx[0] - nb.mn[0], sy = nb.mx[1] - nb.mn[1], sz = nb.mx[2] - nb.mn[2];
+        const double sx = n.stride[0], sy = n.stride[1], sz = n.stride[2];
         int axis;
         if (sx >= sy && sx >= sz) axis = 0;
         else if (sy >= sx && sy >= sz) axis = 1;
@@ -83,6 +87,7 @@ struct Builder {
         n.r = std::make_unique<BNode>();
         n.l->box = split_box(nb, axis, c, true);
         n.r->box = split_box(nb, axis, c, false);
+        for (int k = 0; k < 3; ++k) n.l->stride[k] = n.r->stride[k] = nb.mx[k] - nb.mn[k];
         for (int32_t o : n.objs) {
             if (overlap(tb[o], n.l->box)) n.l->objs.push_back(o);
             if (overlap(tb[o], n.r->box)) n.r->objs.push_back(o);
@@ -150,6 +155,7 @@ extern "C" int pt_bvh_build(const double* vertices, size_t vertex_count, const i
     BNode top;
     top.axis = 0;
     top.box = root;
+    for (int k = 0; k < 3; ++k) top.stride[k] = root.mx[k] - root.mn[k];
     top.objs.resize(tri_count);
     for (size_t t = 0; t < tri_count; ++t) top.objs[t] = (int32_t)t;
     Builder{tb}.recurse(top, 1);

@@ -311,13 +311,14 @@ struct pt_scene {
     uint8_t* d_rgba = nullptr;  // pt_render_image scratch
     size_t rgba_cap = 0;
     WfStreams ws;  // dual-stream wavefront: aux stream + fork/join events (created with d_wf)
+    // pinned mirror of the wavefront control words, copied after every wavefront render on its
+    // stream: a watchdog flag set by an asynchronous render surfaces once that copy has landed
+    // (next call, pt_scene_check) without a synchronisation of its own
+    uint32_t* h_ctl = nullptr;
 };
 
-// The dual-stream wavefront needs its two streams on hardware queues of their own; with HIP's
-// default of 4 queues per process they share one with the caller's streams and the halves
-// serialise (bench: 962 vs 1238 Msamples/s with 8).  Ask for 8 when the library is loaded before
-// the HIP runtime starts (a value the process already set wins; after HIP is up this is inert).
-__attribute__((constructor)) static void pt_hw_queues() { setenv("GPU_MAX_HW_QUEUES", "8", 0); }
+// Set once any call of this library has touched the HIP runtime (pt_set_hw_queues is then too late).
+static bool g_hip_touched = false;
 
 namespace pt {
 thread_local KernelProfiler* t_prof = nullptr;
@@ -378,16 +379,36 @@ int pt_profile_read(pt_scene* s, pt_kernel_time* out, int max_entries, int* n_ou
     if (!s || !n_out || (max_entries > 0 && !out)) return fail(PT_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(s->device));
     pt_kernel_time acc[KID_COUNT] = {};
+    // launch intervals relative to the first record's start event (events of one device compare
+    // across streams): their union per kernel is its busy time
+    std::vector<std::pair<double, double>> iv[KID_COUNT];
     for (const auto& r : s->prof.recs) {
         if (!r.a || !r.b) return fail(PT_ERR_HIP, "profiling event could not be created");
         HIP_TRY(hipEventSynchronize(r.b));
-        float ms = 0.0f;
+        float ms = 0.0f, t0 = 0.0f;
         HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+        HIP_TRY(hipEventElapsedTime(&t0, s->prof.recs.front().a, r.a));
         pt_kernel_time& k = acc[r.kid];
         k.min_ms = k.launches ? std::min(k.min_ms, (double)ms) : (double)ms;
         k.max_ms = k.launches ? std::max(k.max_ms, (double)ms) : (double)ms;
         k.total_ms += ms;
         k.launches++;
+        iv[r.kid].emplace_back((double)t0, (double)t0 + (double)ms);
+    }
+    for (int k = 0; k < KID_COUNT; ++k) {
+        std::sort(iv[k].begin(), iv[k].end());
+        double busy = 0.0, lo = 0.0, hi = -1.0;
+        for (const auto& x : iv[k]) {
+            if (x.first > hi) {
+                if (hi > lo) busy += hi - lo;
+                lo = x.first;
+                hi = x.second;
+            } else {
+                hi = std::max(hi, x.second);
+            }
+        }
+        if (hi > lo) busy += hi - lo;
+        acc[k].busy_ms = busy;
     }
     int n = 0;
     for (int k = 0; k < KID_COUNT; ++k) {
@@ -404,8 +425,18 @@ int pt_profile_read(pt_scene* s, pt_kernel_time* out, int max_entries, int* n_ou
 
 const char* pt_last_error(void) { return g_err.c_str(); }
 
+int pt_set_hw_queues(int n) {
+    if (n < 1 || n > 32) return fail(PT_ERR_INVALID, "hardware queue count must be in [1, 32]");
+    if (g_hip_touched) return fail(PT_ERR_INVALID, "the HIP runtime is already running in this process");
+    char v[16];
+    std::snprintf(v, sizeof v, "%d", n);
+    setenv("GPU_MAX_HW_QUEUES", v, 1);
+    return PT_OK;
+}
+
 int pt_device_count(int* count_out) {
     if (!count_out) return fail(PT_ERR_INVALID, "count_out is NULL");
+    g_hip_touched = true;
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) n = 0;
@@ -417,6 +448,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
                     pt_scene** scene_out) {
     if (!triangle_data || !bvh_data || !scene_out) return fail(PT_ERR_INVALID, "null argument");
     *scene_out = nullptr;
+    g_hip_touched = true;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PT_ERR_NODEVICE, "no HIP device visible");
     if (device < 0 || device >= ndev) return fail(PT_ERR_NODEVICE, "device ordinal out of range");
@@ -496,6 +528,7 @@ void pt_scene_destroy(pt_scene* s) {
     }
     if (s->ws.fork) hipEventDestroy(s->ws.fork);
     if (s->d_rgba) hipFree(s->d_rgba);
+    if (s->h_ctl) hipHostFree(s->h_ctl);
     if (s->d_mem) hipFree(s->d_mem);
     s->prof.destroy();
     delete s;
@@ -572,13 +605,14 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     return lo;
 }
 
-// paths in flight per wavefront batch (~1.1 GB of SoA state at kWfBytesPerPath)
+// paths in flight per wavefront batch (kWfBytesPerPath = 188 B of queue state per path: 8 M
+// paths ~ 1.6 GB, plus the queue slack of the region layout)
 constexpr uint64_t kWfTargetPaths = 8ull << 20;
 
 int ensure_wavefront(pt_scene* s, uint64_t paths) {
     if (s->d_wf && s->wf.capacity >= paths) return PT_OK;
     if (paths > 0x7fffffffull) return fail(PT_ERR_INVALID, "image too large for one wavefront batch");
-    if (s->d_wf) { hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; }
+    if (s->d_wf) { hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; s->wf.capacity = 0; }
     const size_t n = paths;
     // queue arrays carry slack so that each half can be cut into up to kQueueSlackRegions / 1.5
     // regions of a whole number of 64-entry batches holding all its paths (k_wf_step_bf,
@@ -591,7 +625,11 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     const size_t o_p0 = take(16 * qn), o_p1 = take(16 * qn), o_p2 = take(8 * qn), o_hit = take(8 * qn),
                  o_rad = take(12 * n), o_ctl = take(4 * kMaxParts * WF_CTL_WORDS),
                  o_rcnt = take(4 * kMaxParts * 3 * kRegions);
-    if (hipMalloc(&s->d_wf, off) != hipSuccess) { s->d_wf = nullptr; return fail(PT_ERR_NOMEM, "hipMalloc wavefront state"); }
+    if (hipMalloc(&s->d_wf, off) != hipSuccess) {
+        s->d_wf = nullptr;
+        (void)hipGetLastError();  // the failed allocation is reported here, not by a later call
+        return fail(PT_ERR_NOMEM, "hipMalloc wavefront state");
+    }
     char* b = static_cast<char*>(s->d_wf);
     auto f4 = [&](size_t o) { return reinterpret_cast<float4*>(b + o); };
     WfBuffers& w = s->wf;
@@ -614,9 +652,41 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
         for (int h = 0; h < 2 && ok; ++h) ok = hipEventCreateWithFlags(&s->ws.traced[h], hipEventDisableTiming) == hipSuccess;
         if (!ok) return fail(PT_ERR_HIP, "creating the wavefront's streams");
     }
+    if (!s->h_ctl) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&s->h_ctl), 4 * kMaxParts * WF_CTL_WORDS) != hipSuccess) {
+            s->h_ctl = nullptr;
+            return fail(PT_ERR_NOMEM, "hipHostMalloc wavefront control mirror");
+        }
+        std::memset(s->h_ctl, 0, 4 * kMaxParts * WF_CTL_WORDS);
+    }
     w.capacity = (uint32_t)n;
     w.qcap = (uint32_t)qn;
     return PT_OK;
+}
+
+// A trace wave that hit its watchdog (k_wf_trace: kTraceWatchdog iterations or
+// kTraceWatchdogTicks) sets ctl[WF_WATCHDOG] and leaves its state in ctl[WF_SNAP..]; later
+// launches of the scene skip their work.  The pinned mirror h_ctl receives the control words
+// after every wavefront render on its stream; once that copy has landed (the caller synchronised,
+// or the blocking calls' own synchronisation) the flag is reported here and cleared on the device
+// (ordered on `stream`) and in the mirror.
+int take_watchdog(pt_scene* s, hipStream_t stream) {
+    if (!s->h_ctl) return PT_OK;
+    int h = 0;
+    while (h < kMaxParts && !__atomic_load_n(&s->h_ctl[h * WF_CTL_WORDS + WF_WATCHDOG], __ATOMIC_ACQUIRE)) ++h;
+    if (h == kMaxParts) return PT_OK;
+    uint32_t v[WF_SNAP_WORDS];
+    std::memcpy(v, s->h_ctl + h * WF_CTL_WORDS + WF_SNAP, sizeof v);
+    for (int k = 0; k < kMaxParts; ++k)
+        HIP_TRY(hipMemsetAsync(s->wf.ctl + k * WF_CTL_WORDS + WF_WATCHDOG, 0,
+                               (WF_SNAP + WF_SNAP_WORDS - WF_WATCHDOG) * sizeof(uint32_t), stream));
+    std::memset(s->h_ctl, 0, 4 * kMaxParts * WF_CTL_WORDS);
+    char msg[320];
+    std::snprintf(msg, sizeof(msg),
+                  "wavefront trace gave up after kTraceWatchdog iterations (result invalid); first wave: count=%u "
+                  "nwaves=%u w=%u J=%u jl=%u wv=%u nv=%u cur=%u flushed=%u in_flight=%u mask=%08x%08x queue=%u",
+                  v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[11], v[10], v[12]);
+    return fail(PT_ERR_HIP, msg);
 }
 
 int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframes, uint32_t stride, int max_depth,
@@ -646,10 +716,15 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         const uint64_t all = npix * (accum ? nframes : 1);
         const uint64_t two = 2 * npix <= 0x7fffffffull ? 2 * npix : npix;
         const uint64_t want = std::max<uint64_t>(std::min<uint64_t>(all, two), std::min<uint64_t>(all, target));
+        if ((rc = take_watchdog(s, stream)) != PT_OK) return rc;  // an earlier asynchronous render failed
         int rc2 = ensure_wavefront(s, want);
+        // the two-frame minimum doubles the state of images above the batch target (~188 B/path):
+        // fall back to one frame per batch when that does not fit
+        if (rc2 == PT_ERR_NOMEM && want > std::min<uint64_t>(all, npix)) rc2 = ensure_wavefront(s, std::min<uint64_t>(all, npix));
         if (rc2 != PT_OK) return rc2;
         HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
                                  stream, s->ws));
+        HIP_TRY(hipMemcpyAsync(s->h_ctl, s->wf.ctl, 4 * kMaxParts * WF_CTL_WORDS, hipMemcpyDeviceToHost, stream));
         return PT_OK;
     }
     HIP_TRY(launch_megakernel(lo, view, fp, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt, stream));
@@ -679,23 +754,18 @@ int pt_render_async(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t
 
 // After a synchronised call: a trace wave that hit kTraceWatchdog left a flag (cleared here).
 static int check_watchdog(pt_scene* s) {
-    if (!s->d_wf) return PT_OK;
-    uint32_t flag = 0, h = 0;
-    for (; h < kMaxParts; ++h) {  // one control block per part of a batch
-        HIP_TRY(hipMemcpy(&flag, s->wf.ctl + h * WF_CTL_WORDS + WF_WATCHDOG, sizeof(flag), hipMemcpyDeviceToHost));
-        if (flag) break;
-    }
-    if (!flag) return PT_OK;
-    uint32_t* ctl = s->wf.ctl + h * WF_CTL_WORDS;
-    uint32_t v[WF_SNAP_WORDS] = {};
-    HIP_TRY(hipMemcpy(v, ctl + WF_SNAP, sizeof(v), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemset(ctl + WF_WATCHDOG, 0, (WF_SNAP + WF_SNAP_WORDS - WF_WATCHDOG) * sizeof(uint32_t)));
-    char msg[320];
-    std::snprintf(msg, sizeof(msg),
-                  "wavefront trace gave up after kTraceWatchdog iterations (result invalid); first wave: count=%u "
-                  "nwaves=%u w=%u J=%u jl=%u wv=%u nv=%u cur=%u flushed=%u in_flight=%u mask=%08x%08x queue=%u",
-                  v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[11], v[10], v[12]);
-    return fail(PT_ERR_HIP, msg);
+    int rc = take_watchdog(s, s->stream);
+    if (rc != PT_OK) hipStreamSynchronize(s->stream);  // the flag reset is done before the error returns
+    return rc;
+}
+
+int pt_scene_check(pt_scene* s) {
+    if (!s) return fail(PT_ERR_INVALID, "null scene");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());  // every render of the scene, on whatever stream, has finished
+    int rc = take_watchdog(s, nullptr);
+    if (rc != PT_OK) hipDeviceSynchronize();
+    return rc;
 }
 
 // The blocking calls' own stream, created on first use: asynchronous callers never pay for a

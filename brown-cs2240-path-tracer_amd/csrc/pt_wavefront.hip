@@ -135,7 +135,8 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 // Inside a wave, window j's entries have the wave-local sequence numbers 32j .. 32j+31, which
 // index the hit ring.
 template <bool LDS, int TRAV, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out) {
+__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
+                                                          uint32_t watchdog) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     for (uint32_t guard = 0;; ++guard) {
         // every wave reaches an exit: after kTraceWatchdog iterations or kTraceWatchdogTicks of
         // wall clock it reports instead of hanging (and later launches of the render skip)
-        if (guard == kTraceWatchdog ||
+        if (guard == watchdog ||
             ((guard & 1023u) == 1023u && wall_clock64() - t_start > kTraceWatchdogTicks)) {
             const uint64_t hm = __ballot(has);
             if (lane == 0) {
@@ -999,6 +1000,8 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
     int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
     if (const char* e = std::getenv("PT_WF_TRACE_BLOCKS")) tblocks = std::max(1, std::min(tblocks, std::atoi(e)));  // tests
     const int iters = 2 * (fp.max_depth + 1);
+    uint32_t watchdog = kTraceWatchdog;  // PT_TRACE_WATCHDOG: tests of the failure report
+    if (const char* e = std::getenv("PT_TRACE_WATCHDOG")) watchdog = (uint32_t)std::max(1L, std::atol(e));
     int bf_slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
     if (const char* e = std::getenv("PT_BF_SLOTS")) bf_slots = std::max(0, std::min(kBfSlots, std::atoi(e)));
     if constexpr (TRAV >= 500) {  // one workgroup-local launch per batch (k_wf_persist_bf), one stream
@@ -1085,7 +1088,7 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                               dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
                 else
                     PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc,
-                              w, in_q, cnt);
+                              w, in_q, cnt, watchdog);
                 if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
                 if ((it & 1) == 0)
                     PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,

@@ -17,11 +17,18 @@ class Vertex {
     }
 }
 
+// js-geometry's Bounds fixes its strides when it is constructed: bvh.ts builds every child box
+// as new Bounds(parent.min.clone(), parent.max.clone()) and only then moves one face to the
+// split, so a node's stride_* (its split-axis choice, bvh.ts:46-52) is its PARENT's extent.
+// The library's source is not in the reference; the reference's own renders decide it
+// (scenes/student_outputs/final, DESIGN.md §4): with live strides CornellBox full_lighting and
+// mirror differ from them beyond Monte Carlo noise (4x4-block L2 1.19x / 1.70x the noise),
+// with construction-time strides they agree (0.97x / 1.00x).
 class Bounds {
-    constructor(min, max) { this.min = min; this.max = max; }
-    get stride_x() { return this.max.x - this.min.x; }
-    get stride_y() { return this.max.y - this.min.y; }
-    get stride_z() { return this.max.z - this.min.z; }
+    constructor(min, max) {
+        this.min = min; this.max = max;
+        this.stride_x = max.x - min.x; this.stride_y = max.y - min.y; this.stride_z = max.z - min.z;
+    }
 }
 
 const mat4_identity = () => [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1];

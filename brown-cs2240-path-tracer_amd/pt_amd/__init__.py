@@ -11,6 +11,7 @@ The product path never falls back to CPU code: if libpt_hip.so is missing or
 no GPU is visible, calls raise `PtError`.
 """
 from ._lib import (  # noqa: F401
+    ABI_VERSION,
     MODE_AUTO,
     MODE_MEGAKERNEL,
     MODE_WAVEFRONT,
@@ -25,6 +26,7 @@ from ._lib import (  # noqa: F401
     load_library,
     selftest_math,
     selftest_rcp,
+    set_hw_queues,
     tonemap,
 )
 from .host import PackedScene, load_scene, program_entry  # noqa: F401

@@ -6,14 +6,10 @@ import os
 
 import numpy as np
 
-# The dual-stream wavefront wants its two streams on hardware queues of their own; HIP reads
-# this once, when its runtime starts (torch may start it on import, below), so set it first.
-# A value the process already set wins (csrc/pt_capi.hip does the same for non-Python hosts).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _LIB_FILE = os.path.join(_PKG_ROOT, "lib", "libpt_hip.so")
 
+ABI_VERSION = 2  # include/pt_hip.h PT_ABI_VERSION
 MODE_AUTO, MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1, 2
 MATH_FNS = ["sin", "cos", "tan", "acos", "log2", "exp2", "pow", "sqrt", "div", "hash1u", "hash1", "hash2x",
             "hash2y", "min", "max"]
@@ -47,7 +43,7 @@ class SceneInfo(ctypes.Structure):
 
 class KernelTime(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_uint64), ("total_ms", ctypes.c_double),
-                ("min_ms", ctypes.c_double), ("max_ms", ctypes.c_double)]
+                ("min_ms", ctypes.c_double), ("max_ms", ctypes.c_double), ("busy_ms", ctypes.c_double)]
 
 
 _lib = None
@@ -80,6 +76,8 @@ def load_library():
     if not os.path.exists(_LIB_FILE):
         raise PtError(-4, f"{_LIB_FILE} not built (run __graft_entry__.build() or make -C csrc)")
     L = ctypes.CDLL(_LIB_FILE)
+    if L.pt_abi_version() != ABI_VERSION:
+        raise PtError(-1, f"{_LIB_FILE} has ABI {L.pt_abi_version()}, this binding expects {ABI_VERSION} (rebuild)")
     p, i, u32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_size_t
     L.pt_abi_version.restype = i
     L.pt_last_error.restype = ctypes.c_char_p
@@ -102,7 +100,9 @@ def load_library():
     L.pt_render_image.argtypes = [p, p, u32, u32, u32, i, i, p, p]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     L.pt_scene_set_vertex_normals.argtypes = [p, i]
-    for fn in ("pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+    L.pt_scene_check.argtypes = [p]
+    L.pt_set_hw_queues.argtypes = [i]
+    for fn in ("pt_scene_check", "pt_set_hw_queues", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
                "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
@@ -117,6 +117,13 @@ def _check(rc: int):
 
 def abi_version() -> int:
     return int(load_library().pt_abi_version())
+
+
+def set_hw_queues(n: int = 8):
+    """Explicit opt-in (pt_set_hw_queues): ask HIP for n hardware queues per process.  Only
+    effective before the HIP runtime starts in this process (before torch touches the GPU);
+    the library itself never changes the environment."""
+    os.environ["GPU_MAX_HW_QUEUES"] = str(int(n))
 
 
 def device_count() -> int:
@@ -211,6 +218,11 @@ class Scene:
         _check(self._lib.pt_tonemap_async(self._h, ctypes.c_void_p(d_accum_ptr), npix, sample_runs,
                                           ctypes.c_void_p(d_rgba_ptr), ctypes.c_void_p(stream_ptr or None)))
 
+    def check(self):
+        """Wait for this scene's renders and raise if one failed on the device (pt_scene_check:
+        a wavefront traversal wave that gave up at its watchdog limit)."""
+        _check(self._lib.pt_scene_check(self._h))
+
     def profile_enable(self, enable: bool = True):
         """Bracket every kernel launch of this scene with HIP events (discards earlier records)."""
         _check(self._lib.pt_profile_enable(self._h, 1 if enable else 0))
@@ -220,14 +232,16 @@ class Scene:
         _check(self._lib.pt_profile_select(self._h, kernel.encode() if kernel else None))
 
     def profile_read(self) -> dict:
-        """{kernel name: {"launches", "total_ms", "avg_ms", "min_ms", "max_ms"}} since profile_enable()."""
+        """{kernel name: {"launches", "total_ms", "avg_ms", "min_ms", "max_ms", "busy_ms"}} since
+        profile_enable(); busy_ms = union of the launches' intervals (parts on several streams overlap)."""
         buf = (KernelTime * 16)()
         n = ctypes.c_int(0)
         _check(self._lib.pt_profile_read(self._h, buf, 16, ctypes.byref(n)))
         out = {}
         for k in buf[: n.value]:
             out[k.name.decode()] = {"launches": int(k.launches), "total_ms": k.total_ms,
-                                    "avg_ms": k.total_ms / max(1, k.launches), "min_ms": k.min_ms, "max_ms": k.max_ms}
+                                    "avg_ms": k.total_ms / max(1, k.launches), "min_ms": k.min_ms, "max_ms": k.max_ms,
+                                    "busy_ms": k.busy_ms}
         return out
 
     def frame(self, meta, t: int, max_depth: int = -1) -> np.ndarray:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2
 
 typedef enum {
     PT_OK = 0,
@@ -80,6 +80,9 @@ typedef struct {
     double total_ms;   /* sum over launches of the HIP-event time around each launch */
     double min_ms;
     double max_ms;
+    double busy_ms;    /* GPU time during which at least one launch of the kernel ran: the union of the
+                          launches' event intervals (launches on several streams overlap, so this is
+                          <= total_ms; bytes / busy_ms is the kernel's achieved rate) */
 } pt_kernel_time;
 
 /* ABI version of the loaded library (== PT_ABI_VERSION when headers match). */
@@ -117,9 +120,26 @@ int pt_render(pt_scene* scene, const float meta[48], uint32_t frame0, uint32_t n
               int max_depth, int mode, float* accum, pt_counters* counters);
 
 /* Same on device memory, asynchronous on `stream` (hipStream_t; NULL = default stream).
- * d_accum: device f32 [H][W][3] in/out.  d_counters: device pt_counters or NULL (added to). */
+ * d_accum: device f32 [H][W][3] in/out.  d_counters: device pt_counters or NULL (added to).
+ * A device-side failure of an earlier asynchronous render of this scene (a traversal wave that
+ * gave up, see pt_scene_check) is reported by the next call once that render has completed:
+ * this call then fails with PT_ERR_HIP and renders nothing. */
 int pt_render_async(pt_scene* scene, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
                     int max_depth, int mode, float* d_accum, pt_counters* d_counters, void* stream);
+
+/* Completion check of the asynchronous calls: waits for every render of the scene to finish
+ * (blocking) and reports a device-side failure of any of them — a wavefront traversal wave that
+ * gave up after its watchdog limit leaves a flag instead of hanging, and the accumulators of
+ * that render are invalid — as PT_ERR_HIP with the wave's state in pt_last_error().  The flag is
+ * cleared.  The blocking calls (pt_render, pt_frame, pt_render_image) check it themselves. */
+int pt_scene_check(pt_scene* scene);
+
+/* Explicit opt-in (no load-time side effect): ask HIP for `n` hardware queues per process by
+ * setting GPU_MAX_HW_QUEUES, which the HIP runtime reads once, when it starts.  Call before any
+ * HIP use in the process (the first pt_* call that touches a device starts it); afterwards it
+ * has no effect and returns PT_ERR_INVALID.  Hosts that put many streams of their own beside the
+ * wavefront's two part streams (e.g. torch) want 8 so the parts do not share a queue. */
+int pt_set_hw_queues(int n);
 
 /* One reference dispatch: radiance[H][W][3] = radiance() of every pixel for RNG salt t
  * (the resultMatrix of program-raymarch.wgsl:82-84, before host clamping). */

@@ -306,18 +306,27 @@ def _overlap(omin, omax, bmin, bmax):  # math.ts:45-49, vectorised over objects
             (bmin[2] <= omax[:, 2]) & (omin[:, 2] <= bmax[2]))
 
 
-def build_bvh(omin: np.ndarray, omax: np.ndarray, outer_min, outer_max, stats: dict | None = None) -> Node:
+def build_bvh(omin: np.ndarray, omax: np.ndarray, outer_min, outer_max, stats: dict | None = None,
+              live_strides: bool = False) -> Node:
+    """bvh.ts:25-187.  Node strides (the split-axis choice) are js-geometry's construction-time
+    strides, i.e. the parent's extent (DESIGN.md §4 gives the evidence); live_strides=True uses
+    each node's own extent instead — the reading SURVEY.md §8's table was derived with, kept so
+    the survey's independent counts still pin the rest of the builder."""
     MAX_DEPTH, MAX_OBJ = 16, 16
 
     def split_coord(axis, w0, bmin, bmax):
         w1 = 1.0 - w0
         return w0 * bmax[axis] + w1 * bmin[axis]
 
-    def recurse(node: Node, depth: int):
+    def recurse(node: Node, depth: int, stride):
+        # stride: the extent js-geometry's Bounds fixed at construction (bvh.ts:72-73,113-114 clone the
+        # PARENT's min/max into a new Bounds, then move one face), i.e. the parent's extent; the root's own
         if depth >= MAX_DEPTH:
             node.is_leaf = True
             return
-        sx = node.bmax[0] - node.bmin[0]; sy = node.bmax[1] - node.bmin[1]; sz = node.bmax[2] - node.bmin[2]
+        sx, sy, sz = stride
+        if live_strides:
+            sx = node.bmax[0] - node.bmin[0]; sy = node.bmax[1] - node.bmin[1]; sz = node.bmax[2] - node.bmin[2]
         if sx >= sy and sx >= sz:
             axis = 0
         elif sy >= sx and sy >= sz:
@@ -345,18 +354,19 @@ def build_bvh(omin: np.ndarray, omax: np.ndarray, outer_min, outer_max, stats: d
         lsel = node.objs[_overlap(lo, hi, node.bmin, lmax)]
         rsel = node.objs[_overlap(lo, hi, rmin, node.bmax)]
         node.left = Node(False, -1, list(node.bmin), lmax, lsel)
+        own = (node.bmax[0] - node.bmin[0], node.bmax[1] - node.bmin[1], node.bmax[2] - node.bmin[2])
         if len(lsel) <= MAX_OBJ or len(lsel) == len(node.objs):
             node.left.is_leaf = True
         else:
-            recurse(node.left, depth + 1)
+            recurse(node.left, depth + 1, own)
         node.right = Node(False, -1, rmin, list(node.bmax), rsel)
         if len(rsel) <= MAX_OBJ or len(rsel) == len(node.objs):
             node.right.is_leaf = True
         else:
-            recurse(node.right, depth + 1)
+            recurse(node.right, depth + 1, own)
 
     root = Node(False, 0, list(outer_min), list(outer_max), np.arange(len(omin)))
-    recurse(root, 1)
+    recurse(root, 1, (outer_max[0] - outer_min[0], outer_max[1] - outer_min[1], outer_max[2] - outer_min[2]))
     return root
 
 
@@ -470,7 +480,7 @@ class PackedScene:
     stats: dict = field(default_factory=dict)
 
 
-def pack_primitive(obj_text: str, mtl_text: str, ctm) -> PackedScene:
+def pack_primitive(obj_text: str, mtl_text: str, ctm, live_strides: bool = False) -> PackedScene:
     """index.ts:128-161 for one primitive."""
     g = parse_obj(obj_text, mtl_text, ctm)
     tri = pack_scene_object_group(g)
@@ -486,12 +496,12 @@ def pack_primitive(obj_text: str, mtl_text: str, ctm) -> PackedScene:
             recs.append([ind[i], ind[i + 1], ind[i + 2], mat_i])
             omin.append(tmin); omax.append(tmax)
     omin_a, omax_a = np.array(omin, dtype=np.float64), np.array(omax, dtype=np.float64)
-    root = build_bvh(omin_a, omax_a, bmin, bmax)
+    root = build_bvh(omin_a, omax_a, bmin, bmax, live_strides=live_strides)
     bvh = pack_bvh(root, bmin, bmax, np.array(recs, dtype=np.float64))
     return PackedScene(tri, bvh, bmin, bmax, bvh_stats(root))
 
 
-def load_scene(scene_xml_path: str, asset_root: str):
+def load_scene(scene_xml_path: str, asset_root: str, live_strides: bool = False):
     """Loads the XML, packs the FIRST primitive (index.ts:116), returns (camera, PackedScene)."""
     import os
     with open(scene_xml_path) as f:
@@ -507,7 +517,7 @@ def load_scene(scene_xml_path: str, asset_root: str):
             mtl_text = f.read()
     except OSError:
         mtl_text = ""
-    return camera, pack_primitive(obj_text, mtl_text, p["ctm"])
+    return camera, pack_primitive(obj_text, mtl_text, p["ctm"], live_strides=live_strides)
 
 
 # ----------------------------------------------------------------------------

@@ -1,32 +1,66 @@
 #!/usr/bin/env python3
-"""Summarize rocprofv3 FETCH_SIZE / WRITE_SIZE passes (gpurun_out/traffic) into traffic.json.
+"""Summarize the rocprofv3 PMC passes of scripts/collect_traffic.sh (gpurun_out/traffic/{fetch,
+write,valu}) into traffic.json: per kernel instance and launch, HBM bytes (FETCH_SIZE x 2 for
+gfx950 + WRITE_SIZE, KB -> bytes) and the VALU issue fraction
+    valu_issue = 4 * SQ_ACTIVE_INST_VALU / (128 * GRBM_GUI_ACTIVE)
+(SQ_ACTIVE_INST_VALU in quad-cycles, ~1 per wave64 VALU instruction = 4 SIMD cycles;
+GRBM_GUI_ACTIVE summed over the 8 XCDs, each of 32 CUs x 4 SIMDs: SIMD-cycles = GRBM / 8 x 1024).
+PMC passes serialise the kernels, so these are per-launch figures of a kernel running alone.
 Usage: summarize_traffic.py [out.json]"""
-import csv, glob, json, os, sys, collections
-def load(tag, counter):
-    agg = collections.defaultdict(list)
-    for f in glob.glob(f"gpurun_out/traffic/{tag}/**/*counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == counter:
-                agg[(r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Dispatch_Id"])].append(float(r["Counter_Value"]))
-    per = collections.defaultdict(list)
-    for (k, d), v in agg.items():
-        per[k].append(sum(v))
-    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
-(fetch, ndisp), (write, _) = load("fetch", "FETCH_SIZE"), load("write", "WRITE_SIZE")
-line = [json.loads(l) for l in open("gpurun_out/traffic/fetch.log") if l.startswith("{")][0]
-cfg = line["config"]
-W, H = 1024, 1024
+import collections
+import csv
+import glob
+import json
+import os
 import re
-m = re.search(r"(\d+)x(\d+) (\d+)spp depth (\d+)", cfg["workload"])
-key = f"{m.group(1)}x{m.group(2)}x{m.group(3)}x{m.group(4)}x{line['n_gpus']}"
-path = sys.argv[1] if len(sys.argv) > 1 else "profiles/traffic.json"
-t = json.load(open(path)) if os.path.exists(path) else {}
-t[key] = {}
-for k in fetch:
-    short = k.split("::")[-1]
-    fb, wb = fetch[k] * 1024 * 2, write.get(k, 0.0) * 1024
-    t[key][short] = {"fetch_kb_raw": fetch[k], "write_kb": write.get(k, 0.0), "hbm_bytes_per_launch": fb + wb,
-                     "dispatches": ndisp[k],
-                     "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KB -> bytes, mean per dispatch"}
-json.dump(t, open(path, "w"), indent=1)
-print(json.dumps(t[key], indent=1))
+import sys
+
+SRC = "gpurun_out/traffic"
+
+
+def load(tag, counters):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    for f in glob.glob(f"{SRC}/{tag}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] in counters:
+                k = (r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Dispatch_Id"])
+                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (k, _), cs in agg.items():
+        for n, v in cs.items():
+            per[k][n].append(v)
+    mean = {k: {n: sum(v) / len(v) for n, v in cs.items()} for k, cs in per.items()}
+    ndisp = {k: max(len(v) for v in cs.values()) for k, cs in per.items()}
+    return mean, ndisp
+
+
+def main():
+    fetch, ndisp = load("fetch", {"FETCH_SIZE"})
+    write, _ = load("write", {"WRITE_SIZE"})
+    valu, _ = load("valu", {"SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES",
+                            "SQ_WAVES", "GRBM_GUI_ACTIVE"})
+    line = [json.loads(x) for x in open(f"{SRC}/fetch.log") if x.startswith("{")][0]
+    m = re.search(r"(\d+)x(\d+) (\d+)spp depth (\d+)", line["config"]["workload"])
+    key = f"{m.group(1)}x{m.group(2)}x{m.group(3)}x{m.group(4)}x{line['n_gpus']}"
+    path = sys.argv[1] if len(sys.argv) > 1 else "profiles/traffic.json"
+    t = json.load(open(path)) if os.path.exists(path) else {}
+    t[key] = {"_source": "scripts/collect_traffic.sh: rocprofv3 --pmc passes FETCH_SIZE | WRITE_SIZE | SQ_ACTIVE_INST_VALU.. "
+                         "GRBM_GUI_ACTIVE of `bench.py " + " ".join(sys.argv[2:]) + "` (" + line["config"]["workload"] + ")"}
+    for k in fetch:
+        short = k.split("::")[-1]
+        fb, wb = fetch[k]["FETCH_SIZE"] * 1024 * 2, write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+        e = {"fetch_kb_raw": fetch[k]["FETCH_SIZE"], "write_kb": write.get(k, {}).get("WRITE_SIZE", 0.0),
+             "hbm_bytes_per_launch": fb + wb, "dispatches": ndisp[k],
+             "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KB -> bytes, mean per dispatch"}
+        v = valu.get(k)
+        if v and v.get("GRBM_GUI_ACTIVE"):
+            e["valu_issue"] = 4.0 * v["SQ_ACTIVE_INST_VALU"] / (128.0 * v["GRBM_GUI_ACTIVE"])
+            e["valu_lane_util"] = v.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * v["SQ_ACTIVE_INST_VALU"]) if v.get("SQ_ACTIVE_INST_VALU") else None
+            e["valu_counters"] = v
+        t[key][short] = e
+    json.dump(t, open(path, "w"), indent=1)
+    print(json.dumps(t[key], indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -45,7 +46,39 @@ def test_kernels_built_for_gfx950():
 
 
 def test_abi_version():
-    assert pt_amd.abi_version() == 1
+    assert pt_amd.abi_version() == 2 == pt_amd.ABI_VERSION
+
+
+def test_kernel_time_struct_matches_header():
+    # pt_kernel_time: name[32], launches, total/min/max/busy ms
+    assert ctypes.sizeof(pt_amd._lib.KernelTime) == 32 + 8 + 4 * 8
+    assert "busy_ms" in open(HEADER).read()
+
+
+def test_no_load_time_environment_change():
+    """Loading the library changes nothing in the process environment; pt_set_hw_queues is the
+    explicit opt-in, effective only before the library touches HIP."""
+    code = (
+        "import ctypes, os, sys\n"
+        "os.environ.pop('GPU_MAX_HW_QUEUES', None)\n"
+        f"L = ctypes.CDLL({pt_amd.lib_path()!r})\n"
+        "assert 'GPU_MAX_HW_QUEUES' not in os.environ\n"
+        "libc = ctypes.CDLL(None); libc.getenv.restype = ctypes.c_char_p\n"
+        "assert libc.getenv(b'GPU_MAX_HW_QUEUES') is None\n"
+        "assert L.pt_set_hw_queues(0) == -1 and L.pt_set_hw_queues(99) == -1\n"
+        "assert L.pt_set_hw_queues(8) == 0 and libc.getenv(b'GPU_MAX_HW_QUEUES') == b'8'\n"
+        "n = ctypes.c_int(0); assert L.pt_device_count(ctypes.byref(n)) == 0\n"
+        "assert L.pt_set_hw_queues(4) == -1  # the runtime is up now\n"
+    )
+    env = dict(os.environ, PT_AMD_NO_TORCH="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stderr
+
+
+def test_scene_check_rejects_null():
+    lib = pt_amd.load_library()
+    assert lib.pt_scene_check(None) == -1
+    assert b"null" in lib.pt_last_error()
 
 
 def test_errors_without_gpu():

@@ -77,7 +77,7 @@ KERNELS = {
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
-            "PT_CULL", "PT_FUSE_GEN")
+            "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -243,8 +243,9 @@ def test_render_accum_bitexact(packed, kernel, scene, W, H, frame0, nframes, str
 def test_scene_info_matches_survey(packed):
     with pt_amd.Scene(packed["CornellBox"].triangle_data, packed["CornellBox"].bvh_data) as s:
         info = s.info
-    # 21 nodes / 11 leaves (10 internal), 164 leaf refs, max leaf 20, light = 2 triangles
-    assert info["nodes"] == 10 and info["leaves"] == 11 and info["leaf_refs"] == 164 and info["max_leaf"] == 20
+    # js-geometry's construction-time strides: 33 nodes / 17 leaves (16 internal), 247 leaf
+    # refs, max leaf 16 (SURVEY.md §8's 21 / 11 / 164 / 20 read the strides live); light = 2 triangles
+    assert info["nodes"] == 16 and info["leaves"] == 17 and info["leaf_refs"] == 247 and info["max_leaf"] == 16
     assert info["emissive_tris"] == 2 and info["materials"] == 8 and info["vertices"] == 72
 
 

@@ -46,21 +46,7 @@ def test_packed_buffers_golden_sha(packed, scene):
     assert hashlib.sha256(p.bvh_data.tobytes()).hexdigest() == g["bvh_sha256"]
 
 
-@pytest.mark.parametrize("scene", ["CornellBox", "CornellBox-Mirror", "CornellBox-Glossy", "MedievalBoat"])
-def test_scene_counts_match_survey(packed, scene):
-    """SURVEY.md §8 table, derived by the survey's own throwaway restatement."""
-    with open(os.path.join(GOLDEN, "survey_scene_stats.json")) as f:
-        g = json.load(f)[scene]
-    p = packed[scene]
-    tri, bvh = p.triangle_data, p.bvh_data
-    assert int(tri[0]) == g["verts"]
-    assert (int(tri[4]) - int(tri[3])) // 4 == g["tris"]
-    assert bvh.size == g["bvh_len"]
-    if "tri_len_no_vn_pad" in g:
-        assert int(tri[5]) == g["tri_len_no_vn_pad"]
-    if "vn_len" in g:
-        assert int(tri[6]) == g["vn_len"]
-    # walk the packed tree: nodes / leaves / refs / max leaf
+def tree_counts(bvh):
     nodes = leaves = refs = max_leaf = 0
     stack = [6]
     while stack:
@@ -73,7 +59,42 @@ def test_scene_counts_match_survey(packed, scene):
             max_leaf = max(max_leaf, n)
         else:
             stack += [int(bvh[o + 2]), int(bvh[o + 3])]
-    assert (nodes, leaves, refs, max_leaf) == (g["nodes"], g["leaves"], g["refs"], g["max_leaf"])
+    return nodes, leaves, refs, max_leaf
+
+
+@pytest.mark.parametrize("scene", ["CornellBox", "CornellBox-Mirror", "CornellBox-Glossy", "MedievalBoat"])
+def test_scene_counts_match_survey(packed, scene):
+    """SURVEY.md §8 table, derived by the survey's own throwaway restatement: the triangle buffer
+    (tree-independent) from the product, the tree from the oracle's builder under the survey's
+    reading of Bounds.stride_* (each node's own extent).  The product's tree uses js-geometry's
+    construction-time strides instead and is pinned by the next test."""
+    import scene_oracle as so
+    with open(os.path.join(GOLDEN, "survey_scene_stats.json")) as f:
+        g = json.load(f)[scene]
+    p = packed[scene]
+    tri = p.triangle_data
+    assert int(tri[0]) == g["verts"]
+    assert (int(tri[4]) - int(tri[3])) // 4 == g["tris"]
+    if "tri_len_no_vn_pad" in g:
+        assert int(tri[5]) == g["tri_len_no_vn_pad"]
+    if "vn_len" in g:
+        assert int(tri[6]) == g["vn_len"]
+    _, live = so.load_scene(os.path.join(SCENES, "scene_assets", scene + ".xml"), os.path.join(SCENES, "scene_assets"),
+                            live_strides=True)
+    assert live.bvh_data.size == g["bvh_len"]
+    assert tree_counts(live.bvh_data) == (g["nodes"], g["leaves"], g["refs"], g["max_leaf"])
+
+
+def test_product_tree_uses_construction_time_strides(packed):
+    """CornellBox: the product's tree is the oracle's under js-geometry's construction-time
+    strides (a node's split axis follows its parent's extent), not the survey's reading."""
+    import scene_oracle as so
+    p = packed["CornellBox"]
+    _, ctor = so.load_scene(os.path.join(SCENES, "scene_assets", "CornellBox.xml"), os.path.join(SCENES, "scene_assets"))
+    _, live = so.load_scene(os.path.join(SCENES, "scene_assets", "CornellBox.xml"), os.path.join(SCENES, "scene_assets"),
+                            live_strides=True)
+    assert p.bvh_data.tobytes() == ctor.bvh_data.tobytes() != live.bvh_data.tobytes()
+    assert tree_counts(p.bvh_data) != tree_counts(live.bvh_data)
 
 
 def test_ini_configs_meta(tmp_path):
@@ -161,7 +182,7 @@ try { pt.sceneCreate(new Float32Array(64), new Float32Array(64), 0); } catch (e)
 let terr = null;
 try { pt.render(1, 2); } catch (e) { terr = e.constructor.name; }
 console.log(JSON.stringify({abi: pt.abiVersion(), keys: Object.keys(pt).sort(), err, terr}));''')
-    assert r["abi"] == 1
+    assert r["abi"] == 2
     assert r["keys"] == sorted(["abiVersion", "deviceCount", "sceneCreate", "sceneInfo", "render", "renderSync", "frame",
                                 "tonemap", "profileEnable", "profileRead", "bvhBuild", "renderImage",
                                 "sceneSetVertexNormals"])
