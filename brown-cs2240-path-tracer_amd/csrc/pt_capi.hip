@@ -7,8 +7,13 @@
 #include <array>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: librccl is opened on first multi-device use (pt_render_multi)
 
 #include "../../include/pt_hip.h"
 #include "pt_kernels.h"
@@ -315,6 +320,10 @@ struct pt_scene {
     // stream: a watchdog flag set by an asynchronous render surfaces once that copy has landed
     // (next call, pt_scene_check) without a synchronisation of its own
     uint32_t* h_ctl = nullptr;
+    float* d_rad = nullptr;  // radiance of finished wavefront paths (ensure_rad)
+    uint64_t rad_cap = 0;
+    float* d_peer = nullptr;  // pt_render_multi (ordered reduction): another device's partial accumulator
+    size_t peer_cap = 0;
 };
 
 // Set once any call of this library has touched the HIP runtime (pt_set_hw_queues is then too late).
@@ -527,6 +536,12 @@ void pt_scene_destroy(pt_scene* s) {
         if (h < 2 && s->ws.traced[h]) hipEventDestroy(s->ws.traced[h]);
     }
     if (s->ws.fork) hipEventDestroy(s->ws.fork);
+    for (int h = 0; h < kMaxParts; ++h)
+        for (int k = 0; k < 2; ++k)
+            if (s->ws.poll_ev[h][k]) hipEventDestroy(s->ws.poll_ev[h][k]);
+    if (s->ws.h_poll) hipHostFree(s->ws.h_poll);
+    if (s->d_rad) hipFree(s->d_rad);
+    if (s->d_peer) hipFree(s->d_peer);
     if (s->d_rgba) hipFree(s->d_rgba);
     if (s->h_ctl) hipHostFree(s->h_ctl);
     if (s->d_mem) hipFree(s->d_mem);
@@ -601,6 +616,8 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_FUSE")) lo.fuse = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_BF")) lo.bf = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_MAILBOX")) lo.mailbox = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_REGEN")) lo.regen = std::strcmp(e, "0") != 0 ? 1 : 0;
+    if (const char* e = std::getenv("PT_REGEN_TARGET")) lo.regen_target = std::atol(e);
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
     return lo;
 }
@@ -608,6 +625,24 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
 // paths in flight per wavefront batch (kWfBytesPerPath = 188 B of queue state per path: 8 M
 // paths ~ 1.6 GB, plus the queue slack of the region layout)
 constexpr uint64_t kWfTargetPaths = 8ull << 20;
+
+// radiance of finished paths: the batch's (capacity), or with streaming regeneration a whole
+// group of frames, up to kRadMaxPaths (12 B per path: 3.2 GB)
+constexpr uint64_t kRadMaxPaths = 1ull << 28;
+
+int ensure_rad(pt_scene* s, uint64_t paths) {
+    if (s->d_rad && s->rad_cap >= paths) { s->wf.rad = s->d_rad; s->wf.rad_cap = s->rad_cap; return PT_OK; }
+    if (s->d_rad) { hipDeviceSynchronize(); hipFree(s->d_rad); s->d_rad = nullptr; s->rad_cap = 0; }
+    if (hipMalloc(&s->d_rad, 12 * paths) != hipSuccess) {
+        s->d_rad = nullptr;
+        (void)hipGetLastError();
+        return fail(PT_ERR_NOMEM, "hipMalloc wavefront radiance");
+    }
+    s->rad_cap = paths;
+    s->wf.rad = s->d_rad;
+    s->wf.rad_cap = paths;
+    return PT_OK;
+}
 
 int ensure_wavefront(pt_scene* s, uint64_t paths) {
     if (s->d_wf && s->wf.capacity >= paths) return PT_OK;
@@ -623,8 +658,9 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     size_t oq[6];
     for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * qn);
     const size_t o_p0 = take(16 * qn), o_p1 = take(16 * qn), o_p2 = take(8 * qn), o_hit = take(8 * qn),
-                 o_rad = take(12 * n), o_ctl = take(4 * kMaxParts * WF_CTL_WORDS),
-                 o_rcnt = take(4 * kMaxParts * 3 * kRegions);
+                 o_ctl = take(4 * kMaxParts * WF_CTL_WORDS), o_rcnt = take(4 * kMaxParts * 3 * kRegions),
+                 o_rgen = take(4 * kMaxParts * 2 * kRegions), o_live = take(4 * kMaxParts * kLiveRing),
+                 o_fetch = take(4 * kMaxParts * 3 * kRegions * kFetchStride);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) {
         s->d_wf = nullptr;
         (void)hipGetLastError();  // the failed allocation is reported here, not by a later call
@@ -638,9 +674,11 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     w.sp0 = f4(o_p0); w.sp1 = f4(o_p1);
     w.sp2 = reinterpret_cast<float2*>(b + o_p2);
     w.hitq = reinterpret_cast<int2*>(b + o_hit);
-    w.rad = reinterpret_cast<float*>(b + o_rad);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
     w.rcnt = reinterpret_cast<uint32_t*>(b + o_rcnt);
+    w.rgen = reinterpret_cast<uint32_t*>(b + o_rgen);
+    w.live = reinterpret_cast<uint32_t*>(b + o_live);
+    w.rfetch = reinterpret_cast<uint32_t*>(b + o_fetch);
     if (hipMemset(w.ctl, 0, 4 * kMaxParts * WF_CTL_WORDS) != hipSuccess ||
         hipMemset(w.rcnt, 0, 4 * kMaxParts * 3 * kRegions) != hipSuccess)
         return fail(PT_ERR_HIP, "hipMemset wavefront control words");
@@ -650,6 +688,10 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
             ok = hipStreamCreateWithFlags(&s->ws.aux[h], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&s->ws.join[h], hipEventDisableTiming) == hipSuccess;
         for (int h = 0; h < 2 && ok; ++h) ok = hipEventCreateWithFlags(&s->ws.traced[h], hipEventDisableTiming) == hipSuccess;
+        for (int h = 0; h < kMaxParts && ok; ++h)
+            for (int k = 0; k < 2 && ok; ++k)
+                ok = hipEventCreateWithFlags(&s->ws.poll_ev[h][k], hipEventDisableTiming) == hipSuccess;
+        if (ok) ok = hipHostMalloc(reinterpret_cast<void**>(&s->ws.h_poll), 2 * kMaxParts * sizeof(uint32_t)) == hipSuccess;
         if (!ok) return fail(PT_ERR_HIP, "creating the wavefront's streams");
     }
     if (!s->h_ctl) {
@@ -661,6 +703,8 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     }
     w.capacity = (uint32_t)n;
     w.qcap = (uint32_t)qn;
+    w.rad = s->d_rad;
+    w.rad_cap = s->rad_cap;
     return PT_OK;
 }
 
@@ -721,6 +765,11 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         // the two-frame minimum doubles the state of images above the batch target (~188 B/path):
         // fall back to one frame per batch when that does not fit
         if (rc2 == PT_ERR_NOMEM && want > std::min<uint64_t>(all, npix)) rc2 = ensure_wavefront(s, std::min<uint64_t>(all, npix));
+        if (rc2 != PT_OK) return rc2;
+        // radiance: the batch's paths, or (regeneration) the call's frames up to kRadMaxPaths, whole frames
+        const uint64_t rad_want = std::max<uint64_t>(s->wf.capacity, std::min<uint64_t>(all, std::max<uint64_t>(npix, kRadMaxPaths / npix * npix)));
+        rc2 = ensure_rad(s, rad_want);
+        if (rc2 == PT_ERR_NOMEM && rad_want > s->wf.capacity) rc2 = ensure_rad(s, s->wf.capacity);
         if (rc2 != PT_OK) return rc2;
         HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
                                  stream, s->ws));
@@ -919,4 +968,170 @@ int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, u
     return PT_OK;
 }
 
+
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Multi-GPU (pt_render_multi): one host thread per device renders its frames, then ONE reduction
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct RcclApi {
+    bool ok = false;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+std::mutex g_rccl_mu;
+
+// librccl: the copy already in the process (e.g. torch's) if there is one, else the system's
+const RcclApi& rccl_api() {
+    static RcclApi a;
+    static bool tried = false;
+    if (tried) return a;
+    tried = true;
+    void* h = nullptr;
+    for (const char* n : {"librccl.so.1", "librccl.so"})
+        if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD))) break;
+    for (const char* n : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
+        if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return a;
+    a.comm_init_all = reinterpret_cast<decltype(a.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    a.reduce = reinterpret_cast<decltype(a.reduce)>(dlsym(h, "ncclReduce"));
+    a.group_start = reinterpret_cast<decltype(a.group_start)>(dlsym(h, "ncclGroupStart"));
+    a.group_end = reinterpret_cast<decltype(a.group_end)>(dlsym(h, "ncclGroupEnd"));
+    a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
+    a.ok = a.comm_init_all && a.reduce && a.group_start && a.group_end && a.error_string;
+    return a;
+}
+
+// one communicator set per device list, made on first use and kept for the process
+std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+
+int rccl_reduce(pt_scene* const* sc, int n, size_t count) {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    const RcclApi& a = rccl_api();
+    std::vector<int> devs(n);
+    for (int g = 0; g < n; ++g) devs[g] = sc[g]->device;
+    auto it = g_comms.find(devs);
+    if (it == g_comms.end()) {
+        std::vector<ncclComm_t> c(n);
+        const ncclResult_t r = a.comm_init_all(c.data(), n, devs.data());
+        if (r != ncclSuccess) return fail(PT_ERR_HIP, std::string("ncclCommInitAll: ") + a.error_string(r));
+        it = g_comms.emplace(devs, c).first;
+    }
+    ncclResult_t r = a.group_start();
+    for (int g = 0; g < n && r == ncclSuccess; ++g) {
+        HIP_TRY(hipSetDevice(sc[g]->device));
+        r = a.reduce(sc[g]->d_accum, sc[g]->d_accum, count, ncclFloat32, ncclSum, 0, it->second[g], sc[g]->stream);
+    }
+    const ncclResult_t r2 = a.group_end();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return fail(PT_ERR_HIP, std::string("ncclReduce: ") + a.error_string(r != ncclSuccess ? r : r2));
+    for (int g = 0; g < n; ++g) {
+        HIP_TRY(hipSetDevice(sc[g]->device));
+        HIP_TRY(hipStreamSynchronize(sc[g]->stream));
+    }
+    return PT_OK;
+}
+
+// device order: partials of scenes 1..n-1 copied to device 0 and added there one after another
+int ordered_reduce(pt_scene* const* sc, int n, size_t count) {
+    pt_scene* s0 = sc[0];
+    HIP_TRY(hipSetDevice(s0->device));
+    if (s0->peer_cap < count) {
+        if (s0->d_peer) hipFree(s0->d_peer);
+        s0->d_peer = nullptr;
+        s0->peer_cap = 0;
+        if (hipMalloc(&s0->d_peer, count * sizeof(float)) != hipSuccess) return fail(PT_ERR_NOMEM, "hipMalloc peer accumulator");
+        s0->peer_cap = count;
+    }
+    for (int g = 1; g < n; ++g) {
+        if (sc[g]->device == s0->device)
+            HIP_TRY(launch_accum_add(s0->d_accum, sc[g]->d_accum, count, s0->stream));
+        else {
+            HIP_TRY(hipMemcpyPeerAsync(s0->d_peer, s0->device, sc[g]->d_accum, sc[g]->device, count * sizeof(float),
+                                       s0->stream));
+            HIP_TRY(launch_accum_add(s0->d_accum, s0->d_peer, count, s0->stream));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s0->stream));
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" int pt_render_multi(pt_scene* const* scenes, int n, const float meta[48], uint32_t frame0, uint32_t nframes,
+                               uint32_t frame_stride, int max_depth, int mode, float* accum, pt_counters* counters) {
+    if (!scenes || n < 1 || n > 64 || !meta || !accum) return fail(PT_ERR_INVALID, "bad argument");
+    for (int g = 0; g < n; ++g)
+        for (int h = 0; h < g; ++h)
+            if (!scenes[g] || scenes[g] == scenes[h]) return fail(PT_ERR_INVALID, "null or repeated scene");
+    if (!scenes[0]) return fail(PT_ERR_INVALID, "null scene");
+    if (n == 1) return pt_render(scenes[0], meta, frame0, nframes, frame_stride, max_depth, mode, accum, counters);
+    FrameParams fp;
+    int rc = make_params(meta, max_depth, fp);
+    if (rc != PT_OK) return rc;
+    if ((uint64_t)frame0 + (uint64_t)(nframes ? nframes - 1 : 0) * frame_stride >= (1ull << 24))
+        return fail(PT_ERR_INVALID, "frame index >= 2^24 (t_k = u32(f32(k)) would round)");
+    const size_t count = (size_t)fp.width * fp.height * 3;
+    bool distinct = true;
+    for (int g = 0; g < n; ++g)
+        for (int h = 0; h < g; ++h) distinct &= scenes[g]->device != scenes[h]->device;
+    const char* red = std::getenv("PT_REDUCE");
+    const bool want_rccl = !(red && !std::strcmp(red, "ordered"));
+    if (red && std::strcmp(red, "ordered") && std::strcmp(red, "rccl")) return fail(PT_ERR_INVALID, "PT_REDUCE: rccl|ordered");
+    if (red && !std::strcmp(red, "rccl") && (!distinct || !rccl_api().ok))
+        return fail(PT_ERR_INVALID, "PT_REDUCE=rccl needs distinct devices and librccl.so.1");
+    const bool use_rccl = want_rccl && distinct && rccl_api().ok;
+    for (int g = 0; g < n; ++g) {  // accumulators: scenes[0]'s from accum, the others zero
+        pt_scene* s = scenes[g];
+        HIP_TRY(hipSetDevice(s->device));
+        if ((rc = ensure_accum(s, count)) != PT_OK || (rc = blocking_stream(s)) != PT_OK) return rc;
+        if (g == 0) HIP_TRY(hipMemcpyAsync(s->d_accum, accum, count * sizeof(float), hipMemcpyHostToDevice, s->stream));
+        else HIP_TRY(hipMemsetAsync(s->d_accum, 0, count * sizeof(float), s->stream));
+        if (counters) HIP_TRY(hipMemsetAsync(s->d_counters, 0, sizeof(Counters), s->stream));
+    }
+    // frames i = g, g + n, ... on scene g, each device on a host thread of its own (the wavefront's
+    // host loop waits on its device; one thread would serialise the devices)
+    std::vector<int> rcs(n, PT_OK);
+    std::vector<std::string> errs(n);
+    std::vector<std::thread> th;
+    for (int g = 0; g < n; ++g)
+        th.emplace_back([&, g]() {
+            pt_scene* s = scenes[g];
+            const uint32_t cnt = nframes > (uint32_t)g ? (nframes - (uint32_t)g + (uint32_t)n - 1) / (uint32_t)n : 0u;
+            int r = hipSetDevice(s->device) == hipSuccess ? PT_OK : fail(PT_ERR_HIP, "hipSetDevice");
+            if (r == PT_OK)
+                r = render_impl(s, meta, frame0 + (uint32_t)g * frame_stride, cnt, (uint32_t)n * frame_stride, max_depth,
+                                mode, true, s->d_accum, counters ? s->d_counters : nullptr, s->stream);
+            if (r == PT_OK && hipStreamSynchronize(s->stream) != hipSuccess) r = fail(PT_ERR_HIP, "render stream");
+            if (r == PT_OK) r = check_watchdog(s);
+            rcs[g] = r;
+            if (r != PT_OK) errs[g] = pt_last_error();
+        });
+    for (auto& t : th) t.join();
+    for (int g = 0; g < n; ++g)
+        if (rcs[g] != PT_OK) return fail(rcs[g], "device " + std::to_string(scenes[g]->device) + ": " + errs[g]);
+    rc = use_rccl ? rccl_reduce(scenes, n, count) : ordered_reduce(scenes, n, count);
+    if (rc != PT_OK) return rc;
+    pt_scene* s0 = scenes[0];
+    HIP_TRY(hipSetDevice(s0->device));
+    HIP_TRY(hipMemcpyAsync(accum, s0->d_accum, count * sizeof(float), hipMemcpyDeviceToHost, s0->stream));
+    HIP_TRY(hipStreamSynchronize(s0->stream));
+    if (counters) {
+        pt_counters sum{};
+        for (int g = 0; g < n; ++g) {
+            pt_counters c{};
+            HIP_TRY(hipSetDevice(scenes[g]->device));
+            HIP_TRY(hipMemcpy(&c, scenes[g]->d_counters, sizeof c, hipMemcpyDeviceToHost));
+            sum.samples += c.samples; sum.ext_queries += c.ext_queries; sum.shadow_queries += c.shadow_queries;
+            sum.nodes += c.nodes; sum.tri_tests += c.tri_tests; sum.box_tests += c.box_tests;
+        }
+        *counters = sum;
+    }
+    return PT_OK;
+}

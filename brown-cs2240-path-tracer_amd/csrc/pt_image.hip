@@ -6,6 +6,8 @@
 // (pt_capi.hip); the GPU test checks the two byte for byte.
 #include "pt_kernels.h"
 
+#include <algorithm>
+
 namespace pt {
 
 __device__ __forceinline__ int32_t to_int32(double v) {  // ECMAScript ToInt32
@@ -31,6 +33,32 @@ hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t*
     if (npix == 0) return hipSuccess;
     PT_LAUNCH(KID_TONEMAP, stream, k_tonemap, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, acc, npix,
               runs, reinterpret_cast<uchar4*>(rgba));
+    return hipGetLastError();
+}
+
+// dst += src, f32, element-wise (the ordered multi-device reduction of pt_render_multi: partial
+// accumulators added onto device 0's in device order)
+__global__ __launch_bounds__(256) void k_accum_add(float4* __restrict__ dst, const float4* __restrict__ src, size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        float4 a = dst[i];
+        const float4 b = src[i];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        dst[i] = a;
+    }
+}
+__global__ void k_accum_add_tail(float* __restrict__ dst, const float* __restrict__ src, size_t from, size_t n) {
+    const size_t i = from + threadIdx.x;
+    if (i < n) dst[i] += src[i];
+}
+
+hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t stream) {
+    const size_t n4 = n / 4;
+    if (n4) {
+        const unsigned blocks = (unsigned)std::min<size_t>((n4 + 255) / 256, 8192);
+        hipLaunchKernelGGL(k_accum_add, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<float4*>(dst),
+                           reinterpret_cast<const float4*>(src), n4);
+    }
+    if (n % 4) hipLaunchKernelGGL(k_accum_add_tail, dim3(1), dim3(4), 0, stream, dst, src, n4 * 4, n);
     return hipGetLastError();
 }
 

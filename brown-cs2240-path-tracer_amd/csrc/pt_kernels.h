@@ -71,6 +71,8 @@ struct LaunchOpts {
     int regen_bf = -1;     // megakernel with brute-force + replay on mailbox scenes: -1 default (off)
     int persist = -1;      // fused bf as one workgroup-local launch per batch (k_wf_persist_bf): -1 default (off)
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
+    int regen = -1;        // fused kernel: streaming path regeneration (every extension launch refills): -1 default (off)
+    long regen_target = 0; // paths in flight per part with regeneration (0 = the batch capacity)
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -107,7 +109,18 @@ struct WfBuffers {
     uint32_t* rcnt;
     uint32_t rstride;
     uint32_t nreg;
+    // streaming path regeneration (k_wf_step_bf<..., REGEN>): every extension launch tops each
+    // region up to `target` entries with new camera paths of the region's share of the render;
+    // rgen[slot * kRegions + r] = camera batches of region r made so far (two slots, alternating
+    // by extension launch), live[it % kLiveRing] = regions with work in launch it (host polling)
+    uint32_t* rgen;
+    uint32_t* live;
+    uint32_t* rfetch;   // k_wf_regen_bf: per launch slot (3) and region, the region's next batch (kFetchStride apart)
+    uint32_t target;
+    uint64_t rad_cap;   // paths whose radiance `rad` holds (>= capacity; regeneration: a whole group of frames)
 };
+constexpr uint32_t kLiveRing = 64;
+constexpr uint32_t kFetchStride = 32;  // u32 between two regions' fetch counters: 128 B
 constexpr uint32_t kRegions = 512;
 // queue slack (entries per half = 64 * this): regions of R <= 2/3 of it hold ceil(batches / R)
 // 64-entry batches each (k_wf_persist_bf uses one region per workgroup, at most kPersistMaxBlocks)
@@ -126,6 +139,11 @@ struct WfStreams {
     bool stagger = false;
     bool fuse_gen = true;  // LaunchOpts::fuse_gen
     int nparts = 2;
+    bool regen = true;     // LaunchOpts::regen
+    uint32_t regen_target = 0;  // LaunchOpts::regen_target (paths in flight per part; 0 = the queue capacity)
+    // host polling of the regeneration loop: pinned words (2 per part) and their events
+    uint32_t* h_poll = nullptr;
+    hipEvent_t poll_ev[kMaxParts][2] = {};
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
@@ -144,6 +162,8 @@ hipError_t launch_regen_bf(const LaunchOpts& lo, const SceneView& sc, const Fram
 
 // display transform of program-raymarch.ts:295-316 on device (pt_image.hip)
 hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t* rgba, hipStream_t stream);
+// dst[i] += src[i] for i < n (f32; both on the stream's device; pt_image.hip)
+hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t stream);
 
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);

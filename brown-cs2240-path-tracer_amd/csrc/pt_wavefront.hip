@@ -282,6 +282,10 @@ __device__ __forceinline__ uint64_t phase_clock() {
 constexpr bool kBfScalarPrefetch = false;  // phase 1: next record's s_load in flight during a test (measured -2 %)
 constexpr bool kBfPrefetch = true;  // bf_step_batch loads q2/q3 before the trace
 
+__device__ __forceinline__ uint32_t sload_u32(const uint32_t* p) {  // uniform address: s_load
+    return *(const __attribute__((address_space(4))) uint32_t*)p;
+}
+
 __device__ __forceinline__ TriRec load_tri_scalar(const Tri* tris, int i) {
     // uniform index: constant address space, so the record comes through s_load (no VGPRs)
     const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(tris + i);
@@ -560,28 +564,32 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
 // instead of read from the queue — path p = (b * R + region) * 64 + lane, k_wf_generate's
 // layout — and packed into the very words store_entry would have written, so everything after
 // reads the same bits as from the queue (the queue write and read of the camera rays saved).
+// Camera batches: region rg's k-th camera batch is the 64 paths (k * R + rg) * 64 + lane < P.
 struct GenArgs {
-    uint32_t frame0, stride, fbase, R, rg;
+    uint32_t frame0, stride, fbase, R, rg, P;
     bool raw_salt;
 };
+// genk (GEN instances; wave-uniform): >= 0 makes this batch camera batch genk of the region
+// instead of queue batch b (streaming regeneration and the first launch); -1 reads the queue.
 template <bool EXT, bool FAST_RCP, bool COUNT, bool GEN = false, class Append>
 __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gtris, const FrameParams& fp,
                                               const WfBuffers& wb, size_t rbase, uint32_t b, uint32_t count,
                                               const BfLds& l, int nslots, Counters& c, Append append,
                                               bool cull = false,  // cull: wave-uniform (bf_cull_mask)
-                                              const GenArgs& gen = GenArgs{}) {
+                                              const GenArgs& gen = GenArgs{}, int64_t genk = -1) {
     const WfQueue& in = EXT ? wb.ext : wb.shd;
     const WfQueue& out = EXT ? wb.shd : wb.ext;
     const uint32_t lane = lane_id();
     uint64_t tm[6];
     if (PT_PHASE_TIMING) tm[0] = phase_clock();
-    const bool valid = b * 64 + lane < count;
-    const size_t e = rbase + (valid ? b * 64 + lane : 0);
+    const bool fresh = GEN && genk >= 0;
+    const uint32_t pg = fresh ? ((uint32_t)genk * gen.R + gen.rg) * 64 + lane : 0u;
+    const bool valid = fresh ? pg < gen.P : b * 64 + lane < count;
+    const size_t e = rbase + ((valid && !fresh) ? b * 64 + lane : 0);
     float4 a0 = make_float4(0, 0, 0, 1), a1 = make_float4(0, 0, 0, 0);
     float4 c2 = make_float4(0, 0, 0, 0), d3 = c2;
-    if constexpr (GEN) {
+    if (fresh) {
         if (valid) {
-            const uint32_t pg = (b * gen.R + gen.rg) * 64 + lane;
             uint32_t x, y, f;
             path_pixel(pg, fp.width * fp.height, fp.width, x, y, f);
             const uint32_t tt = gen.raw_salt ? gen.frame0 : (uint32_t)(float)(gen.frame0 + (gen.fbase + f) * gen.stride);
@@ -602,7 +610,7 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     Ray r = unpack_ray(a0, a1, p);
     const uint64_t todo = cull ? bf_cull_mask(sc, r, valid, sc.n_tris - sc.mb_base) : ~0ull;  // before the prefetch: fewer live VGPRs
     // the path state is loaded before the trace and arrives while it runs (kBfPrefetch)
-    if (!GEN && kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
+    if (!fresh && kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
     float t;
     if (PT_PHASE_TIMING) tm[1] = phase_clock();
     const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t, todo,
@@ -611,7 +619,7 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     bool more = false;
     PathState ps;
     if (valid) {
-        if (!GEN && !kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
+        if (!fresh && !kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
         unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
         ps.L = mk(c2.x, c2.y, c2.z);
         ps.seed = __builtin_bit_cast(uint32_t, c2.w);
@@ -654,14 +662,14 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
 }
 
 // Trace + shade in one launch per iteration (mailbox scenes; PT_PERSIST=0): queues are cut
-// into wb.nreg regions (k_wf_generate deals 64-path batches round-robin); the waves w ≡ r (mod
-// nreg) serve region r of the input and append to region r of the output, one atomicAdd per
-// wave and batch on that region's counter (a counter shared by all waves serialises at one
-// memory channel, and each wave waits for its add: measured 2x slower).  A region's output
-// never exceeds its input, so every region holds its paths through all bounces.  Iteration
-// `it` reads the counts of slot it % 3, appends to slot (it + 1) % 3 and zeroes slot
-// (it + 2) % 3 for iteration it + 1 (iteration it - 1 read that slot and it - 2 wrote it, both
-// finished: stream order).
+// into wb.nreg regions (64-path batches dealt round-robin: camera batch j to region j mod nreg);
+// the waves w ≡ r (mod nreg) serve region r of the input and append to region r of the output,
+// one atomicAdd per wave and batch on that region's counter (a counter shared by all waves
+// serialises at one memory channel, and each wave waits for its add: measured 2x slower).  A
+// region's output never exceeds its input, so every region holds its paths through all
+// bounces.  Iteration `it` reads the counts of slot it % 3, appends to slot (it + 1) % 3 and
+// zeroes slot (it + 2) % 3 for iteration it + 1 (iteration it - 1 read that slot and it - 2
+// wrote it, both finished: stream order).
 // amdgpu_waves_per_eu(8): the path logic pushed the kernel to 75 VGPRs (6 waves/SIMD); capped
 // at 64 it keeps 8 waves/SIMD with no VGPR spills (a few SGPR spills to VGPR lanes): +7 %
 // CULL: the entry cull (bf_cull_mask) — its own instance, so the launches without it keep
@@ -679,25 +687,92 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     const uint32_t R = wb.nreg;  // <= nwaves (host)
     const uint32_t rg = w % R, g = w / R, G = (nwaves - rg + R - 1) / R;
     if (g == 0 && lane_id() == 0) wb.rcnt[((it + 2) % 3) * kRegions + rg] = 0;
-    uint32_t count;
+    const uint32_t nbat = (P + 63) / 64;
+    const uint32_t ncam = rg < nbat ? (nbat - rg + R - 1) / R : 0u;  // camera batches of region rg
+    uint32_t count, nqb, nnew = 0;
     if constexpr (GEN) {  // k_wf_generate's closed-form count of region rg
-        const uint32_t nbat = (P + 63) / 64;
-        const uint32_t n = rg < nbat ? (nbat - rg + R - 1) / R : 0u;
-        const uint32_t last = rg + (n - 1) * R;
-        count = n == 0 ? 0u : n * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
+        const uint32_t last = rg + (ncam - 1) * R;
+        count = ncam == 0 ? 0u : ncam * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
         if (w == 0 && lane_id() == 0) { wb.ctl[WF_COUNT0] = P; wb.ctl[WF_COUNT1] = 0; }
+        nqb = 0;
+        nnew = ncam;
     } else {
         count = wb.rcnt[(it % 3) * kRegions + rg];
+        nqb = (count + 63) / 64;
     }
     uint32_t* out_count = &wb.rcnt[((it + 1) % 3) * kRegions + rg];
     const Tri* gtris = sc.tris;  // global records for phase 1
     if (LDS) stage_scene_lds(sc, l.scene);
-    const uint32_t nb = (count + 63) / 64;
-    const GenArgs ga{frame0, stride, fbase, R, rg, raw_salt};
+    const uint32_t nb = nqb + nnew;
+    const GenArgs ga{frame0, stride, fbase, R, rg, P, raw_salt};
     Counters c = {};
     for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves
         bf_step_batch<EXT, FAST_RCP, COUNT, GEN>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
-                                                 [&](uint32_t n) { return atomicAdd(out_count, n); }, CULL, ga);
+                                                 [&](uint32_t n) { return atomicAdd(out_count, n); }, CULL, ga,
+                                                 b < nqb ? (int64_t)-1 : (int64_t)(b - nqb));
+    if (COUNT) flush_counters(c, cnt_out);
+}
+
+// Streaming path regeneration (the default for the fused kernel): the render's P paths are the
+// camera batches of the regions (camera batch k of region r: paths (k R + r) 64 + lane).  Every
+// extension launch e = it / 2 tops region r up from its queued count c to wb.target entries with
+// the region's next camera batches: after the c queued entries come batches rgen[e % 2][r] ..
+// + n_new, made in registers by the wave that traces them (no queue write or read of camera rays),
+// and the region's cursor moves to slot (e + 1) % 2.  So the queues stay full until the camera
+// batches run out — one per-bounce tail at the end of the render instead of one per batch of
+// frames.  Each path writes its radiance to rad[p] when it ends; k_wf_accum adds them in frame
+// order afterwards, so the result is bit-identical.
+// Scheduling: region r is served by the waves w ≡ r (mod R) (with 8 waves per block and
+// R = 512 all of them sit in blocks b ≡ b0 (mod 64), so on one XCD when the dispatcher deals
+// blocks round-robin to the 8 XCDs: a region's queue and path state stay in one L2), and those
+// waves take the region's batches from the region's counter rfetch[it % 3][r] (one cache line
+// per region: device-scope atomics on one line serialise at ~12 ns each) instead of a static
+// interleave: a static split of ~16 batches per wave left the slowest of 8192 waves ~25 % behind
+// the mean at every launch.  A wave fetches its next batch while it works on the current one.
+// Wave g == 0 of each region keeps its books: the next launch's count and fetch slots zeroed,
+// the camera cursor, and live[it % kLiveRing] = regions with work left (queued entries or camera
+// batches); the host stops launching when a launch saw none.
+template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_wf_regen_bf(
+    SceneView sc, FrameParams fp, WfBuffers wb, int it, Counters* cnt_out, int nslots, uint32_t frame0,
+    uint32_t stride, uint32_t fbase, uint32_t P, bool raw_salt) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const BfLds l = bf_lds(smem, sc);
+    const uint32_t lane = lane_id();
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    const uint32_t R = wb.nreg;  // <= waves (host)
+    const uint32_t rg = w % R, g = w / R;
+    const uint32_t e = (uint32_t)it / 2;
+    const uint32_t nbat = (P + 63) / 64;
+    const uint32_t ncam = rg < nbat ? (nbat - rg + R - 1) / R : 0u;  // camera batches of region rg
+    const uint32_t count = wb.rcnt[(it % 3) * kRegions + rg];
+    const uint32_t k0 = wb.rgen[((EXT ? e : e + 1) % 2) * kRegions + rg];
+    const uint32_t nnew = EXT && wb.target > count ? min((wb.target - count) / 64, ncam - k0) : 0u;
+    const uint32_t nqb = (count + 63) / 64, nb = nqb + nnew;
+    if (g == 0 && lane == 0) {  // region rg's books
+        wb.rcnt[((it + 2) % 3) * kRegions + rg] = 0;
+        wb.rfetch[(((it + 2) % 3) * kRegions + rg) * kFetchStride] = 0;
+        if (EXT) wb.rgen[((e + 1) % 2) * kRegions + rg] = k0 + nnew;
+        if (count > 0 || k0 < ncam) atomicAdd(&wb.live[it % kLiveRing], 1u);
+        if (rg == 0) wb.live[(it + 2) % kLiveRing] = 0;
+    }
+    uint32_t* out_count = &wb.rcnt[((it + 1) % 3) * kRegions + rg];
+    uint32_t* fetch = &wb.rfetch[((it % 3) * kRegions + rg) * kFetchStride];
+    const Tri* gtris = sc.tris;  // global records for phase 1
+    if (LDS) stage_scene_lds(sc, l.scene);
+    const GenArgs ga{frame0, stride, fbase, R, rg, P, raw_salt};
+    Counters c = {};
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(fetch, 1u);
+    b = __builtin_amdgcn_readfirstlane(b);
+    while (b < nb) {
+        uint32_t bn = 0;
+        if (lane == 0) bn = atomicAdd(fetch, 1u);  // the next batch, in flight while this one runs
+        bf_step_batch<EXT, FAST_RCP, COUNT, EXT>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
+                                                 [&](uint32_t n) { return atomicAdd(out_count, n); }, false, ga,
+                                                 b < nqb ? (int64_t)-1 : (int64_t)(k0 + (b - nqb)));
+        b = __builtin_amdgcn_readfirstlane(bn);
+    }
     if (COUNT) flush_counters(c, cnt_out);
 }
 
@@ -980,9 +1055,109 @@ static WfBuffers wb_part(const WfBuffers& wb, int h, int nparts, size_t rad_off)
     v.rad += rad_off;
     v.ctl += h * WF_CTL_WORDS;
     v.rcnt += h * 3 * kRegions;
+    v.rgen += h * 2 * kRegions;
+    v.live += h * kLiveRing;
+    v.rfetch += h * 3 * kRegions * kFetchStride;
     v.capacity = wb.capacity / nparts;
     v.qcap = wb.qcap / nparts;
     return v;
+}
+
+// Streaming regeneration (k_wf_regen_bf): the call's frames in groups whose radiance
+// fits wb.rad_cap paths; a group's frames are dealt to the parts in contiguous runs, each part on
+// its own stream runs extension / shadow launches until a launch finds no work left in any
+// region (the host polls live[] every kPollChunk launches through pinned memory, one chunk
+// ahead, so the stream never waits for the host), then k_wf_accum adds the group's frames in
+// order.
+constexpr int kPollChunk = 8;
+template <bool LDS, int TRAV, bool COUNT>
+static hipError_t wf_render_regen(const SceneView& sc, const FrameParams& fp, const WfBuffers& wb, uint32_t frame0,
+                                  uint32_t nframes, uint32_t stride, bool accum, float* out, Counters* cnt,
+                                  hipStream_t stream, const WfStreams& ws, int tblocks, size_t lds, int bf_slots) {
+    constexpr bool rcp = ((TRAV / 10) & 1) != 0;
+    const uint32_t npix = fp.width * fp.height;
+    const int np = (ws.aux[0] != nullptr && ws.h_poll) ? ws.nparts : 1;
+    const uint32_t Fs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nframes, wb.rad_cap / npix));
+    const uint32_t R = std::min<uint32_t>(kRegions, (uint32_t)tblocks * (kTraceBlock / 64));
+    for (uint32_t fb = 0; fb < nframes; fb += Fs) {
+        const uint32_t Fb = std::min(Fs, nframes - fb);
+        const int nh = (int)std::min<uint32_t>((uint32_t)np, Fb);
+        struct Part { WfBuffers w; uint32_t fbase, P, ncam_max; hipStream_t st; int it, chunk; bool done; };
+        Part pv[kMaxParts];
+        uint32_t f0 = 0;
+        for (int h = 0; h < nh; ++h) {
+            const uint32_t fh = (Fb - f0 + (nh - h) - 1) / (nh - h);  // frames left over parts left
+            Part& q = pv[h];
+            q.w = np > 1 ? wb_part(wb, h, np, (size_t)f0 * npix * 3) : wb;
+            q.fbase = fb + f0;
+            q.P = fh * npix;
+            q.st = np > 1 ? ws.aux[h] : stream;
+            q.w.nreg = R;
+            q.w.rstride = q.w.qcap / R / 64 * 64;  // >= capacity / R (queue slack)
+            uint64_t T = q.w.capacity;
+            if (ws.regen_target) T = std::min<uint64_t>(T, ws.regen_target / (uint64_t)nh);
+            q.w.target = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(64, T / R / 64 * 64), q.w.rstride);
+            const uint32_t nbat = (q.P + 63) / 64;
+            q.ncam_max = (nbat + R - 1) / R;
+            q.it = 0;
+            q.chunk = 0;
+            q.done = false;
+            f0 += fh;
+        }
+        if (np > 1) {
+            HIP_RETURN_IF(hipEventRecord(ws.fork, stream));
+            for (int h = 0; h < nh; ++h) HIP_RETURN_IF(hipStreamWaitEvent(pv[h].st, ws.fork, 0));
+        }
+        for (int h = 0; h < nh; ++h) {  // counts of launches 0 (read) and 1 (appended), camera cursors, liveness
+            HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rcnt, 0, 2 * kRegions * sizeof(uint32_t), pv[h].st));
+            HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rgen, 0, kRegions * sizeof(uint32_t), pv[h].st));
+            HIP_RETURN_IF(hipMemsetAsync(pv[h].w.live, 0, kLiveRing * sizeof(uint32_t), pv[h].st));
+            HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rfetch, 0, 2 * kRegions * kFetchStride * sizeof(uint32_t), pv[h].st));
+        }
+        // a hard bound on the launches (every path at most 2 (D + 1) launches; a region makes at
+        // least one camera batch per extension launch while it has room): a bug, never a hang
+        int left = nh;
+        while (left > 0) {
+            for (int h = 0; h < nh; ++h) {
+                Part& q = pv[h];
+                if (q.done) continue;
+                const int cap = 2 * (fp.max_depth + 1) * ((int)q.ncam_max + 2) + 64;
+                if (q.it > cap) return hipErrorLaunchFailure;
+                for (int k = 0; k < kPollChunk; ++k, ++q.it) {
+#define PT_RSTEP(E) PT_LAUNCH(KID_WF_STEP, q.st, (k_wf_regen_bf<E, LDS, rcp, COUNT>), dim3(tblocks), \
+                              dim3(kTraceBlock), lds, q.st, sc, fp, q.w, q.it, cnt, bf_slots, frame0, stride, q.fbase, \
+                              q.P, !accum)
+                    if ((q.it & 1) == 0) PT_RSTEP(true);
+                    else PT_RSTEP(false);
+#undef PT_RSTEP
+                }
+                const int slot = q.chunk & 1;
+                HIP_RETURN_IF(hipMemcpyAsync(&ws.h_poll[2 * h + slot], q.w.live + (q.it - 1) % kLiveRing, sizeof(uint32_t),
+                                             hipMemcpyDeviceToHost, q.st));
+                HIP_RETURN_IF(hipEventRecord(ws.poll_ev[h][slot], q.st));
+                ++q.chunk;
+            }
+            for (int h = 0; h < nh; ++h) {  // the chunk before the one just queued: did its last launch find work?
+                Part& q = pv[h];
+                if (q.done || q.chunk < 2) continue;
+                const int slot = (q.chunk - 2) & 1;
+                HIP_RETURN_IF(hipEventSynchronize(ws.poll_ev[h][slot]));
+                if (__atomic_load_n(&ws.h_poll[2 * h + slot], __ATOMIC_ACQUIRE) == 0) {
+                    q.done = true;
+                    --left;
+                }
+            }
+        }
+        if (np > 1) {
+            for (int h = 0; h < nh; ++h) {
+                HIP_RETURN_IF(hipEventRecord(ws.join[h], pv[h].st));
+                HIP_RETURN_IF(hipStreamWaitEvent(stream, ws.join[h], 0));
+            }
+        }
+        PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix, Fb,
+                  accum);
+    }
+    return hipGetLastError();
 }
 
 template <bool LDS, int TRAV, bool COUNT>
@@ -1018,6 +1193,11 @@ static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const 
                       Fb, accum);
         }
         return hipGetLastError();
+    }
+    if constexpr (TRAV >= 400 && TRAV < 500) {
+        if (ws.regen)
+            return wf_render_regen<LDS, TRAV, COUNT>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream, ws,
+                                                     tblocks, lds, bf_slots);
     }
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
@@ -1115,9 +1295,13 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
                             Counters* cnt, hipStream_t stream, const WfStreams& ws_in) {
     WfStreams ws = lo.dual != 0 ? ws_in : WfStreams{};  // parts on streams by default: +15 % measured (in-process A/B)
+    ws.h_poll = ws_in.h_poll;  // the regeneration loop's polling words, with one stream too
+    for (int h = 0; h < kMaxParts; ++h) for (int k = 0; k < 2; ++k) ws.poll_ev[h][k] = ws_in.poll_ev[h][k];
     ws.nparts = std::max(1, std::min(kMaxParts, lo.parts > 0 ? lo.parts : 2));
     ws.stagger = lo.stagger > 0;
     ws.fuse_gen = lo.fuse_gen != 0;
+    ws.regen = lo.regen > 0 && ws.h_poll != nullptr;  // PT_REGEN=1 (measured slower so far)
+    ws.regen_target = lo.regen_target > 0 ? (uint32_t)std::min<long>(lo.regen_target, 0x7fffffffL) : 0u;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     if (sc.node_bias <= 0) sc.node_bias = 8;  // measured best with lean16 (1 = majority: -13 %)

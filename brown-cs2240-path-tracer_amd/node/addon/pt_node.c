@@ -57,15 +57,41 @@ static int get_u8(napi_env env, napi_value v, uint8_t** data, size_t* len) {
 static int get_i32(napi_env env, napi_value v, int32_t* out) { return napi_get_value_int32(env, v, out) == napi_ok; }
 static int get_u32(napi_env env, napi_value v, uint32_t* out) { return napi_get_value_uint32(env, v, out) == napi_ok; }
 
+/* A JS scene handle: the library's scene plus the addon's job guard.  Calls on one pt_scene are
+ * not re-entrant (include/pt_hip.h), and render()/renderImage() run on libuv worker threads, so
+ * a second job on a scene whose job is still running is rejected (busy), and so are
+ * renderSync()/frame()/sceneDestroy() while one runs.  All of these checks run on the JS thread,
+ * which also clears `busy` when the job completes: no locking needed. */
+typedef struct {
+    pt_scene* s;
+    int busy;
+} scene_box;
+
 static void scene_finalize(napi_env env, void* data, void* hint) {
     (void)env; (void)hint;
-    pt_scene_destroy((pt_scene*)data);
+    scene_box* b = (scene_box*)data;
+    if (b->s) pt_scene_destroy(b->s);
+    free(b);
 }
 
-static pt_scene* get_scene(napi_env env, napi_value v) {
+static scene_box* get_box(napi_env env, napi_value v) {
     void* p = NULL;
     if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
-    return (pt_scene*)p;
+    return (scene_box*)p;
+}
+
+/* the live scene of a handle: NULL (and a pending JS error) if destroyed or busy */
+static pt_scene* get_scene(napi_env env, napi_value v) {
+    scene_box* b = get_box(env, v);
+    if (!b) return NULL;
+    if (!b->s) { napi_throw_error(env, NULL, "scene was destroyed (sceneDestroy)"); return NULL; }
+    if (b->busy) { napi_throw_error(env, NULL, "scene is busy: a render job on it has not completed"); return NULL; }
+    return b->s;
+}
+
+static int pending_exception(napi_env env) {
+    bool p = false;
+    return napi_is_exception_pending(env, &p) == napi_ok && p;
 }
 
 static napi_value counters_obj(napi_env env, const pt_counters* c) {
@@ -115,9 +141,45 @@ static napi_value js_scene_create(napi_env env, napi_callback_info info) {
     pt_scene* s = NULL;
     int rc = pt_scene_create(tri, tl, bvh, bl, dev, &s);
     if (rc) return throw_pt(env, rc);
+    scene_box* b = (scene_box*)calloc(1, sizeof(scene_box));
+    if (!b) { pt_scene_destroy(s); napi_throw_error(env, NULL, "out of memory"); return NULL; }
+    b->s = s;
     napi_value ext;
-    CHECK_NAPI(env, napi_create_external(env, s, scene_finalize, NULL, &ext));
+    if (napi_create_external(env, b, scene_finalize, NULL, &ext) != napi_ok) {
+        pt_scene_destroy(s);
+        free(b);
+        napi_throw_error(env, NULL, "napi_create_external failed");
+        return NULL;
+    }
+    /* V8 cannot see device memory: tell it, so that dropped scenes are collected */
+    pt_scene_info si;
+    if (pt_scene_get_info(s, &si) == PT_OK) {
+        int64_t adj = 0;
+        napi_adjust_external_memory(env, (int64_t)si.device_bytes, &adj);
+    }
     return ext;
+}
+
+/* sceneDestroy(scene): free the scene's device memory now (the handle becomes unusable); throws
+ * while a render job on it runs */
+static napi_value js_scene_destroy(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    scene_box* b = argc ? get_box(env, argv[0]) : NULL;
+    if (!b) { napi_throw_type_error(env, NULL, "sceneDestroy(scene)"); return NULL; }
+    if (b->busy) { napi_throw_error(env, NULL, "scene is busy: a render job on it has not completed"); return NULL; }
+    if (b->s) {
+        pt_scene_info si;
+        int have = pt_scene_get_info(b->s, &si) == PT_OK;
+        pt_scene_destroy(b->s);
+        b->s = NULL;
+        if (have) {
+            int64_t adj = 0;
+            napi_adjust_external_memory(env, -(int64_t)si.device_bytes, &adj);
+        }
+    }
+    return NULL;
 }
 
 /* sceneInfo(scene) -> object */
@@ -126,7 +188,7 @@ static napi_value js_scene_info(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
-    if (!s) { napi_throw_type_error(env, NULL, "sceneInfo(scene)"); return NULL; }
+    if (!s) { if (!pending_exception(env)) napi_throw_type_error(env, NULL, "sceneInfo(scene)"); return NULL; }
     pt_scene_info si;
     int rc = pt_scene_get_info(s, &si);
     if (rc) return throw_pt(env, rc);
@@ -143,6 +205,7 @@ typedef struct {
     napi_async_work work;
     napi_deferred deferred;
     napi_ref refs[3]; /* scene, meta, accum kept alive while the worker runs */
+    scene_box* box;   /* busy while the job runs */
     pt_scene* scene;
     float meta[48];
     uint32_t frame0, nframes, stride;
@@ -166,6 +229,7 @@ static void render_execute(napi_env env, void* data) {
 
 static void render_complete(napi_env env, napi_status status, void* data) {
     render_job* j = (render_job*)data;
+    if (j->box) j->box->busy = 0;
     if (status == napi_ok && j->rc == 0) {
         napi_value none;
         napi_get_null(env, &none);
@@ -200,6 +264,7 @@ static int parse_render_args(napi_env env, napi_callback_info info, render_job* 
     if (!parse_want_counters(env, argc, argv, j)) return 0;
     float* meta;
     size_t ml, al;
+    j->box = get_box(env, argv[0]);
     j->scene = get_scene(env, argv[0]);
     if (!j->scene || !get_f32(env, argv[1], &meta, &ml) || ml < 48) return 0;
     memcpy(j->meta, meta, sizeof j->meta);
@@ -217,11 +282,13 @@ static napi_value js_render(napi_env env, napi_callback_info info) {
     if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
     if (!parse_render_args(env, info, j, argv)) {
         free(j);
-        napi_throw_type_error(env, NULL,
-                              "render(scene, Float32Array meta[48], frame0, nframes, stride, maxDepth, mode, "
-                              "Float32Array accum[W*H*3], counters?)");
+        if (!pending_exception(env))
+            napi_throw_type_error(env, NULL,
+                                  "render(scene, Float32Array meta[48], frame0, nframes, stride, maxDepth, mode, "
+                                  "Float32Array accum[W*H*3], counters?)");
         return NULL;
     }
+    j->box->busy = 1;
     napi_value promise, name;
     CHECK_NAPI(env, napi_create_promise(env, &j->deferred, &promise));
     napi_create_reference(env, argv[0], 1, &j->refs[0]);
@@ -229,6 +296,107 @@ static napi_value js_render(napi_env env, napi_callback_info info) {
     napi_create_reference(env, argv[7], 1, &j->refs[2]);
     napi_create_string_utf8(env, "pt_render", NAPI_AUTO_LENGTH, &name);
     CHECK_NAPI(env, napi_create_async_work(env, NULL, name, render_execute, render_complete, j, &j->work));
+    CHECK_NAPI(env, napi_queue_async_work(env, j->work));
+    return promise;
+}
+
+/* renderMulti([scene, ...], meta, frame0, nframes, stride, maxDepth, mode, accum[, counters=true])
+ * -> Promise<counters|null>: one image over one scene per device (pt_render_multi: frames dealt
+ * round-robin, partial accumulators reduced onto the first scene's device) */
+#define PT_NODE_MAX_DEVICES 64
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref refs[3]; /* scene array, meta, accum */
+    scene_box* boxes[PT_NODE_MAX_DEVICES];
+    pt_scene* scenes[PT_NODE_MAX_DEVICES];
+    int n;
+    float meta[48];
+    uint32_t frame0, nframes, stride;
+    int32_t max_depth, mode;
+    float* accum;
+    pt_counters counters;
+    int want_counters;
+    int rc;
+    char err[512];
+} multi_job;
+
+static void multi_execute(napi_env env, void* data) {
+    (void)env;
+    multi_job* j = (multi_job*)data;
+    j->rc = pt_render_multi(j->scenes, j->n, j->meta, j->frame0, j->nframes, j->stride, j->max_depth, j->mode, j->accum,
+                            j->want_counters ? &j->counters : NULL);
+    if (j->rc) snprintf(j->err, sizeof j->err, "pt_hip error %d: %s", j->rc, pt_last_error());
+}
+
+static void multi_complete(napi_env env, napi_status status, void* data) {
+    multi_job* j = (multi_job*)data;
+    for (int i = 0; i < j->n; ++i) j->boxes[i]->busy = 0;
+    if (status == napi_ok && j->rc == 0) {
+        napi_value none;
+        napi_get_null(env, &none);
+        napi_resolve_deferred(env, j->deferred, j->want_counters ? counters_obj(env, &j->counters) : none);
+    } else {
+        napi_value msg, e;
+        napi_create_string_utf8(env, j->rc ? j->err : "render cancelled", NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, NULL, msg, &e);
+        napi_reject_deferred(env, j->deferred, e);
+    }
+    for (int i = 0; i < 3; ++i) napi_delete_reference(env, j->refs[i]);
+    napi_delete_async_work(env, j->work);
+    free(j);
+}
+
+static napi_value js_render_multi(napi_env env, napi_callback_info info) {
+    size_t argc = 9;
+    napi_value argv[9];
+    multi_job* j = (multi_job*)calloc(1, sizeof(multi_job));
+    if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
+    int ok = napi_get_cb_info(env, info, &argc, argv, NULL, NULL) == napi_ok && argc >= 8;
+    bool is_arr = false;
+    uint32_t n = 0;
+    if (ok) ok = napi_is_array(env, argv[0], &is_arr) == napi_ok && is_arr &&
+                 napi_get_array_length(env, argv[0], &n) == napi_ok && n >= 1 && n <= PT_NODE_MAX_DEVICES;
+    for (uint32_t i = 0; ok && i < n; ++i) {
+        napi_value e;
+        ok = napi_get_element(env, argv[0], i, &e) == napi_ok && (j->boxes[i] = get_box(env, e)) != NULL &&
+             (j->scenes[i] = get_scene(env, e)) != NULL;
+        for (uint32_t k = 0; ok && k < i; ++k) ok = j->boxes[k] != j->boxes[i];
+    }
+    j->n = (int)n;
+    float* meta = NULL;
+    size_t ml = 0, al = 0;
+    if (ok) {
+        bool want = true;
+        if (argc > 8) {
+            napi_valuetype t;
+            ok = napi_typeof(env, argv[8], &t) == napi_ok && (t == napi_undefined || napi_get_value_bool(env, argv[8], &want) == napi_ok);
+        }
+        j->want_counters = want ? 1 : 0;
+    }
+    if (ok) ok = get_f32(env, argv[1], &meta, &ml) && ml >= 48;
+    if (ok) {
+        memcpy(j->meta, meta, sizeof j->meta);
+        ok = get_u32(env, argv[2], &j->frame0) && get_u32(env, argv[3], &j->nframes) && get_u32(env, argv[4], &j->stride) &&
+             get_i32(env, argv[5], &j->max_depth) && get_i32(env, argv[6], &j->mode) && get_f32(env, argv[7], &j->accum, &al) &&
+             al == (size_t)j->meta[0] * (size_t)j->meta[1] * 3;
+    }
+    if (!ok) {
+        free(j);
+        if (!pending_exception(env))
+            napi_throw_type_error(env, NULL,
+                                  "renderMulti([scene, ...] (distinct handles, <= 64), Float32Array meta[48], frame0, "
+                                  "nframes, stride, maxDepth, mode, Float32Array accum[W*H*3], counters?)");
+        return NULL;
+    }
+    for (int i = 0; i < j->n; ++i) j->boxes[i]->busy = 1;
+    napi_value promise, name;
+    CHECK_NAPI(env, napi_create_promise(env, &j->deferred, &promise));
+    napi_create_reference(env, argv[0], 1, &j->refs[0]);
+    napi_create_reference(env, argv[1], 1, &j->refs[1]);
+    napi_create_reference(env, argv[7], 1, &j->refs[2]);
+    napi_create_string_utf8(env, "pt_render_multi", NAPI_AUTO_LENGTH, &name);
+    CHECK_NAPI(env, napi_create_async_work(env, NULL, name, multi_execute, multi_complete, j, &j->work));
     CHECK_NAPI(env, napi_queue_async_work(env, j->work));
     return promise;
 }
@@ -246,6 +414,7 @@ static napi_value js_render_image(napi_env env, napi_callback_info info) {
     int ok = napi_get_cb_info(env, info, &argc, argv, NULL, NULL) == napi_ok && argc >= 8 &&
              parse_want_counters(env, argc, argv, j);
     if (ok) {
+        j->box = get_box(env, argv[0]);
         j->scene = get_scene(env, argv[0]);
         ok = j->scene && get_f32(env, argv[1], &meta, &ml) && ml >= 48;
     }
@@ -257,11 +426,13 @@ static napi_value js_render_image(napi_env env, napi_callback_info info) {
     }
     if (!ok) {
         free(j);
-        napi_throw_type_error(env, NULL,
-                              "renderImage(scene, Float32Array meta[48], frame0, nframes, stride, maxDepth, mode, "
-                              "Uint8Array rgba[W*H*4])");
+        if (!pending_exception(env))
+            napi_throw_type_error(env, NULL,
+                                  "renderImage(scene, Float32Array meta[48], frame0, nframes, stride, maxDepth, mode, "
+                                  "Uint8Array rgba[W*H*4])");
         return NULL;
     }
+    j->box->busy = 1;
     napi_value promise, name;
     CHECK_NAPI(env, napi_create_promise(env, &j->deferred, &promise));
     napi_create_reference(env, argv[0], 1, &j->refs[0]);
@@ -279,7 +450,8 @@ static napi_value js_render_sync(napi_env env, napi_callback_info info) {
     render_job j;
     memset(&j, 0, sizeof j);
     if (!parse_render_args(env, info, &j, argv)) {
-        napi_throw_type_error(env, NULL, "renderSync(scene, meta, frame0, nframes, stride, maxDepth, mode, accum)");
+        if (!pending_exception(env))
+            napi_throw_type_error(env, NULL, "renderSync(scene, meta, frame0, nframes, stride, maxDepth, mode, accum)");
         return NULL;
     }
     int rc = pt_render(j.scene, j.meta, j.frame0, j.nframes, j.stride, j.max_depth, j.mode, j.accum,
@@ -302,7 +474,7 @@ static napi_value js_frame(napi_env env, napi_callback_info info) {
     pt_scene* s = argc >= 5 ? get_scene(env, argv[0]) : NULL;
     if (!s || !get_f32(env, argv[1], &meta, &ml) || ml < 48 || !get_u32(env, argv[2], &t) || !get_i32(env, argv[3], &md) ||
         !get_f32(env, argv[4], &out, &ol) || ol != (size_t)meta[0] * (size_t)meta[1] * 3) {
-        napi_throw_type_error(env, NULL, "frame(scene, meta, t, maxDepth, Float32Array out[W*H*3])");
+        if (!pending_exception(env)) napi_throw_type_error(env, NULL, "frame(scene, meta, t, maxDepth, Float32Array out[W*H*3])");
         return NULL;
     }
     int rc = pt_frame(s, meta, t, md, out);
@@ -365,7 +537,7 @@ static napi_value js_profile_enable(napi_env env, napi_callback_info info) {
     pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
     bool on = true;
     if (!s || (argc > 1 && napi_get_value_bool(env, argv[1], &on) != napi_ok)) {
-        napi_throw_type_error(env, NULL, "profileEnable(scene, enable)");
+        if (!pending_exception(env)) napi_throw_type_error(env, NULL, "profileEnable(scene, enable)");
         return NULL;
     }
     int rc = pt_profile_enable(s, on ? 1 : 0);
@@ -381,7 +553,7 @@ static napi_value js_scene_set_vertex_normals(napi_env env, napi_callback_info i
     pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
     bool on = true;
     if (!s || (argc > 1 && napi_get_value_bool(env, argv[1], &on) != napi_ok)) {
-        napi_throw_type_error(env, NULL, "sceneSetVertexNormals(scene, enable)");
+        if (!pending_exception(env)) napi_throw_type_error(env, NULL, "sceneSetVertexNormals(scene, enable)");
         return NULL;
     }
     int rc = pt_scene_set_vertex_normals(s, on ? 1 : 0);
@@ -389,13 +561,13 @@ static napi_value js_scene_set_vertex_normals(napi_env env, napi_callback_info i
     return NULL;
 }
 
-/* profileRead(scene) -> {kernel: {launches, totalMs, minMs, maxMs}} */
+/* profileRead(scene) -> {kernel: {launches, totalMs, minMs, maxMs, busyMs}} */
 static napi_value js_profile_read(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1];
     CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     pt_scene* s = argc ? get_scene(env, argv[0]) : NULL;
-    if (!s) { napi_throw_type_error(env, NULL, "profileRead(scene)"); return NULL; }
+    if (!s) { if (!pending_exception(env)) napi_throw_type_error(env, NULL, "profileRead(scene)"); return NULL; }
     pt_kernel_time kt[16];
     int n = 0;
     int rc = pt_profile_read(s, kt, 16, &n);
@@ -408,6 +580,7 @@ static napi_value js_profile_read(napi_env env, napi_callback_info info) {
         napi_create_double(env, kt[i].total_ms, &v); napi_set_named_property(env, k, "totalMs", v);
         napi_create_double(env, kt[i].min_ms, &v); napi_set_named_property(env, k, "minMs", v);
         napi_create_double(env, kt[i].max_ms, &v); napi_set_named_property(env, k, "maxMs", v);
+        napi_create_double(env, kt[i].busy_ms, &v); napi_set_named_property(env, k, "busyMs", v);
         napi_set_named_property(env, o, kt[i].name, k);
     }
     return o;
@@ -419,8 +592,10 @@ static napi_value init(napi_env env, napi_value exports) {
         {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
         {"sceneCreate", NULL, js_scene_create, NULL, NULL, NULL, napi_enumerable, NULL},
         {"sceneInfo", NULL, js_scene_info, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"sceneDestroy", NULL, js_scene_destroy, NULL, NULL, NULL, napi_enumerable, NULL},
         {"render", NULL, js_render, NULL, NULL, NULL, napi_enumerable, NULL},
         {"renderSync", NULL, js_render_sync, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"renderMulti", NULL, js_render_multi, NULL, NULL, NULL, napi_enumerable, NULL},
         {"renderImage", NULL, js_render_image, NULL, NULL, NULL, napi_enumerable, NULL},
         {"frame", NULL, js_frame, NULL, NULL, NULL, napi_enumerable, NULL},
         {"tonemap", NULL, js_tonemap, NULL, NULL, NULL, napi_enumerable, NULL},

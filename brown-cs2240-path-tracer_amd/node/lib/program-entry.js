@@ -32,7 +32,8 @@ function make_meta(screenDimension, camera_data, scene_description, time_elapsed
 /**
  * programEntry(screenDimension, primitive_data, camera_data, scene_description, options?)
  *   -> Promise<{accum: Float32Array(W*H*3), sample_runs, rgba: Uint8ClampedArray(W*H*4), counters, scene_info}>
- * options: {device=0, maxDepth=16, mode='auto', frame0=0, chunk=spp, onFrames(done, total), imageOnly=false,
+ * options: {device=0, devices=[...] (several GPUs: pt_render_multi), maxDepth=16, mode='auto', frame0=0, chunk=spp,
+ *           onFrames(done, total), imageOnly=false,
  *           vertexNormals=false (the reference's commented-out smooth-normal branch; changes results),
  *           counters=false (work counters: the kernels' counting builds, slower; counters is null without)}
  * imageOnly: render and tone-map on the device in one call and return only {rgba, counters, ...}
@@ -44,29 +45,58 @@ async function programEntry(screenDimension, primitive_data, camera_data, scene_
     const pt = load();
     const [W, H] = screenDimension;
     const meta = make_meta(screenDimension, camera_data, scene_description, 0);
-    const scene = pt.sceneCreate(primitive_data[0].triangle_data, primitive_data[0].bvh_data, o.device);
-    if (o.vertexNormals) pt.sceneSetVertexNormals(scene, true);
-    const spp = scene_description.Settings.samplesPerPixel;
-    const chunk = Math.max(1, o.chunk || spp);
-    const accum = new Float32Array(W * H * 3);
-    const counters = { samples: 0, ext_queries: 0, shadow_queries: 0, nodes: 0, tri_tests: 0, box_tests: 0 };
     const mode = typeof o.mode === 'number' ? o.mode : MODE[o.mode];
     if (mode === undefined) throw Error(`unknown mode ${o.mode}`);
-    if (o.imageOnly) {
+    if (o.devices && o.devices.length > 1) return programEntryMulti(pt, meta, W, H, primitive_data, scene_description, o, mode);
+    const scene = pt.sceneCreate(primitive_data[0].triangle_data, primitive_data[0].bvh_data,
+                                 o.devices && o.devices.length ? o.devices[0] : o.device);
+    // the scene's device memory (scene + wavefront state) is released when the call ends, not
+    // when V8 happens to collect the handle
+    try {
+        if (o.vertexNormals) pt.sceneSetVertexNormals(scene, true);
+        const spp = scene_description.Settings.samplesPerPixel;
+        const chunk = Math.max(1, o.chunk || spp);
+        const scene_info = pt.sceneInfo(scene);
+        if (o.imageOnly) {
+            const rgba = new Uint8ClampedArray(W * H * 4);
+            const c = await pt.renderImage(scene, meta, o.frame0, spp, 1, o.maxDepth, mode, new Uint8Array(rgba.buffer),
+                                           !!o.counters);
+            return { accum: null, sample_runs: spp, rgba, counters: c, scene_info };
+        }
+        const accum = new Float32Array(W * H * 3);
+        const counters = { samples: 0, ext_queries: 0, shadow_queries: 0, nodes: 0, tri_tests: 0, box_tests: 0 };
+        for (let done = 0; done < spp; done += chunk) {
+            const n = Math.min(chunk, spp - done);
+            const c = await pt.render(scene, meta, o.frame0 + done, n, 1, o.maxDepth, mode, accum, !!o.counters);
+            if (c) for (const k of Object.keys(counters)) counters[k] += c[k];
+            if (o.onFrames) o.onFrames(done + n, spp);
+        }
         const rgba = new Uint8ClampedArray(W * H * 4);
-        const c = await pt.renderImage(scene, meta, o.frame0, spp, 1, o.maxDepth, mode, new Uint8Array(rgba.buffer),
-                                       !!o.counters);
-        return { accum: null, sample_runs: spp, rgba, counters: c, scene_info: pt.sceneInfo(scene) };
+        pt.tonemap(accum, spp, rgba);
+        return { accum, sample_runs: spp, rgba, counters: o.counters ? counters : null, scene_info };
+    } finally {
+        pt.sceneDestroy(scene);
     }
-    for (let done = 0; done < spp; done += chunk) {
-        const n = Math.min(chunk, spp - done);
-        const c = await pt.render(scene, meta, o.frame0 + done, n, 1, o.maxDepth, mode, accum, !!o.counters);
-        if (c) for (const k of Object.keys(counters)) counters[k] += c[k];
-        if (o.onFrames) o.onFrames(done + n, spp);
+}
+
+// options.devices = [d0, d1, ...]: the scene on every device, frames dealt round-robin and the
+// partial accumulators reduced onto d0 (pt_render_multi: RCCL over xGMI for distinct devices)
+async function programEntryMulti(pt, meta, W, H, primitive_data, scene_description, o, mode) {
+    const scenes = [];
+    try {
+        for (const d of o.devices) scenes.push(pt.sceneCreate(primitive_data[0].triangle_data, primitive_data[0].bvh_data, d));
+        if (o.vertexNormals) for (const s of scenes) pt.sceneSetVertexNormals(s, true);
+        const spp = scene_description.Settings.samplesPerPixel;
+        const scene_info = pt.sceneInfo(scenes[0]);
+        const accum = new Float32Array(W * H * 3);
+        const counters = await pt.renderMulti(scenes, meta, o.frame0, spp, 1, o.maxDepth, mode, accum, !!o.counters);
+        if (o.onFrames) o.onFrames(spp, spp);
+        const rgba = new Uint8ClampedArray(W * H * 4);
+        pt.tonemap(accum, spp, rgba);
+        return { accum, sample_runs: spp, rgba, counters: o.counters ? counters : null, scene_info, devices: o.devices.slice() };
+    } finally {
+        for (const s of scenes) pt.sceneDestroy(s);
     }
-    const rgba = new Uint8ClampedArray(W * H * 4);
-    pt.tonemap(accum, spp, rgba);
-    return { accum, sample_runs: spp, rgba, counters: o.counters ? counters : null, scene_info: pt.sceneInfo(scene) };
 }
 
 module.exports = { programEntry, make_meta, MODE };

@@ -24,6 +24,7 @@ from ._lib import (  # noqa: F401
     device_count,
     lib_path,
     load_library,
+    render_multi,
     selftest_math,
     selftest_rcp,
     set_hw_queues,

@@ -101,8 +101,9 @@ def load_library():
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     L.pt_scene_set_vertex_normals.argtypes = [p, i]
     L.pt_scene_check.argtypes = [p]
+    L.pt_render_multi.argtypes = [ctypes.POINTER(p), i, p, u32, u32, u32, i, i, p, p]
     L.pt_set_hw_queues.argtypes = [i]
-    for fn in ("pt_scene_check", "pt_set_hw_queues", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+    for fn in ("pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
                "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
@@ -251,6 +252,23 @@ class Scene:
         out = np.zeros((H, W, 3), np.float32)
         _check(self._lib.pt_frame(self._h, _ptr(meta), t, max_depth, _ptr(out)))
         return out
+
+
+def render_multi(scenes, meta, frame0: int, nframes: int, stride: int = 1, max_depth: int = -1,
+                 mode: int = MODE_AUTO, accum: np.ndarray | None = None, counters: bool = False):
+    """pt_render_multi: one image over several Scenes (one per device, repeats allowed), frames dealt
+    round-robin, partial accumulators reduced onto scenes[0]'s device (RCCL, or PT_REDUCE=ordered)."""
+    meta = _f32(meta)
+    W, H = int(meta[0]), int(meta[1])
+    if accum is None:
+        accum = np.zeros((H, W, 3), np.float32)
+    if accum.dtype != np.float32 or not accum.flags.c_contiguous or accum.size != W * H * 3:
+        raise ValueError("accum must be a contiguous float32 array of H*W*3 elements")
+    handles = (ctypes.c_void_p * len(scenes))(*[s._h.value for s in scenes])
+    c = Counters()
+    _check(load_library().pt_render_multi(handles, len(scenes), _ptr(meta), frame0, nframes, stride, max_depth, mode,
+                                          _ptr(accum), ctypes.byref(c) if counters else None))
+    return (accum, c.as_dict()) if counters else accum
 
 
 def tonemap(accum, sample_runs: int) -> np.ndarray:

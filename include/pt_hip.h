@@ -141,6 +141,22 @@ int pt_scene_check(pt_scene* scene);
  * wavefront's two part streams (e.g. torch) want 8 so the parts do not share a queue. */
 int pt_set_hw_queues(int n);
 
+/* Multi-GPU render of one image (the `n_gpus` of §8(b)): scenes[g] is the same
+ * packed scene uploaded to device g (pt_scene_create per device, any devices, repeats allowed).
+ * Frames k = frame0 + i*frame_stride (i < nframes) are dealt round-robin: scene g renders the i
+ * with i % n == g (frame-interleaved: every device sees the same mix of path lengths), each into
+ * an f32 accumulator on its own device (scenes[0]'s starts from accum, the others from zero), on
+ * one host thread per device; the partial accumulators are then summed onto scenes[0]'s device
+ * and copied to accum (host f32 [H][W][3], in/out).
+ * Reduction (environment PT_REDUCE): "rccl" (default when the devices are distinct and
+ * librccl.so.1 loads) = ONE ncclReduce(sum, f32) to device 0 over a communicator made once per
+ * device list (ncclCommInitAll, single process) — the summation order is RCCL's; "ordered" (and
+ * always with repeated devices) = peer copies added on device 0 in device order,
+ * deterministic.  n == 1 is exactly pt_render.  counters: nullable, summed over devices.
+ * Blocking; the scenes must not be in use by other calls meanwhile. */
+int pt_render_multi(pt_scene* const* scenes, int n, const float meta[48], uint32_t frame0, uint32_t nframes,
+                    uint32_t frame_stride, int max_depth, int mode, float* accum, pt_counters* counters);
+
 /* One reference dispatch: radiance[H][W][3] = radiance() of every pixel for RNG salt t
  * (the resultMatrix of program-raymarch.wgsl:82-84, before host clamping). */
 int pt_frame(pt_scene* scene, const float meta[48], uint32_t t, int max_depth, float* radiance);

@@ -105,3 +105,16 @@ def test_tonemap_matches_oracle():
         got = pt_amd.tonemap(acc, runs).reshape(-1)
         want = oracle.tonemap(acc, runs)
         assert np.array_equal(got, want)
+
+
+def test_render_multi_argument_checks():
+    lib = pt_amd.load_library()
+    meta = np.zeros(48, np.float32)
+    acc = np.zeros(3, np.float32)
+    assert lib.pt_render_multi(None, 2, meta.ctypes.data_as(ctypes.c_void_p), 0, 1, 1, 8, 0,
+                               acc.ctypes.data_as(ctypes.c_void_p), None) == -1
+    arr = (ctypes.c_void_p * 2)(None, None)
+    assert lib.pt_render_multi(arr, 2, meta.ctypes.data_as(ctypes.c_void_p), 0, 1, 1, 8, 0,
+                               acc.ctypes.data_as(ctypes.c_void_p), None) == -1
+    assert lib.pt_render_multi(arr, 0, meta.ctypes.data_as(ctypes.c_void_p), 0, 1, 1, 8, 0,
+                               acc.ctypes.data_as(ctypes.c_void_p), None) == -1

@@ -1,0 +1,83 @@
+"""pt_render_multi (the C ABI's multi-GPU entry): frames dealt round-robin over one
+scene per device, partial f32 accumulators reduced onto the first scene's device.
+
+The box has one GPU, so the multi-device orchestration runs with repeated devices (several scenes
+on device 0: one host thread each, then the ORDERED reduction: partials added in device order).
+That reduction is deterministic, so it is pinned bit for bit against the oracle's per-shard
+renders summed in the same order; n = 1 is pt_render exactly.  The RCCL reduction (distinct
+devices) changes only the summation order of the same partials; the driver's 8-GPU node runs it.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import pt_amd
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def env(monkeypatch):
+    for k in ("PT_KERNEL", "PT_REDUCE", "PT_PARTS", "PT_WF_PATHS", "PT_REGEN"):
+        monkeypatch.delenv(k, raising=False)
+    return monkeypatch
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def test_single_device_list_is_pt_render(packed, env):
+    p = packed["CornellBox"]
+    meta = p.meta_for(256, 256)
+    init = np.random.default_rng(3).uniform(0, 1, (256, 256, 3)).astype(np.float32)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        a, ca = pt_amd.render_multi([s], meta, 0, 20, 1, 8, accum=init.copy(), counters=True)
+        b, cb = s.render(meta, 0, 20, 1, 8, accum=init.copy(), counters=True)
+    assert np.array_equal(bits(a), bits(b)) and ca == cb
+
+
+@pytest.mark.parametrize("n,mode", [(2, pt_amd.MODE_AUTO), (3, pt_amd.MODE_MEGAKERNEL), (4, pt_amd.MODE_WAVEFRONT)])
+def test_repeated_device_ordered_reduction_vs_oracle(packed, env, n, mode):
+    p = packed["CornellBox"]
+    W = H = 64
+    meta = p.meta_for(W, H)
+    frame0, nframes, stride, depth = 3, 11, 2, 8
+    init = np.random.default_rng(5).uniform(0, 1, (H, W, 3)).astype(np.float32)
+    scenes = [pt_amd.Scene(p.triangle_data, p.bvh_data, device=0) for _ in range(n)]
+    try:
+        got, cnt = pt_amd.render_multi(scenes, meta, frame0, nframes, stride, depth, mode, accum=init.copy(),
+                                       counters=True)
+    finally:
+        for s in scenes:
+            s.close()
+    # oracle: shard g renders frames i = g, g + n, ... (k = frame0 + i * stride) onto init (g = 0) or zero,
+    # then the partials are added in device order
+    parts, total = [], {}
+    for g in range(n):
+        cnt_g = len(range(g, nframes, n))
+        acc, c = oracle.render(p.triangle_data, p.bvh_data, meta, frame0 + g * stride, cnt_g, n * stride, depth,
+                               acc=init.copy() if g == 0 else np.zeros_like(init))
+        parts.append(acc)
+        for k, v in c.items():
+            total[k] = total.get(k, 0) + v
+    want = parts[0].copy()
+    for g in range(1, n):
+        want += parts[g]
+    assert np.array_equal(bits(got), bits(want))
+    assert cnt == total
+    # and within f32 rounding of the single-device render of all frames
+    ref, _ = oracle.render(p.triangle_data, p.bvh_data, meta, frame0, nframes, stride, depth, acc=init.copy())
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_rccl_mode_rejects_repeated_devices(packed, env):
+    p = packed["CornellBox"]
+    env.setenv("PT_REDUCE", "rccl")
+    scenes = [pt_amd.Scene(p.triangle_data, p.bvh_data, device=0) for _ in range(2)]
+    try:
+        with pytest.raises(pt_amd.PtError):
+            pt_amd.render_multi(scenes, p.meta_for(32, 32), 0, 2, 1, 4)
+    finally:
+        for s in scenes:
+            s.close()

@@ -70,3 +70,56 @@ def test_pt_render_cli_writes_png():
         img = np.array(Image.open(info["output"]))
     assert img.shape == (info["height"], info["width"], 4) and info["spp"] == 2
     assert img[..., 3].min() == 255 and img[..., :3].mean() > 10
+
+
+NODE_MULTI = r"""
+const fs = require('fs');
+const host = require(process.argv[1]);
+(async () => {
+    const s = host.load_scene_from_ini(process.argv[2], { web_root: process.argv[3], quiet: true });
+    const S = s.scene_description.Settings;
+    S.imageWidth = %d; S.imageHeight = %d; S.samplesPerPixel = %d;
+    const dim = host.screen_dimension(S);
+    const a = await host.programEntry(dim, s.primitive_data, s.camera_data, s.scene_description,
+                                      { maxDepth: 8, devices: [0, 0, 0], counters: true });
+    fs.writeFileSync(process.argv[4] + '/accum_multi.f32', Buffer.from(a.accum.buffer));
+    // one job per scene at a time: a second render on a busy scene is rejected, not raced
+    const pt = host.native();
+    const sc = pt.sceneCreate(s.primitive_data[0].triangle_data, s.primitive_data[0].bvh_data, 0);
+    const meta = host.make_meta(dim, s.camera_data, s.scene_description, 0);
+    const acc = new Float32Array(dim[0] * dim[1] * 3);
+    const p1 = pt.render(sc, meta, 0, 4, 1, 8, 0, acc, false);
+    let busy = null;
+    try { await pt.render(sc, meta, 0, 4, 1, 8, 0, new Float32Array(acc.length), false); } catch (e) { busy = e.message; }
+    let busy_sync = null;
+    try { pt.renderSync(sc, meta, 0, 1, 1, 8, 0, new Float32Array(acc.length), false); } catch (e) { busy_sync = e.message; }
+    let busy_destroy = null;
+    try { pt.sceneDestroy(sc); } catch (e) { busy_destroy = e.message; }
+    await p1;
+    pt.sceneDestroy(sc);
+    let gone = null;
+    try { pt.sceneInfo(sc); } catch (e) { gone = e.message; }
+    fs.writeFileSync(process.argv[4] + '/busy.json', JSON.stringify({busy, busy_sync, busy_destroy, gone, counters: a.counters}));
+})().catch((e) => { console.error(e.stack || String(e)); process.exit(1); });
+""" % (W, H, SPP)
+
+
+def test_node_multi_device_and_busy_scene():
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.run(["node", "-e", NODE_MULTI, os.path.join(PKG, "node"), INI, SCENES, td], check=True,
+                       capture_output=True, timeout=300)
+        acc = np.fromfile(os.path.join(td, "accum_multi.f32"), np.float32).reshape(H, W, 3)
+        info = json.load(open(os.path.join(td, "busy.json")))
+        p = pack_with_node(INI, os.path.join(td, "packed"), "--web-root", SCENES, "--width", str(W), "--height", str(H),
+                           "--spp", str(SPP))
+    scenes = [pt_amd.Scene(p.triangle_data, p.bvh_data) for _ in range(3)]
+    try:
+        ref, c = pt_amd.render_multi(scenes, p.meta, 0, SPP, 1, 8, counters=True)
+    finally:
+        for s in scenes:
+            s.close()
+    assert acc.tobytes() == ref.tobytes()
+    assert info["counters"] == c
+    for k in ("busy", "busy_sync", "busy_destroy"):
+        assert info[k] and "busy" in info[k], info
+    assert info["gone"] and "destroyed" in info["gone"]

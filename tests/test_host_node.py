@@ -183,7 +183,8 @@ let terr = null;
 try { pt.render(1, 2); } catch (e) { terr = e.constructor.name; }
 console.log(JSON.stringify({abi: pt.abiVersion(), keys: Object.keys(pt).sort(), err, terr}));''')
     assert r["abi"] == 2
-    assert r["keys"] == sorted(["abiVersion", "deviceCount", "sceneCreate", "sceneInfo", "render", "renderSync", "frame",
+    assert r["keys"] == sorted(["abiVersion", "deviceCount", "sceneCreate", "sceneDestroy", "sceneInfo", "render",
+                                "renderSync", "renderMulti", "frame",
                                 "tonemap", "profileEnable", "profileRead", "bvhBuild", "renderImage",
                                 "sceneSetVertexNormals"])
     assert r["terr"] == "TypeError"
