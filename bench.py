@@ -43,10 +43,19 @@ sys.path.insert(0, PKG)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def pack_scene(scene: str, out_dir: str, W: int, H: int, spp: int):
-    xml = os.path.join(ROOT, "scenes", "scene_assets", scene + ".xml")
+def pack_scene(scene: str, out_dir: str, W: int, H: int, spp: int, synthetic: int = 0, bvh: str = "reference",
+               all_meshes: bool = False):
+    """Pack with the product's Node host.  synthetic N: scripts/synth_scene.py's N-triangle
+    Cornell-sized scene (the sweep of SURVEY.md §8(d)) instead of a reference scene."""
+    if synthetic:
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import synth_scene  # noqa: E402
+        xml = synth_scene.write(synthetic, os.path.join(out_dir, "synth"))
+    else:
+        xml = os.path.join(ROOT, "scenes", "scene_assets", scene + ".xml")
+    extra = ["--bvh", bvh] + (["--native-bvh"] if synthetic or all_meshes else []) + (["--all-meshes"] if all_meshes else [])
     subprocess.run(["node", os.path.join(PKG, "node", "bin", "pt-pack.js"), xml, out_dir, "--width", str(W),
-                    "--height", str(H), "--spp", str(spp), "--rr", "0.9"], check=True)
+                    "--height", str(H), "--spp", str(spp), "--rr", "0.9", *extra], check=True)
     tri = np.fromfile(os.path.join(out_dir, "triangle_data.f32"), np.float32)
     bvh = np.fromfile(os.path.join(out_dir, "bvh_data.f32"), np.float32)
     meta = np.fromfile(os.path.join(out_dir, "meta.f32"), np.float32)
@@ -127,6 +136,9 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--mode", default="auto", choices=["auto", "megakernel", "wavefront"])
+    ap.add_argument("--synthetic", type=int, default=0, help="N-triangle synthetic Cornell-sized scene (BVH sweep)")
+    ap.add_argument("--bvh", default="reference", choices=["reference", "sah"], help="sah: the fast (non-parity) tree")
+    ap.add_argument("--all-meshes", action="store_true", help="every primitive of the scene (reference: first only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch HIP events")
     args = ap.parse_args()
@@ -145,8 +157,11 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
+    if args.synthetic:
+        args.scene = f"synthetic-{args.synthetic}"
     with tempfile.TemporaryDirectory() as td:
-        tri, bvh, meta = pack_scene(args.scene, td, args.width, args.height, args.spp)
+        tri, bvh, meta = pack_scene(args.scene, td, args.width, args.height, args.spp, args.synthetic, args.bvh,
+                                    args.all_meshes)
     W, H = int(meta[0]), int(meta[1])
     mode = {"auto": pt_amd.MODE_AUTO, "megakernel": pt_amd.MODE_MEGAKERNEL, "wavefront": pt_amd.MODE_WAVEFRONT}[args.mode]
     scene = pt_amd.Scene(tri, bvh, device=local_rank)
@@ -253,11 +268,15 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic (reference {args.scene}.xml scene packed by the Node host; RNG salts t_k = k)",
+            "data": (f"synthetic ({args.synthetic} triangles in the Cornell box, scripts/synth_scene.py, seed 1234; "
+                     if args.synthetic else f"synthetic (reference {args.scene}.xml scene ") +
+                    f"packed by the Node host, {args.bvh} BVH" + (", all meshes" if args.all_meshes else "") +
+                    "; RNG salts t_k = k)",
             "config": {"workload": f"{args.scene}.xml {W}x{H} {args.spp}spp depth {args.depth}, rr 0.9, "
                                    f"frames sharded k mod {world}" + (", RCCL sum-reduce of the f32 accumulator"
                                                                         if world > 1 else ""),
-                       "mode": args.mode, "samples_per_step": total_samples},
+                       "mode": args.mode, "bvh": args.bvh, "samples_per_step": total_samples,
+                       "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic[0] * launches_per_render / (busy_ms * 1e-3) / 1e9 if traffic and busy_ms else None,

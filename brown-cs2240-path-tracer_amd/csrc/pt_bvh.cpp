@@ -167,3 +167,149 @@ extern "C" int pt_bvh_build(const double* vertices, size_t vertex_count, const i
     for (size_t i = 0; i < out.size(); ++i) bvh_out[i] = (float)out[i];
     return PT_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Fast mode ("gives up topology parity"): a binned surface-area-heuristic
+// build over triangle centroids — each triangle in exactly one leaf, child boxes tight around
+// their triangles — written in the reference's packed layout, so the same traversal (exit-distance
+// pruning and all) runs on it.  Renders differ from the reference's tree only where that pruning
+// quirk bites differently; the GPU still equals the oracle on these buffers bit for bit.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kSahBins = 16;
+constexpr int kSahMaxLeaf = 8;   // a node above this many triangles is always split
+constexpr int kSahMaxDepth = 28; // the device stack (kStackMax 32) and the reference's 64-entry marker stack
+constexpr int kSahMinLeaf = 4;    // never split below this
+constexpr double kSahTraversal = 2.0;  // cost of a node step relative to one triangle test (a node tests two boxes)
+
+double area(const Box& b) {
+    const double x = b.mx[0] - b.mn[0], y = b.mx[1] - b.mn[1], z = b.mx[2] - b.mn[2];
+    return (x < 0 || y < 0 || z < 0) ? 0.0 : 2.0 * (x * y + y * z + z * x);
+}
+Box empty_box() {
+    Box b;
+    for (int k = 0; k < 3; ++k) { b.mn[k] = std::numeric_limits<double>::infinity(); b.mx[k] = -b.mn[k]; }
+    return b;
+}
+void grow(Box& b, const Box& o) {
+    for (int k = 0; k < 3; ++k) { b.mn[k] = std::min(b.mn[k], o.mn[k]); b.mx[k] = std::max(b.mx[k], o.mx[k]); }
+}
+
+struct SahBuilder {
+    const std::vector<Box>& tb;
+    std::vector<double> cen;  // 3 per triangle
+
+    void build(BNode& n, int depth) {
+        n.box = empty_box();
+        Box cb = empty_box();
+        for (int32_t o : n.objs) {
+            grow(n.box, tb[o]);
+            for (int k = 0; k < 3; ++k) {
+                cb.mn[k] = std::min(cb.mn[k], cen[3 * (size_t)o + k]);
+                cb.mx[k] = std::max(cb.mx[k], cen[3 * (size_t)o + k]);
+            }
+        }
+        const int cnt = (int)n.objs.size();
+        if (cnt <= kSahMinLeaf || depth >= kSahMaxDepth) { n.leaf = true; return; }
+        double best = std::numeric_limits<double>::infinity();
+        int bax = -1, bsplit = 0;
+        for (int ax = 0; ax < 3; ++ax) {
+            const double lo = cb.mn[ax], ext = cb.mx[ax] - cb.mn[ax];
+            if (!(ext > 0)) continue;
+            Box bb[kSahBins];
+            int bn[kSahBins] = {};
+            for (int i = 0; i < kSahBins; ++i) bb[i] = empty_box();
+            for (int32_t o : n.objs) {
+                int i = (int)((cen[3 * (size_t)o + ax] - lo) / ext * kSahBins);
+                i = std::min(std::max(i, 0), kSahBins - 1);
+                bn[i]++;
+                grow(bb[i], tb[o]);
+            }
+            double ra[kSahBins];
+            int rn[kSahBins];
+            Box acc = empty_box();
+            int an = 0;
+            for (int i = kSahBins - 1; i > 0; --i) { grow(acc, bb[i]); an += bn[i]; ra[i] = area(acc); rn[i] = an; }
+            acc = empty_box();
+            an = 0;
+            for (int i = 0; i < kSahBins - 1; ++i) {
+                grow(acc, bb[i]);
+                an += bn[i];
+                if (an == 0 || rn[i + 1] == 0) continue;
+                const double c = area(acc) * an + ra[i + 1] * rn[i + 1];
+                if (c < best) { best = c; bax = ax; bsplit = i + 1; }
+            }
+        }
+        const double leaf_cost = (double)cnt, split_cost = kSahTraversal + best / std::max(area(n.box), 1e-300);
+        if (cnt <= kSahMaxLeaf && !(split_cost < leaf_cost)) { n.leaf = true; return; }
+        n.l = std::make_unique<BNode>();
+        n.r = std::make_unique<BNode>();
+        if (bax < 0) {  // every centroid in one point: halve the list
+            n.l->objs.assign(n.objs.begin(), n.objs.begin() + cnt / 2);
+            n.r->objs.assign(n.objs.begin() + cnt / 2, n.objs.end());
+        } else {
+            const double lo = cb.mn[bax], ext = cb.mx[bax] - cb.mn[bax];
+            for (int32_t o : n.objs) {
+                int i = (int)((cen[3 * (size_t)o + bax] - lo) / ext * kSahBins);
+                i = std::min(std::max(i, 0), kSahBins - 1);
+                (i < bsplit ? n.l : n.r)->objs.push_back(o);
+            }
+        }
+        std::vector<int32_t>().swap(n.objs);
+        build(*n.l, depth + 1);
+        build(*n.r, depth + 1);
+    }
+};
+
+}  // namespace
+
+extern "C" int pt_bvh_build_sah(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count,
+                                float* bvh_out, size_t bvh_cap, size_t* bvh_len) {
+    if (!vertices || !tris || !bvh_len || vertex_count == 0 || tri_count == 0 || (bvh_cap && !bvh_out))
+        return PT_ERR_INVALID;
+    std::vector<Box> tb(tri_count);
+    std::vector<double> cen(3 * tri_count);
+    for (size_t t = 0; t < tri_count; ++t) {
+        Box b = empty_box();
+        for (int v = 0; v < 3; ++v) {
+            const int32_t i = tris[4 * t + v];
+            if (i < 1 || (size_t)i > vertex_count) return PT_ERR_INVALID;
+            const double* p = vertices + 3 * (size_t)(i - 1);
+            for (int k = 0; k < 3; ++k) { b.mn[k] = std::min(b.mn[k], p[k]); b.mx[k] = std::max(b.mx[k], p[k]); }
+        }
+        tb[t] = b;
+        for (int k = 0; k < 3; ++k) cen[3 * t + k] = 0.5 * (b.mn[k] + b.mx[k]);
+    }
+    Box root{};
+    for (size_t i = 0; i < vertex_count; ++i)
+        for (int k = 0; k < 3; ++k) {
+            const double x = vertices[3 * i + k];
+            if (i == 0 || x <= root.mn[k]) root.mn[k] = x;
+            if (i == 0 || x >= root.mx[k]) root.mx[k] = x;
+        }
+    BNode top;
+    top.axis = 0;
+    top.objs.resize(tri_count);
+    for (size_t t = 0; t < tri_count; ++t) top.objs[t] = (int32_t)t;
+    SahBuilder{tb, std::move(cen)}.build(top, 1);
+    if (top.leaf) {  // the layout needs an internal root: two leaves under it
+        top.leaf = false;
+        top.l = std::make_unique<BNode>();
+        top.r = std::make_unique<BNode>();
+        top.l->leaf = top.r->leaf = true;
+        top.l->box = top.r->box = top.box;
+        top.l->objs.assign(top.objs.begin(), top.objs.begin() + top.objs.size() / 2);
+        top.r->objs.assign(top.objs.begin() + top.objs.size() / 2, top.objs.end());
+        if (top.l->objs.empty()) top.l->box = Box{};
+    }
+    std::vector<double> out(root.mn, root.mn + 3);
+    out.insert(out.end(), root.mx, root.mx + 3);
+    pack(top, tris, out);
+    if (out.size() >= (1u << 24)) return PT_ERR_INVALID;  // float offsets exact below 2^24 (packer.ts layout)
+    *bvh_len = out.size();
+    if (bvh_cap < out.size()) return bvh_cap ? PT_ERR_INVALID : PT_OK;
+    for (size_t i = 0; i < out.size(); ++i) bvh_out[i] = (float)out[i];
+    return PT_OK;
+}
+

@@ -1321,10 +1321,12 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     const bool bf = lo.bf != 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0;
     // k_wf_persist_bf (PT_PERSIST=1) measured slower: 1771 vs 2207 Msamples/s (its workgroups idle
     // at the per-iteration barrier once a region's queue is down to a few batches)
+    // big-leaf cooperation (+160) for lean<4..16> on scenes with leaves of >= big_leaf entries
+    const bool big = !bf && !mb && sc.big_leaf > 0 && base >= 5 && base <= 7 && !pipe && !ifif;
     const int trav = bf ? (lo.fuse == 0 ? 300 : lo.persist > 0 ? 500 : 400) + (fast ? 10 : 0)
                    : mb ? 100 + base + (fast ? 10 : 0)
                         : base + ((base >= 3 && fast) ? 10 : 0) + ((base >= 3 && fast && pipe) ? 20 : 0) +
-                              ((base >= 3 && fast && ifif && !pipe) ? 40 : 0);
+                              ((base >= 3 && fast && ifif && !pipe) ? 40 : 0) + (big ? 160 : 0);
 #define WF(L, T)                                                                                               \
     if (trav == T) {                                                                                           \
         if (count) return wf_render_t<L, T, true>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream, ws); \
@@ -1335,11 +1337,13 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
         WF(true, 13) WF(true, 14) WF(true, 15) WF(true, 16) WF(true, 17) WF(true, 18) WF(true, 35) WF(true, 36) WF(true, 37) WF(true, 55) WF(true, 56) WF(true, 57)
         WF(true, 300) WF(true, 310) WF(true, 400) WF(true, 410) WF(true, 500) WF(true, 510)
         WF(true, 105) WF(true, 106) WF(true, 107) WF(true, 115) WF(true, 116) WF(true, 117) WF(true, 118)
+        WF(true, 165) WF(true, 166) WF(true, 167) WF(true, 175) WF(true, 176) WF(true, 177)
     } else {
         WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
         WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18) WF(false, 35) WF(false, 36) WF(false, 37) WF(false, 55) WF(false, 56) WF(false, 57)
         WF(false, 300) WF(false, 310) WF(false, 400) WF(false, 410) WF(false, 500) WF(false, 510)
         WF(false, 105) WF(false, 106) WF(false, 107) WF(false, 115) WF(false, 116) WF(false, 117) WF(false, 118)
+        WF(false, 165) WF(false, 166) WF(false, 167) WF(false, 175) WF(false, 176) WF(false, 177)
     }
 #undef WF
     return hipErrorInvalidValue;

@@ -4,8 +4,10 @@
 // bench/tests).  Writes <out>/triangle_data.f32, <out>/bvh_data.f32 (little-endian f32,
 // the reference's SceneObjectPacked) and <out>/scene.json (meta[48], screenDimension,
 // camera, settings) plus <out>/meta.f32.  Usage: pt-pack.js <scene.ini|scene.xml> <out_dir> [--web-root DIR]
-//                            [--width W --height H --spp N --rr P --direct-only --native-bvh]
+//                            [--width W --height H --spp N --rr P --direct-only --native-bvh --all-meshes]
 // --native-bvh builds the BVH with the library's C++ builder (pt_bvh_build, byte-identical).
+// --all-meshes packs every primitive of the scene into one (the reference packs the first only).
+// --bvh sah builds the fast binned-SAH tree (same layout, not the reference's topology).
 const fs = require('fs');
 const path = require('path');
 const host = require('..');
@@ -16,12 +18,15 @@ function main(argv) {
         const a = argv[i];
         if (a === '--direct-only') args.direct_only = true;
         else if (a === '--native-bvh') args.native_bvh = true;
+        else if (a === '--all-meshes') args.all_meshes = true;
         else if (a.startsWith('--')) args[a.slice(2).replace(/-/g, '_')] = argv[++i];
         else args._.push(a);
     }
     if (args._.length < 2) { console.error('usage: pt-pack.js <scene.ini|scene.xml> <out_dir> [options]'); process.exit(2); }
     const [src, out] = args._;
-    const opts = { web_root: args.web_root, quiet: true, native_bvh: !!args.native_bvh };
+    const opts = { web_root: args.web_root, quiet: true, native_bvh: !!args.native_bvh, all_meshes: !!args.all_meshes,
+                   bvh: args.bvh || 'reference' };
+    if (opts.bvh !== 'reference' && opts.bvh !== 'sah') { console.error('--bvh reference|sah'); process.exit(2); }
     let loaded;
     if (src.endsWith('.ini')) loaded = host.load_scene_from_ini(src, opts);
     else {
@@ -48,7 +53,7 @@ function main(argv) {
         meta: Array.from(meta), screenDimension, settings: S, io: loaded.scene_description.IO,
         camera: { pos: loaded.camera_data.pos.toArray(), focus: loaded.camera_data.focus.toArray(),
             up: loaded.camera_data.up.toArray(), heightangle: loaded.camera_data.heightangle },
-        triangle_len: p.triangle_data.length, bvh_len: p.bvh_data.length,
+        triangle_len: p.triangle_data.length, bvh_len: p.bvh_data.length, meshes: loaded.meshes, bvh: opts.bvh,
     }, null, 1));
 }
 main(process.argv.slice(2));

@@ -2,7 +2,7 @@
 // Scene loading: INI -> XML (camera + object tree) -> first mesh -> OBJ/MTL -> packed
 // triangle buffer + f64 BVH -> packed BVH.  Mirrors src/index.ts:24-176 (browser XHR
 // replaced by fs; the canvas is gone).  Like the reference, only the FIRST primitive
-// of the traversal is packed (index.ts:116).
+// of the traversal is packed (index.ts:116) unless opts.all_meshes merges them all.
 const fs = require('fs');
 const path = require('path');
 const { parse_ini_file, ini_file_to_ini_scene } = require('./parse-ini');
@@ -79,7 +79,29 @@ function parse_scene_xml(scene_xml) {
 
 /** index.ts:128-161 for one primitive: SceneObjectPacked {triangle_data, bvh_data, bounds}. */
 function pack_primitive(obj_data, mtl_data, ctm, opts) {
-    const intermediate = parse_obj(obj_data, mtl_data, ctm);
+    return pack_group(parse_obj(obj_data, mtl_data, ctm), opts);
+}
+
+/** Several primitives (each parsed with its own CTM, parse-obj.ts:24's transform included) as ONE
+ * SceneObjectGroup: vertices concatenated, a later mesh's 1-based indices shifted by the vertices
+ * before it, objects (and their materials) in primitive order — so the emissive slots are the first
+ * four emissive objects over all meshes (packer.ts:65-68).  Vertex normals are laid out per vertex
+ * (each mesh's list cut or zero-padded to 3 per vertex) so that vn_start + (index - 1) * 3 still
+ * finds a vertex's normal (intersection-logic.wgsl:81-97). */
+function merge_groups(groups) {
+    const out = { vertices: [], vertex_normals: [], objects: [] };
+    for (const g of groups) {
+        const base = out.vertices.length / 3;
+        const nv = g.vertices.length / 3;
+        out.vertices.push(...g.vertices);
+        for (let i = 0; i < 3 * nv; i++) out.vertex_normals.push(i < g.vertex_normals.length ? g.vertex_normals[i] : 0);
+        for (const o of g.objects) out.objects.push(Object.assign({}, o, { indices: o.indices.map((v) => v + base) }));
+    }
+    return out;
+}
+
+/** SceneObjectGroup -> SceneObjectPacked (index.ts:130-161). */
+function pack_group(intermediate, opts) {
     for (const o of intermediate.objects)
         if (!o.material) throw TypeError(`material '${o.name}' is not defined in the MTL file`);
     const packed_array = pack_scene_object_group(intermediate);
@@ -94,10 +116,12 @@ function pack_primitive(obj_data, mtl_data, ctm, opts) {
             bvh_objects.push({ obj: [ind[i], ind[i + 1], ind[i + 2], mat_i], bounds: bounds_of_vec3(tri) });
         }
     });
-    if (opts && opts.native_bvh) {  // the same build in C++ (pt_bvh_build), byte-identical, for big meshes
+    // native_bvh: the same build in C++ (pt_bvh_build), byte-identical, for big meshes; bvh 'sah':
+    // the fast binned-SAH tree (pt_bvh_build_sah) in the same layout — not the reference's topology
+    if (opts && (opts.native_bvh || opts.bvh === 'sah')) {
         const tris = new Int32Array(bvh_objects.length * 4);
         bvh_objects.forEach((o, t) => tris.set(o.obj, 4 * t));
-        const bvh_data = require('./addon').load().bvhBuild(Float64Array.from(vertices), tris);
+        const bvh_data = require('./addon').load().bvhBuild(Float64Array.from(vertices), tris, opts.bvh === 'sah');
         return { triangle_data: packed_array, bvh_data, bounds: bvh_bounds };
     }
     const bvh = new BVH(bvh_objects, bvh_bounds, opts);
@@ -132,14 +156,21 @@ function load_scene_xml_file(scene_path, opts) {
     const web_root = opts.web_root || path.resolve(path.dirname(scene_path), '..');
     const load_file = opts.load_file || make_loader(web_root);
     const { camera_data, final_primitives } = parse_scene_xml(load_file(scene_path));
-    const primitive_data = final_primitives.slice(0, 1).map((p) => {
+    const popts = { quiet: opts.quiet !== false, native_bvh: !!opts.native_bvh, bvh: opts.bvh };
+    const parse = (p) => {
         if (!p.data) throw Error('mesh primitive missing its data');
         const obj_data = load_file(p.data.path);
         let mtl_data;
         try { mtl_data = load_file(p.data.path.slice(0, -3) + 'mtl'); } catch (e) { mtl_data = ''; }
-        return pack_primitive(obj_data, mtl_data, p.ctm, { quiet: opts.quiet !== false, native_bvh: !!opts.native_bvh });
-    });
-    return { primitive_data, camera_data };
+        return parse_obj(obj_data, mtl_data, p.ctm);
+    };
+    // opts.all_meshes: every primitive of the scene in one packed scene (SURVEY.md §8(f) row 1); the
+    // default is the reference's first primitive only (index.ts:116)
+    const primitive_data = opts.all_meshes
+        ? [pack_group(merge_groups(final_primitives.map(parse)), popts)]
+        : final_primitives.slice(0, 1).map((p) => pack_group(parse(p), popts));
+    return { primitive_data, camera_data, meshes: opts.all_meshes ? final_primitives.length : Math.min(1, final_primitives.length) };
 }
 
-module.exports = { parse_scene_xml, pack_primitive, screen_dimension, load_scene_from_ini, load_scene_xml_file };
+module.exports = { parse_scene_xml, pack_primitive, pack_group, merge_groups, screen_dimension, load_scene_from_ini,
+                   load_scene_xml_file };

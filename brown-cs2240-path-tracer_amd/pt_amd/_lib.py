@@ -96,6 +96,7 @@ def load_library():
     L.pt_profile_select.argtypes = [p, ctypes.c_char_p]
     L.pt_selftest_rcp.argtypes = [i, i, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
     L.pt_bvh_build.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
+    L.pt_bvh_build_sah.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_tonemap_async.argtypes = [p, p, sz, u32, p, p]
     L.pt_render_image.argtypes = [p, p, u32, u32, u32, i, i, p, p]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
@@ -103,7 +104,7 @@ def load_library():
     L.pt_scene_check.argtypes = [p]
     L.pt_render_multi.argtypes = [ctypes.POINTER(p), i, p, u32, u32, u32, i, i, p, p]
     L.pt_set_hw_queues.argtypes = [i]
-    for fn in ("pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+    for fn in ("pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
                "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
@@ -298,14 +299,16 @@ def selftest_rcp(steps: int = -1, lo_bits: int = 0x00800000, hi_bits: int = 0x7E
     return int(m.value), int(b.value)
 
 
-def bvh_build(vertices, tris) -> np.ndarray:
+def bvh_build(vertices, tris, sah: bool = False) -> np.ndarray:
     """Native BVH build + pack (host only, no GPU): vertices f64 [n, 3] (post-CTM), tris
-    int32 [m, 4] = (i0, i1, i2, material) with 1-based vertex indices -> packed bvh_data (f32)."""
+    int32 [m, 4] = (i0, i1, i2, material) with 1-based vertex indices -> packed bvh_data (f32).
+    sah=True: the fast binned-SAH tree (pt_bvh_build_sah), same layout, not the reference's tree."""
     L = load_library()
+    fn = L.pt_bvh_build_sah if sah else L.pt_bvh_build
     v = np.ascontiguousarray(vertices, dtype=np.float64).reshape(-1)
     t = np.ascontiguousarray(tris, dtype=np.int32).reshape(-1)
     n = ctypes.c_size_t(0)
-    _check(L.pt_bvh_build(_ptr(v), v.size // 3, _ptr(t), t.size // 4, None, 0, ctypes.byref(n)))
+    _check(fn(_ptr(v), v.size // 3, _ptr(t), t.size // 4, None, 0, ctypes.byref(n)))
     out = np.empty(n.value, np.float32)
-    _check(L.pt_bvh_build(_ptr(v), v.size // 3, _ptr(t), t.size // 4, _ptr(out), out.size, ctypes.byref(n)))
+    _check(fn(_ptr(v), v.size // 3, _ptr(t), t.size // 4, _ptr(out), out.size, ctypes.byref(n)))
     return out

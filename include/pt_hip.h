@@ -188,6 +188,14 @@ int pt_render_image(pt_scene* scene, const float meta[48], uint32_t frame0, uint
 int pt_bvh_build(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count, float* bvh_out,
                  size_t bvh_cap, size_t* bvh_len);
 
+/* Fast BVH build (SURVEY.md §8(f) row 2's flagged mode; gives up topology parity with the
+ * reference's builder): binned SAH over triangle centroids, each triangle in one leaf of at most 8
+ * (depth-capped), tight child boxes, written in the same packed layout (src/packer.ts:83-137) so the
+ * unchanged traversal runs on it.  Same arguments and size query as pt_bvh_build; fails with
+ * PT_ERR_INVALID when the packed buffer would exceed 2^24 floats (offsets are stored as f32). */
+int pt_bvh_build_sah(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count, float* bvh_out,
+                     size_t bvh_cap, size_t* bvh_len);
+
 /* Kernel timing (no counterpart in the reference, which has no GPU timing): while enabled,
  * every kernel the scene launches is bracketed by two HIP events on the launch stream (no
  * synchronisation, a few microseconds per launch).  enable != 0 also discards earlier

@@ -480,9 +480,30 @@ class PackedScene:
     stats: dict = field(default_factory=dict)
 
 
+def merge_groups(groups: list) -> dict:
+    """Several parsed primitives as one SceneObjectGroup (the Node host's all-meshes mode,
+    SURVEY.md §8(f) row 1): vertices concatenated, later meshes' 1-based indices shifted by the
+    vertices before them, objects in primitive order, vertex normals laid out 3 per vertex (each
+    mesh's list cut or zero-padded) so vn_start + (index - 1) * 3 finds a vertex's normal."""
+    out = {"vertices": [], "vertex_normals": [], "objects": []}
+    for g in groups:
+        base = len(out["vertices"]) // 3
+        nv = len(g["vertices"]) // 3
+        out["vertices"].extend(g["vertices"])
+        vn = g["vertex_normals"]
+        out["vertex_normals"].extend([vn[i] if i < len(vn) else 0 for i in range(3 * nv)])
+        for o in g["objects"]:
+            out["objects"].append(dict(o, indices=[v + base for v in o["indices"]]))
+    return out
+
+
 def pack_primitive(obj_text: str, mtl_text: str, ctm, live_strides: bool = False) -> PackedScene:
     """index.ts:128-161 for one primitive."""
-    g = parse_obj(obj_text, mtl_text, ctm)
+    return pack_group(parse_obj(obj_text, mtl_text, ctm), live_strides)
+
+
+def pack_group(g: dict, live_strides: bool = False) -> PackedScene:
+    """SceneObjectGroup -> SceneObjectPacked (index.ts:130-161)."""
     tri = pack_scene_object_group(g)
     V = g["vertices"]
     verts = [V[i:i + 3] for i in range(0, len(V), 3)]
@@ -501,23 +522,28 @@ def pack_primitive(obj_text: str, mtl_text: str, ctm, live_strides: bool = False
     return PackedScene(tri, bvh, bmin, bmax, bvh_stats(root))
 
 
-def load_scene(scene_xml_path: str, asset_root: str, live_strides: bool = False):
-    """Loads the XML, packs the FIRST primitive (index.ts:116), returns (camera, PackedScene)."""
+def load_scene(scene_xml_path: str, asset_root: str, live_strides: bool = False, all_meshes: bool = False):
+    """Loads the XML, packs the FIRST primitive (index.ts:116) — or, all_meshes, every primitive
+    merged into one (merge_groups) — and returns (camera, PackedScene)."""
     import os
     with open(scene_xml_path) as f:
         camera, prims = load_scene_xml(f.read())
     if not prims:
         raise ValueError("scene has no primitives")
-    p = prims[0]
-    path = os.path.join(asset_root, p["path"].lstrip("/").split("/", 1)[1])
-    with open(path) as f:
-        obj_text = f.read()
-    try:
-        with open(path[:-3] + "mtl") as f:
-            mtl_text = f.read()
-    except OSError:
-        mtl_text = ""
-    return camera, pack_primitive(obj_text, mtl_text, p["ctm"], live_strides=live_strides)
+
+    def parse(p):
+        path = os.path.join(asset_root, p["path"].lstrip("/").split("/", 1)[1])
+        with open(path) as f:
+            obj_text = f.read()
+        try:
+            with open(path[:-3] + "mtl") as f:
+                mtl_text = f.read()
+        except OSError:
+            mtl_text = ""
+        return parse_obj(obj_text, mtl_text, p["ctm"])
+
+    g = merge_groups([parse(p) for p in prims]) if all_meshes else parse(prims[0])
+    return camera, pack_group(g, live_strides)
 
 
 # ----------------------------------------------------------------------------

@@ -1,11 +1,3 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r02f_kt -o run -- python3 scripts/env_ab.py --reps 1 PT_REGEN=0,PT_PARTS=1 PT_REGEN=1,PT_PARTS=1 > gpurun_out/r02f_kt.log 2>&1; rc=$?
-grep -h '^{' gpurun_out/r02f_kt.log; python3 - <<'PY'
-import csv, glob
-for f in glob.glob("gpurun_out/r02f_kt/**/*kernel_stats.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        if "wf_" in r["Name"]:
-            print(r["Name"].split("(")[0][:90], r["Calls"], round(float(r["AverageNs"])/1e3,1), "us avg", round(float(r["TotalDurationNs"])/1e6,2), "ms total")
-PY
-exit $rc
+timeout -k 10 600 python -u scripts/env_ab.py --scene MedievalBoat --width 1920 --height 1080 --spp 2 --depth 16 --reps 1 PT_BIG_LEAF=0 PT_BIG_LEAF=1000,PT_BIG_RATIO=64,PT_BIG_MODE=1 PT_BIG_LEAF=1000,PT_BIG_RATIO=1,PT_BIG_MODE=1 PT_BIG_LEAF=0,PT_PIPE=1 PT_BIG_LEAF=0,PT_TRAV=lean8 PT_BIG_LEAF=0,PT_TRAV=lean32 PT_BIG_LEAF=0,PT_NODE_BIAS=1 2>&1 | tee gpurun_out/r02j_ab.log

@@ -72,12 +72,22 @@ KERNELS = {
     "wavefront_gen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1"},
     "wavefront_nogen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "0"},
     "wavefront_gen_cull_1block": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1", "PT_CULL": "2", "PT_WF_TRACE_BLOCKS": "1"},
+    # big-leaf cooperation (MedievalBoat by default; forced onto small leaves: every scene, many turns)
+    "wavefront_big8": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0"},
+    "wavefront_big4_ratio4_lean8_div": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_BIG_RATIO": "4",
+                                         "PT_TRAV": "lean8", "PT_FASTRCP": "0", "PT_MAILBOX": "0"},
+    "wavefront_nobig": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "0"},
+    # streaming path regeneration (opt-in): one and four parts, a small in-flight target
+    "wavefront_regen": {"PT_KERNEL": "wavefront", "PT_REGEN": "1"},
+    "wavefront_regen_4parts_small": {"PT_KERNEL": "wavefront", "PT_REGEN": "1", "PT_PARTS": "4",
+                                     "PT_REGEN_TARGET": "4096"},
 }
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
-            "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET")
+            "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
+            "PT_BIG_LEAF", "PT_BIG_RATIO", "PT_TRACE_WATCHDOG", "PT_REDUCE")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -479,3 +489,28 @@ def test_entry_cull_full_size(packed, monkeypatch, scene):
     assert same_bits(out["2"], out["0"]), mismatch_report(out["2"], out["0"])
     assert same_bits(out["99"], out["0"]), mismatch_report(out["99"], out["0"])
     assert same_bits(out["gen0"], out["gen1"]), mismatch_report(out["gen0"], out["gen1"])
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-mesh scene (Node host --all-meshes): CornellBox2 = Cornell box + MedievalBoat
+# ---------------------------------------------------------------------------------------------
+@pytest.fixture(scope="session")
+def packed_multi(tmp_path_factory):
+    from conftest import SCENES, pack_with_node
+    import os
+    return pack_with_node(os.path.join(SCENES, "scene_assets", "CornellBox2.xml"),
+                          str(tmp_path_factory.mktemp("multi") / "cb2"), "--all-meshes", "--native-bvh")
+
+
+@pytest.mark.parametrize("env", [{}, {"PT_KERNEL": "wavefront"}, {"PT_KERNEL": "mega"}])
+def test_multi_mesh_frame_bitexact(packed_multi, monkeypatch, env):
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = packed_multi
+    meta = p.meta_for(32, 24)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        gpu = s.frame(meta, 5, 8)
+    ref, _ = oracle.frame(p.triangle_data, p.bvh_data, meta, 5, 8)
+    assert same_bits(gpu, ref), mismatch_report(gpu, ref)

@@ -201,3 +201,25 @@ require("fs").writeFileSync({json.dumps(str(out))}, h.encode_png(px, W, H));''')
     img = np.array(Image.open(out))
     assert img.shape == (3, 5, 4)
     assert np.array_equal(img.reshape(-1), (np.arange(60) * 37) & 255)
+
+
+def test_multi_mesh_buffers_match_oracle(tmp_path):
+    """--all-meshes: every primitive of CornellBox2.xml (the Cornell box and
+    the MedievalBoat under its own CTM, parse-obj.ts:24's transform per mesh) merged into one scene,
+    byte-identical to the oracle's restatement; without the flag only the first primitive, as
+    index.ts:116."""
+    import scene_oracle as so
+    xml = os.path.join(SCENES, "scene_assets", "CornellBox2.xml")
+    assets = os.path.join(SCENES, "scene_assets")
+    multi = pack_with_node(xml, str(tmp_path / "multi"), "--all-meshes", "--native-bvh")
+    first = pack_with_node(xml, str(tmp_path / "first"))
+    _, om = so.load_scene(xml, assets, all_meshes=True)
+    _, of = so.load_scene(xml, assets)
+    assert multi.info["meshes"] == 2 and first.info["meshes"] == 1
+    assert multi.triangle_data.tobytes() == om.triangle_data.tobytes()
+    assert multi.bvh_data.tobytes() == om.bvh_data.tobytes()
+    assert first.triangle_data.tobytes() == of.triangle_data.tobytes()
+    assert first.bvh_data.tobytes() == of.bvh_data.tobytes()
+    # the merged scene holds both meshes: 72 + 15222 vertices, 36 + 12573 triangles
+    tri = multi.triangle_data
+    assert int(tri[0]) == 72 + 15222 and (int(tri[4]) - int(tri[3])) // 4 == 36 + 12573
