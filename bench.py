@@ -125,6 +125,48 @@ def metric_name(scene: str, W: int, H: int, depth: int) -> str:
     return f"Msamples/s (paths/s) {scene} {W}x{H} depth {depth}"
 
 
+def native_multi(args):
+    """bench.py --native-multi --gpus N: ONE process renders the step over N devices with the C ABI's
+    pt_render_multi (frames dealt round-robin, one host thread per device, one ncclReduce onto
+    device 0 inside the library).  Host-buffer call: the accumulator upload and read-back (12 MB
+    each way at 1024^2) over PCIe are inside the timed step."""
+    import pt_amd
+    n = max(1, args.gpus)
+    if args.synthetic:
+        args.scene = f"synthetic-{args.synthetic}"
+    with tempfile.TemporaryDirectory() as td:
+        tri, bvh, meta = pack_scene(args.scene, td, args.width, args.height, args.spp, args.synthetic, args.bvh,
+                                    args.all_meshes)
+    W, H = int(meta[0]), int(meta[1])
+    mode = {"auto": pt_amd.MODE_AUTO, "megakernel": pt_amd.MODE_MEGAKERNEL, "wavefront": pt_amd.MODE_WAVEFRONT}[args.mode]
+    scenes = [pt_amd.Scene(tri, bvh, device=g) for g in range(n)]
+    acc = np.zeros((H, W, 3), np.float32)
+    for _ in range(args.warmup):
+        acc[:] = 0
+        pt_amd.render_multi(scenes, meta, 0, args.spp, 1, args.depth, mode, accum=acc)
+    t = []
+    for _ in range(args.steps):
+        acc[:] = 0
+        t0 = time.perf_counter()
+        pt_amd.render_multi(scenes, meta, 0, args.spp, 1, args.depth, mode, accum=acc)
+        t.append(time.perf_counter() - t0)
+    for s in scenes:
+        s.close()
+    elapsed = float(np.sum(t))
+    total = W * H * args.spp
+    out = {"metric": metric_name(args.scene, W, H, args.depth), "value": round(total / (elapsed / args.steps) / 1e6, 3),
+           "unit": "Msamples/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "f32",
+           "data": f"synthetic (reference {args.scene}.xml scene packed by the Node host; RNG salts t_k = k)",
+           "config": {"workload": f"{args.scene}.xml {W}x{H} {args.spp}spp depth {args.depth}, rr 0.9, frames dealt "
+                                  f"round-robin over {n} devices in one process (pt_render_multi), host accumulator "
+                                  f"(PCIe upload + read-back in the step)",
+                      "mode": args.mode, "samples_per_step": total,
+                      "reduce": os.environ.get("PT_REDUCE", "rccl" if n > 1 else "none")}}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -139,6 +181,8 @@ def main():
     ap.add_argument("--synthetic", type=int, default=0, help="N-triangle synthetic Cornell-sized scene (BVH sweep)")
     ap.add_argument("--bvh", default="reference", choices=["reference", "sah"], help="sah: the fast (non-parity) tree")
     ap.add_argument("--all-meshes", action="store_true", help="every primitive of the scene (reference: first only)")
+    ap.add_argument("--native-multi", action="store_true",
+                    help="one process drives --gpus devices through pt_render_multi (RCCL reduce inside the library)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch HIP events")
     args = ap.parse_args()
@@ -150,6 +194,10 @@ def main():
     from pt_amd.shard import frames_for_rank, reduce_accum
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.native_multi:
+        if world != 1:
+            raise SystemExit("--native-multi is single-process (it drives --gpus devices itself)")
+        return native_multi(args)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

@@ -752,15 +752,11 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     } prof_scope(s->prof_on ? &s->prof : nullptr);
     SceneView view = s->view;
     if (const char* e = std::getenv("PT_NODE_BIAS")) view.node_bias = std::max(1, std::atoi(e));  // A/B runs
-    // big-leaf cooperation (lean traversal): leaves of >= PT_BIG_LEAF entries (default 64; 0 = off)
+    // big leaves in step (lean traversal): leaves of >= PT_BIG_LEAF entries (0 = off, the default)
     {
-        int big = 64, ratio = 1;
+        int big = 0;
         if (const char* e = std::getenv("PT_BIG_LEAF")) big = std::max(0, std::atoi(e));
-        if (const char* e = std::getenv("PT_BIG_RATIO")) ratio = std::max(1, std::atoi(e));
         view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? big : 0;
-        view.big_ratio = ratio;
-        view.big_mode = 0;
-        if (const char* e = std::getenv("PT_BIG_MODE")) view.big_mode = std::atoi(e);
     }
     if (lo.wavefront) {
         uint64_t target = kWfTargetPaths;

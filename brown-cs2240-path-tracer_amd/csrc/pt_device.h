@@ -278,13 +278,17 @@ __device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r
 // lanes reject at the same step, which practically never happens), each unit is one exec
 // region and the push/pop decision is straight-line (stack[sp] is the free slot above the
 // top: max_stack = max depth + 1, pt_capi.hip).  Same units, same order, same arithmetic.
-enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8, TF_BCUR = 16, TF_PARK = 32 };
+enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8, TF_BCUR = 16 };
 struct TravLean {
     int node, sp, k, na, nt, la, lb, fl, best;
     float ld, rd, best_t;
     uint64_t tested, rem;  // mailbox flavours only: uids tested by this query / left in this pair
+    int rot;               // big-leaf flavour: rotation of the big leaf being walked
+    uint32_t step;         // big-leaf flavour: the wave's leaf-test step counter (same in every lane)
 };
 __device__ __forceinline__ void trav_init(TravLean& s, bool active) {
+    s.rot = 0;
+    if (!active) s.step = 0;  // a kernel's first (inactive) init; later queries keep the wave's count
     s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1;
     s.fl = active ? 0 : TF_DONE;
     s.ld = 0.0f; s.rd = 0.0f; s.best_t = -1.0f;
@@ -314,34 +318,42 @@ __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r
     return s.nt == 0;  // no leaf to test: decide now
 }
 
-// Big-leaf cooperation (BIG; SceneView::big_leaf): a lane whose next entry starts a leaf of at
-// least big_leaf entries parks there (TF_PARK) instead of walking it alone, and stops a leaf turn
-// at the start of such a leaf; big_seg() gives the parked leaf (first record, entry count).
-__device__ __forceinline__ bool big_at(const SceneView& sc, const TravLean& s) {
-    return (s.k < s.na) ? (s.k == 0 && s.na >= sc.big_leaf) : (s.k == s.na && s.k < s.nt && s.nt - s.na >= sc.big_leaf);
-}
-__device__ __forceinline__ void big_seg(const TravLean& s, int& rec0, int& n) {
-    const bool left = s.k < s.na;
-    rec0 = left ? s.la : s.lb;
-    n = left ? s.na : s.nt - s.na;
-}
-
+// Big leaves in step (BIG; SceneView::big_leaf): a lane in a leaf of at least big_leaf entries
+// walks it in a rotated order that is the same for every lane of the wave in that leaf — entry
+// (rot + i) mod n at its i-th test, rot = the wave's test-step counter mod n when the lane enters
+// the leaf — so the lanes in one big leaf read the same record at the same step (one cache line
+// instead of a gather per lane; the steps of a leaf turn advance the counter for every lane).
+// The leaf's result must be the FIRST entry in leaf order among those with the smallest t (the
+// reference's sequential strict-< loop); out of order that is: take a hit when t < best_t, or when
+// t == best_t and the best is an earlier entry of this same leaf (a leaf is tested once per query,
+// so a best inside the leaf's record range was taken in this walk).  An equal t from an earlier
+// leaf is never replaced, as in order.
 template <int K, bool COUNT, bool FAST_RCP, bool PIPE, bool BIG = false>
 __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
-    if constexpr (BIG) {  // park at a big leaf: now, or where this turn would enter it
-        if (big_at(sc, s)) { s.fl |= TF_PARK; return false; }
-    }
-    // a turn of lanes with a big right leaf stops at its start (they park below)
-    const int lim = (BIG && s.k < s.na && s.nt - s.na >= sc.big_leaf) ? s.na : s.nt;
     if constexpr (!PIPE) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const bool live = j == 0 || s.k < lim;   // the first test always is
+            const bool live = j == 0 || s.k < s.nt;  // the first test always is
             if (j > 0 && !__any(live)) break;        // every lane's leaf pair is done
-            const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+            int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+            bool big = false;
+            int seg0 = 0, segn = 0;
+            if constexpr (BIG) {
+                const bool left = s.k < s.na;
+                seg0 = left ? s.la : s.lb;
+                segn = left ? s.na : s.nt - s.na;
+                const int i = left ? s.k : s.k - s.na;  // position in the leaf
+                big = segn >= sc.big_leaf;
+                if (big && i == 0) s.rot = (int)((s.step + (uint32_t)j) % (uint32_t)segn);
+                int e = s.rot + i;
+                e -= (e >= segn) ? segn : 0;
+                idx = big ? seg0 + e : idx;
+            }
             float t;
-            const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
-                              ((s.best_t < 0.0f) | (t < s.best_t));
+            const bool hit = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live;
+            bool take = hit & ((s.best_t < 0.0f) | (t < s.best_t));
+            if constexpr (BIG)
+                take |= hit & big & (t == s.best_t) & (s.best >= seg0) & (s.best < seg0 + segn) & (idx < s.best);
             s.best_t = take ? t : s.best_t;
             s.best = take ? idx : s.best;
             if (COUNT) cnt.tri_tests += live ? 1 : 0;
@@ -371,64 +383,7 @@ __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r
     }
     const bool decide = s.k == s.nt;
     s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
-    if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
     return decide;
-}
-
-__device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int stride);
-
-// One cooperative turn: the parked lanes of the wave's first parked leaf test its entries
-// together, in entry order, each against its own closest t (the strict-< update of the leaf
-// loop, so each lane's result is the one its own walk would give).  Records are loaded 64 at a
-// time, one per lane (a coalesced load instead of one gather per lane and entry), and broadcast
-// with v_readlane.  Returns after the leaf; lanes whose pair ended decide.
-template <bool COUNT, bool FAST_RCP>
-__device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, int32_t* stack,
-                                         int stride, Counters& cnt) {
-    int my0 = 0, myn = 0;
-    big_seg(s, my0, myn);
-    const int f = (int)__builtin_ctzll(parked);
-    const int rec0 = __builtin_amdgcn_readlane(my0, f), n = __builtin_amdgcn_readlane(myn, f);
-    const bool mine = ((s.fl & TF_PARK) != 0) & (my0 == rec0);
-    const uint32_t lane = threadIdx.x & 63u;
-    if (sc.big_mode == 1) {  // records through the scalar cache (uniform address: s_load)
-        for (int j = 0; j < n; ++j) {
-            const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(sc.tris + rec0 + j);
-            const TriRec tr{make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]), f[8]};
-            if (mine) {
-                float t;
-                const bool take = tri_hit<FAST_RCP>(tr, r, t) & ((s.best_t < 0.0f) | (t < s.best_t));
-                s.best_t = take ? t : s.best_t;
-                s.best = take ? rec0 + j : s.best;
-            }
-        }
-    } else
-    for (int c = 0; c < n; c += 64) {
-        const int m = min(64, n - c);
-        TriRec own = load_tri(sc.tris, rec0 + c + ((int)lane < m ? (int)lane : 0));
-        for (int j = 0; j < m; ++j) {
-            auto bc = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j)); };
-            const TriRec tr{make_float4(bc(own.a.x), bc(own.a.y), bc(own.a.z), bc(own.a.w)),
-                            make_float4(bc(own.b.x), bc(own.b.y), bc(own.b.z), bc(own.b.w)), bc(own.c)};
-            if (mine) {
-                float t;
-                const bool take = tri_hit<FAST_RCP>(tr, r, t) & ((s.best_t < 0.0f) | (t < s.best_t));
-                s.best_t = take ? t : s.best_t;
-                s.best = take ? rec0 + c + j : s.best;
-            }
-        }
-    }
-    if (mine) {
-        if (COUNT) cnt.tri_tests += n;
-        s.k += n;
-        s.fl &= ~TF_PARK;
-        if (s.k == s.nt) {
-            s.fl &= ~TF_LEAF;
-            lean_decide(s, stack, stride);
-        } else if (big_at(sc, s)) {
-            s.fl |= TF_PARK;  // its right leaf is big too
-        }
-    }
 }
 
 __device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int stride) {
@@ -450,17 +405,9 @@ __device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int str
 template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false, bool IFIF = false, bool BIG = false>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
                                                int stride, Counters& cnt) {
-    const int state = s.fl & (TF_LEAF | TF_DONE | (BIG ? TF_PARK : 0));
+    const int state = s.fl & (TF_LEAF | TF_DONE);
     const uint64_t want_leaf = __ballot(state == TF_LEAF);
     const uint64_t want_node = __ballot(state == 0);
-    if constexpr (BIG) {
-        const uint64_t parked = __ballot((state & TF_PARK) != 0);
-        if (parked && (((want_leaf | want_node) == 0) ||
-                       __popcll(parked) * sc.big_ratio >= __popcll(want_leaf | want_node))) {  // wave-uniform
-            big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);
-            return true;
-        }
-    }
     if ((want_leaf | want_node) == 0) return false;
     bool decide = false;
     if constexpr (IFIF) {
@@ -470,9 +417,11 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     } else {
         if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
             if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE, BIG>(sc, r, s, cnt);
+            // every lane still in a big leaf ran all K steps of the turn (the turn ends early only
+            // when no lane is live), so the wave's step counter advances by K for all lanes alike
+            if constexpr (BIG) s.step += K;
         } else if (state == 0) {
             decide = lean_node_unit<COUNT>(sc, r, s, cnt);
-            if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
         }
     }
     if (decide) lean_decide(s, stack, stride);

@@ -104,12 +104,9 @@ struct SceneView {
     // (pt_capi.hip build_layout); cull_its = the wavefront launches that use it (it < cull_its)
     const float4* cull;
     int32_t cull_its;
-    // big-leaf cooperation (lean traversal, TRAV + 200): leaves of at least big_leaf entries are
-    // tested by the lanes of a wave together, records broadcast from registers (0 = off);
-    // big_ratio: a cooperative turn runs once parked lanes x big_ratio >= the wave's other lanes
+    // big leaves in step (lean traversal, TRAV + 160): the lanes of a wave walk a leaf of at least
+    // big_leaf entries in one shared rotated order (lean_leaf_loop; 0 = off)
     int32_t big_leaf;
-    int32_t big_ratio;
-    int32_t big_mode;  // 0: records broadcast with v_readlane, 1: through the scalar cache
     // the distinct entries in pairs for phase 1's packed-f32 test (mailbox scenes): pair j =
     // entries 2j, 2j+1 as 20 floats {v0.x of 2j, v0.x of 2j+1, v0.y, v0.y, ..., e2.z, e2.z, 0, 0};
     // an odd count ends with an all-zero entry (det = 0: never a hit)

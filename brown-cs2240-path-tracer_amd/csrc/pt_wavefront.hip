@@ -134,8 +134,17 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 // contiguous chunk is an image region whose cost differs systematically from the others.
 // Inside a wave, window j's entries have the wave-local sequence numbers 32j .. 32j+31, which
 // index the hit ring.
+// PT_TRACE_WAVES (build-time A/B): cap the traversal kernel's VGPRs for this many waves per SIMD
+#ifndef PT_TRACE_WAVES
+#define PT_TRACE_WAVES 0
+#endif
+#if PT_TRACE_WAVES > 0
+#define PT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES, PT_TRACE_WAVES)))
+#else
+#define PT_TRACE_OCC
+#endif
 template <bool LDS, int TRAV, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
+__global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
                                                           uint32_t watchdog) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;

@@ -72,10 +72,10 @@ KERNELS = {
     "wavefront_gen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1"},
     "wavefront_nogen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "0"},
     "wavefront_gen_cull_1block": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1", "PT_CULL": "2", "PT_WF_TRACE_BLOCKS": "1"},
-    # big-leaf cooperation (MedievalBoat by default; forced onto small leaves: every scene, many turns)
+    # big leaves walked in step (opt-in; forced onto small leaves: every scene, many big-leaf walks)
     "wavefront_big8": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0"},
-    "wavefront_big4_ratio4_lean8_div": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_BIG_RATIO": "4",
-                                         "PT_TRAV": "lean8", "PT_FASTRCP": "0", "PT_MAILBOX": "0"},
+    "wavefront_big4_lean8_div": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_TRAV": "lean8", "PT_FASTRCP": "0",
+                                 "PT_MAILBOX": "0"},
     "wavefront_nobig": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "0"},
     # streaming path regeneration (opt-in): one and four parts, a small in-flight target
     "wavefront_regen": {"PT_KERNEL": "wavefront", "PT_REGEN": "1"},
