@@ -1,18 +1,26 @@
 #!/bin/bash
-# BASELINE.json configs 3 and 4 (other scenes) at reduced spp: one bench line each.
+# BASELINE.json configs[2..3] at their stated spp (depth 16, the reference default) plus the fast
+# SAH tree of the same scenes: one bench line each -> gpurun_out/profiles/<TAG>_configs.jsonl
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-OUT=gpurun_out/configs.jsonl
+TAG=${1:-r02}
+OUT=gpurun_out/profiles/${TAG}_configs.jsonl
+mkdir -p gpurun_out/profiles
 : > $OUT
-for args in "--scene CornellBox-Mirror --spp 64 --depth 16" "--scene CornellBox-Glossy --spp 64 --depth 16" \
-            "--scene MedievalBoat --width 1920 --height 1080 --spp 16 --depth 16"; do
-  timeout -k 10 300 python bench.py $args --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/cfg.log 2>&1
-  rc=$?; if [ $rc -ne 0 ]; then tail -5 gpurun_out/cfg.log; exit $rc; fi
-  grep "^{" gpurun_out/cfg.log >> $OUT
-done
-python3 -c "
-import json
-for l in open('$OUT'):
-    d=json.loads(l); r=d['roofline']; print(d['config']['workload'], d['value'], r['kernel'], r.get('kernels_ms_warmup_step'))"
+run() {
+  timeout -k 10 600 python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/cfg.log 2>&1
+  rc=$?; echo "config $* rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  grep -h '^{' gpurun_out/cfg.log >> $OUT
+}
+run --scene CornellBox-Mirror --spp 1024 --depth 16
+run --scene CornellBox-Glossy --spp 1024 --depth 16
+run --scene CornellBox-Glossy --spp 1024 --depth 16 --bvh sah
+run --scene MedievalBoat --width 1920 --height 1080 --spp 512 --depth 16
+run --scene MedievalBoat --width 1920 --height 1080 --spp 512 --depth 16 --bvh sah
+python3 - "$OUT" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l); r = d["roofline"]
+    print(d["metric"], d["config"]["bvh"], d["value"], "Msamples/s", r["kernel"], "frac", r["frac"])
+PY
