@@ -64,6 +64,8 @@ struct HostLayout {
     std::vector<float4> tnorm;    // vertex-normal mode: 3 per record (SceneView::tnorm)
     std::vector<float4> cull;     // mailbox scenes: 3 per distinct entry (SceneView::cull)
     std::vector<float> bfpair;    // mailbox scenes: 20 per pair of distinct entries (SceneView::bfpair)
+    std::vector<BfNode> bfnode;   // mailbox scenes with <= 64 internal nodes, <= 63 entries (SceneView::bfnode)
+    std::vector<int32_t> bfmap;
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -248,6 +250,31 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             L.lmask.assign(std::max<size_t>(1, entry.size()), 0);
             for (const auto& lr : leaf_ranges)
                 for (int32_t k = 0; k < lr.second; ++k) L.lmask[(size_t)lr.first] |= 1ull << uid[(size_t)(lr.first + k)];
+            // the stackless replay tree (BfNode): internal nodes in the reference's visiting
+            // order — pre-order with the right subtree first — so the next node to visit is always
+            // the smallest-numbered pending one
+            if (U <= 63 && L.nodes.size() <= 64) {
+                std::vector<int32_t> pre(L.nodes.size(), -1);
+                std::vector<int32_t> st{0};
+                int32_t next = 0;
+                while (!st.empty()) {
+                    const int32_t n = st.back();
+                    st.pop_back();
+                    pre[(size_t)n] = next++;
+                    L.bfmap.push_back(n);
+                    const Node& nd = L.nodes[(size_t)n];
+                    if (nd.lcnt < 0) st.push_back(nd.lref);  // popped after the right subtree
+                    if (nd.rcnt < 0) st.push_back(nd.rref);
+                }
+                L.bfnode.resize(L.nodes.size());
+                for (size_t i = 0; i < L.bfmap.size(); ++i) {
+                    const Node& nd = L.nodes[(size_t)L.bfmap[i]];
+                    BfNode& b = L.bfnode[i];
+                    for (int c = 0; c < 3; ++c) { b.lmin[c] = nd.lmin[c]; b.lmax[c] = nd.lmax[c]; b.rmin[c] = nd.rmin[c]; b.rmax[c] = nd.rmax[c]; }
+                    b.lm = nd.lcnt < 0 ? (1ull << 63) | (uint64_t)pre[(size_t)nd.lref] : (nd.lcnt > 0 ? L.lmask[(size_t)nd.lref] : 0ull);
+                    b.rm = nd.rcnt < 0 ? (1ull << 63) | (uint64_t)pre[(size_t)nd.rref] : (nd.rcnt > 0 ? L.lmask[(size_t)nd.rref] : 0ull);
+                }
+            }
         }
     }
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
@@ -470,7 +497,9 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_mats = align_up(o_tris + std::max<size_t>(1, L.tris.size()) * sizeof(Tri), 256);
     const size_t o_lights = align_up(o_mats + L.mats.size() * sizeof(Material), 256);
     const size_t o_lmask = align_up(o_lights + L.lights.size() * sizeof(Light), 16);
-    const size_t o_cnt = align_up(o_lmask + L.lmask.size() * sizeof(uint64_t), 256);
+    const size_t o_bfnode = align_up(o_lmask + L.lmask.size() * sizeof(uint64_t), 16);
+    const size_t o_bfmap = align_up(o_bfnode + L.bfnode.size() * sizeof(BfNode), 16);
+    const size_t o_cnt = align_up(o_bfmap + L.bfmap.size() * sizeof(int32_t), 256);
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
     const size_t o_cull = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     const size_t o_pair = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
@@ -485,6 +514,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_mats, L.mats.data(), L.mats.size() * sizeof(Material)) != hipSuccess ||
         up(o_lights, L.lights.data(), L.lights.size() * sizeof(Light)) != hipSuccess ||
         up(o_lmask, L.lmask.data(), L.lmask.size() * sizeof(uint64_t)) != hipSuccess ||
+        up(o_bfnode, L.bfnode.data(), L.bfnode.size() * sizeof(BfNode)) != hipSuccess ||
+        up(o_bfmap, L.bfmap.data(), L.bfmap.size() * sizeof(int32_t)) != hipSuccess ||
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess ||
         up(o_pair, L.bfpair.data(), L.bfpair.size() * sizeof(float)) != hipSuccess) {
@@ -516,7 +547,11 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.cull_its = 0;  // per launch (launch_wavefront)
     s->view.bfpair = reinterpret_cast<const float*>(base + o_pair);
     s->view.mb_base = L.mb_base;
-    s->view.span_bytes = (uint32_t)align_up(o_lmask + L.lmask.size() * sizeof(uint64_t) - o_nodes, 16);
+    s->view.bfnode = L.bfnode.empty() ? nullptr : reinterpret_cast<const BfNode*>(base + o_bfnode);
+    s->view.bfmap = L.bfmap.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_bfmap);
+    s->view.off_bfnode = (uint32_t)(o_bfnode - o_nodes);
+    s->view.off_bfmap = (uint32_t)(o_bfmap - o_nodes);
+    s->view.span_bytes = (uint32_t)align_up(o_bfmap + L.bfmap.size() * sizeof(int32_t) - o_nodes, 16);
     s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);
     s->info = L.info;
     s->info.device_bytes = total;
@@ -758,6 +793,9 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         if (const char* e = std::getenv("PT_BIG_LEAF")) big = std::max(0, std::atoi(e));
         view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? big : 0;
     }
+    // the brute-force replay walks the BfNode tree without a stack (PT_BF_STACKLESS=0: the stack walk; A/B)
+    if (const char* e = std::getenv("PT_BF_STACKLESS"))
+        if (!std::strcmp(e, "0")) view.bfnode = nullptr;
     if (lo.wavefront) {
         uint64_t target = kWfTargetPaths;
         if (const char* e = std::getenv("PT_WF_PATHS")) target = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));  // A/B

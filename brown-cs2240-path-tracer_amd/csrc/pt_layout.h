@@ -32,6 +32,20 @@ struct alignas(16) Node {
 };
 static_assert(sizeof(Node) == 64, "node is 4 x 16 B");
 
+// Mailbox scenes with <= 64 internal nodes and <= 63 distinct entries: the internal nodes again,
+// numbered in the reference's visiting order (pre-order, right subtree first), each child's
+// payload in one 64-bit word — a leaf child's uid set (bit 63 clear; 0 for an empty leaf) or, for
+// an internal child, bit 63 | its pre-order number.  The brute-force replay walks this tree with a
+// 64-bit set of pending nodes instead of a stack (pt_wavefront.hip bf_closest).
+struct alignas(16) BfNode {
+    float lmin[3];
+    float lmax[3];
+    float rmin[3];
+    float rmax[3];
+    uint64_t lm, rm;
+};
+static_assert(sizeof(BfNode) == 64, "bf node is 4 x 16 B");
+
 // The nine floats a triangle test reads fill the first 36 bytes so that a test loads them
 // with two ds_read_b128 + one ds_read_b32 (10 LDS cycles per wave); with v0/e1/e2 each in its
 // own 16-byte slot the compiler reads three ds_read_b96 (8 cycles each on gfx950: 24).
@@ -94,6 +108,12 @@ struct SceneView {
     int32_t mb_base;
     uint32_t off_lmask;
     const uint64_t* lmask;
+    // BfNode tree (nullptr when the scene does not qualify) and bfmap[i] = the nodes[] index of
+    // pre-order node i (its leaf ranges, for the tie-break scan and the counting build); both inside
+    // the LDS span at off_bfnode / off_bfmap
+    const BfNode* bfnode;
+    const int32_t* bfmap;
+    uint32_t off_bfnode, off_bfmap;
     // vertex-normal mode (pt_scene_set_vertex_normals; the reference's commented-out branch,
     // intersection-logic.wgsl:81-108): per record (v0n, v1n, v2n) as 3 float4, v0n.w = 1 where
     // i2 < vn_range (the branch applies); global memory, read for the winning record only

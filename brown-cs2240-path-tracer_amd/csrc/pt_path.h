@@ -193,6 +193,10 @@ __device__ __forceinline__ void stage_scene_lds(SceneView& sc, char* base) {
     sc.mats = reinterpret_cast<const Material*>(base + sc.off_mats);
     sc.lights = reinterpret_cast<const Light*>(base + sc.off_lights);
     sc.lmask = reinterpret_cast<const uint64_t*>(base + sc.off_lmask);
+    if (sc.bfnode) {
+        sc.bfnode = reinterpret_cast<const BfNode*>(base + sc.off_bfnode);
+        sc.bfmap = reinterpret_cast<const int32_t*>(base + sc.off_bfmap);
+    }
 }
 
 }  // namespace pt

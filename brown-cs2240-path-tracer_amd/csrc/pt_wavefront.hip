@@ -423,6 +423,76 @@ __device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool
     }
 }
 
+// Phase 2 without a stack (SceneView::bfnode; scenes of <= 64 internal nodes, <= 63 entries).
+// The reference's traversal visits nodes depth first, right child before left (a node with both
+// children to visit keeps the left one on its stack), and a child's visit is decided when its
+// parent is visited (the exit-distance test against the closest t at that moment).  With the
+// internal nodes numbered in that visiting order (pre-order, right subtree first; pt_capi.hip
+// build_layout), the node the stack walk takes next is always the smallest-numbered node
+// decided but not yet visited: a stacked left child of an ancestor comes after everything below
+// that ancestor's right child, and the current node's children come after it but before every
+// stacked node.  So a 64-bit set of pending nodes walked by ctz replaces the stack, visiting the
+// same nodes in the same order with the same decisions: the same leaf pairs, resolved exactly as
+// in the stack walk below (mailbox set, phase 1's t, strict < with the pair's tie-break).
+__device__ __forceinline__ bool mb_first_node(const SceneView& sc, int node, bool li, bool ri, int a, int b) {
+    const int4 d = reinterpret_cast<const int4*>(sc.nodes)[4 * node + 3];
+    const int na = (li & (d.z >= 0)) ? d.z : 0;
+    const int nt = na + ((ri & (d.w >= 0)) ? d.w : 0);
+    for (int k = 0; k < nt; ++k) {
+        const int u = sc.tris[k < na ? d.x + k : d.y + (k - na)].uid;
+        if (u == a || u == b) return u == a;
+    }
+    return false;
+}
+
+template <bool FAST_RCP>
+__device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ray& r, bool active, uint64_t hits,
+                                                   float tmin, const float* slot, int nslots, float& t_out) {
+    constexpr uint64_t kInner = 1ull << 63;
+    uint64_t pend = active ? 1ull : 0ull;  // pre-order node 0 = the root
+    uint64_t tested = 0;
+    int best = -1;
+    float best_t = -1.0f;
+    while (__any(pend != 0)) {
+        if (pend != 0) {
+            const int n = (int)__builtin_ctzll(pend);
+            pend &= pend - 1;
+            const BfNode& bn = sc.bfnode[n];
+            const float ld = ray_box(r, bn.lmin[0], bn.lmin[1], bn.lmin[2], bn.lmax[0], bn.lmax[1], bn.lmax[2]);
+            const float rd = ray_box(r, bn.rmin[0], bn.rmin[1], bn.rmin[2], bn.rmax[0], bn.rmax[1], bn.rmax[2]);
+            const bool li = 0.0f < ld, ri = 0.0f < rd;
+            const bool lint = (bn.lm & kInner) != 0, rint = (bn.rm & kInner) != 0;
+            const uint64_t m = ((li & !lint) ? bn.lm : 0ull) | ((ri & !rint) ? bn.rm : 0ull);
+            uint64_t rh = m & ~tested & hits;
+            tested |= m;
+            bool bcur = false;  // the best came from this leaf pair
+            while (rh) {
+                const int u = (int)__builtin_ctzll(rh);
+                rh &= rh - 1;
+                const int k = __popcll(hits & ((1ull << u) - 1));
+                const int rec = sc.mb_base + u;
+                float t;
+                if (k < nslots) t = slot[64 * k];
+                else tri_hit<FAST_RCP>(sc.tris, rec, r, t);  // a hit, so the same t as phase 1
+                bool take = (best_t < 0.0f) | (t < best_t);
+                if ((t == best_t) & bcur) take = mb_first_node(sc, sc.bfmap[n], li, ri, u, best - sc.mb_base);
+                best_t = take ? t : best_t;
+                best = take ? rec : best;
+                bcur |= take;
+            }
+            if (best_t == tmin) {
+                pend = 0;
+            } else {
+                const bool tl = (li & lint) && !((best_t > 0.0f) & (ld > best_t));
+                const bool tr = (ri & rint) && !((best_t > 0.0f) & (rd > best_t));
+                pend |= (tl ? 1ull << (uint32_t)(bn.lm & 63u) : 0ull) | (tr ? 1ull << (uint32_t)(bn.rm & 63u) : 0ull);
+            }
+        }
+    }
+    t_out = best_t;
+    return best;
+}
+
 // Closest hit of the 64 rays of one batch (lane = ray; `valid` false lanes give no hit):
 // phase 1 + phase 2 above.  Returns the record (or -1) and its t in t_out.
 template <bool FAST_RCP, bool COUNT, bool PK = kBfPacked>
@@ -492,6 +562,11 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     // equal one can only win inside the pair just resolved (strict-< across pairs) — so the
     // result is final; a ray that hits nothing at all is final at once.  The counting build
     // (COUNT) walks on, to count the reference's work.
+    if constexpr (!COUNT) {
+        if (sc.bfnode) {  // wave-uniform: the stackless walk (bf_replay_stackless)
+            return bf_replay_stackless<FAST_RCP>(sc, r, valid && hits != 0, hits, tmin, slot, nslots, t_out);
+        }
+    }
     TravLean s;
     trav_init(s, valid && (COUNT || hits != 0));
     while (__any(!trav_finished(s))) {

@@ -81,13 +81,16 @@ KERNELS = {
     "wavefront_regen": {"PT_KERNEL": "wavefront", "PT_REGEN": "1"},
     "wavefront_regen_4parts_small": {"PT_KERNEL": "wavefront", "PT_REGEN": "1", "PT_PARTS": "4",
                                      "PT_REGEN_TARGET": "4096"},
+    # brute-force replay: the stack walk instead of the stackless pre-order walk (the default)
+    "wavefront_bf_stack_replay": {"PT_KERNEL": "wavefront", "PT_BF_STACKLESS": "0"},
+    "mega_bf_stack_replay": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1", "PT_BF_STACKLESS": "0"},
 }
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
             "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
-            "PT_BIG_LEAF", "PT_BIG_RATIO", "PT_TRACE_WATCHDOG", "PT_REDUCE")
+            "PT_BIG_LEAF", "PT_BIG_RATIO", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -393,9 +396,10 @@ def packed_tie(tmp_path_factory):
                                  {"PT_MB_UID_ORDER": "reverse", "PT_BF_SLOTS": "1"},
                                  {"PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
                                  {"PT_FUSE": "0", "PT_MB_UID_ORDER": "reverse"},
-                                 {"PT_PERSIST": "1", "PT_MB_UID_ORDER": "reverse"}],
+                                 {"PT_PERSIST": "1", "PT_MB_UID_ORDER": "reverse"},
+                                 {"PT_BF_STACKLESS": "0", "PT_MB_UID_ORDER": "reverse"}],
                          ids=["bf", "bf_reverse_uids", "no_mailbox", "bf_reverse_1slot", "mb_lean16_reverse",
-                              "bf_nofuse_reverse", "persist_reverse"])
+                              "bf_nofuse_reverse", "persist_reverse", "bf_stack_reverse"])
 def test_mailbox_exact_ties(packed_tie, monkeypatch, env):
     for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
