@@ -985,9 +985,11 @@ void k_regen_bf(SceneView sc, FrameParams fp, uint32_t frame0, uint32_t nframes,
     if (COUNT) flush_counters(c, cnt_out);
 }
 
-hipError_t launch_regen_bf(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
+hipError_t launch_regen_bf(const LaunchOpts& lo, const SceneView& sc_in, const FrameParams& fp, uint32_t frame0,
                            uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
                            hipStream_t stream) {
+    SceneView sc = sc_in;
+    if (!count && sc.bfnode) sc.max_stack = 0;  // the stackless replay (bf_view)
     const bool lds = lo.lds && scene_fits_lds(sc);
     const bool fast = lo.fast_rcp != 0 && sc.fast_rcp;
     int slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
@@ -1244,10 +1246,21 @@ static hipError_t wf_render_regen(const SceneView& sc, const FrameParams& fp, co
     return hipGetLastError();
 }
 
+// The brute-force kernels without counters replay without a stack when the scene has the BfNode
+// tree (bf_replay_stackless): no per-lane stack in their LDS (CornellBox: 14 KB of a 512-thread
+// block's 43 KB, so 4 blocks fit a CU's 160 KB instead of 3 — 8 waves per SIMD instead of 6).
+template <int TRAV, bool COUNT>
+static SceneView bf_view(const SceneView& sc) {
+    SceneView v = sc;
+    if (TRAV >= 300 && !COUNT && sc.bfnode) v.max_stack = 0;
+    return v;
+}
+
 template <bool LDS, int TRAV, bool COUNT>
-static hipError_t wf_render_t(const SceneView& sc, const FrameParams& fp, const WfBuffers& wb, uint32_t frame0,
+static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, const WfBuffers& wb, uint32_t frame0,
                               uint32_t nframes, uint32_t stride, bool accum, float* out, Counters* cnt,
                               hipStream_t stream, const WfStreams& ws) {
+    const SceneView sc = bf_view<TRAV, COUNT>(sc_in);
     const uint32_t npix = fp.width * fp.height;
     // the batch in ws.nparts parts on as many streams when a part holds at least a frame: one
     // part's kernel fills the others' launch tails and boundaries (and, with separate trace and
