@@ -200,8 +200,13 @@ def main():
         return native_multi(args)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # PT_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with several ranks on fewer GPUs (the
+    # reduce then goes through host memory); the driver's runs use RCCL, one rank per GPU
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
+    if backend == "gloo":
+        local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -270,7 +275,7 @@ def main():
     prof = scene.profile_read()
     scene.profile_enable(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

@@ -26,5 +26,11 @@ def frames_for_rank(rank: int, world: int, spp: int, frame0: int = 0):
 def reduce_accum(acc, dist, dst: int = 0):
     """Sum-reduce the per-rank accumulators onto `dst` (one collective per render)."""
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.reduce(acc, dst=dst, op=dist.ReduceOp.SUM)
+        if acc.is_cuda and dist.get_backend() == "gloo":  # rehearsal backend: through host memory
+            h = acc.cpu()
+            dist.reduce(h, dst=dst, op=dist.ReduceOp.SUM)
+            if dist.get_rank() == dst:
+                acc.copy_(h)
+        else:
+            dist.reduce(acc, dst=dst, op=dist.ReduceOp.SUM)
     return acc
