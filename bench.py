@@ -326,7 +326,8 @@ def main():
                     f"packed by the Node host, {args.bvh} BVH" + (", all meshes" if args.all_meshes else "") +
                     "; RNG salts t_k = k)",
             "config": {"workload": f"{args.scene}.xml {W}x{H} {args.spp}spp depth {args.depth}, rr 0.9, "
-                                   f"frames sharded k mod {world}" + (", RCCL sum-reduce of the f32 accumulator"
+                                   f"frames sharded k mod {world}" + ((", RCCL sum-reduce of the f32 accumulator" if backend == "nccl" else
+                                                                         f", {backend} sum-reduce through host memory (rehearsal)")
                                                                         if world > 1 else ""),
                        "mode": args.mode, "bvh": args.bvh, "samples_per_step": total_samples,
                        "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size)},
