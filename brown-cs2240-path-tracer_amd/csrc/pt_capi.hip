@@ -653,6 +653,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
     if (const char* e = std::getenv("PT_MAILBOX")) lo.mailbox = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_REGEN")) lo.regen = std::strcmp(e, "0") != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_REGEN_TARGET")) lo.regen_target = std::atol(e);
+    if (const char* e = std::getenv("PT_SORT")) lo.sort = std::atoi(e);  // 1 / 8: direction octant; 64: + origin octant
     if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
     return lo;
 }
