@@ -278,17 +278,13 @@ __device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r
 // lanes reject at the same step, which practically never happens), each unit is one exec
 // region and the push/pop decision is straight-line (stack[sp] is the free slot above the
 // top: max_stack = max depth + 1, pt_capi.hip).  Same units, same order, same arithmetic.
-enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8, TF_BCUR = 16 };
+enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8, TF_BCUR = 16, TF_PARK = 32 };
 struct TravLean {
     int node, sp, k, na, nt, la, lb, fl, best;
     float ld, rd, best_t;
     uint64_t tested, rem;  // mailbox flavours only: uids tested by this query / left in this pair
-    int rot;               // big-leaf flavour: rotation of the big leaf being walked
-    uint32_t step;         // big-leaf flavour: the wave's leaf-test step counter (same in every lane)
 };
 __device__ __forceinline__ void trav_init(TravLean& s, bool active) {
-    s.rot = 0;
-    if (!active) s.step = 0;  // a kernel's first (inactive) init; later queries keep the wave's count
     s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1;
     s.fl = active ? 0 : TF_DONE;
     s.ld = 0.0f; s.rd = 0.0f; s.best_t = -1.0f;
@@ -318,42 +314,35 @@ __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r
     return s.nt == 0;  // no leaf to test: decide now
 }
 
-// Big leaves in step (BIG; SceneView::big_leaf): a lane in a leaf of at least big_leaf entries
-// walks it in a rotated order that is the same for every lane of the wave in that leaf — entry
-// (rot + i) mod n at its i-th test, rot = the wave's test-step counter mod n when the lane enters
-// the leaf — so the lanes in one big leaf read the same record at the same step (one cache line
-// instead of a gather per lane; the steps of a leaf turn advance the counter for every lane).
-// The leaf's result must be the FIRST entry in leaf order among those with the smallest t (the
-// reference's sequential strict-< loop); out of order that is: take a hit when t < best_t, or when
-// t == best_t and the best is an earlier entry of this same leaf (a leaf is tested once per query,
-// so a best inside the leaf's record range was taken in this walk).  An equal t from an earlier
-// leaf is never replaced, as in order.
+// Big leaves (BIG; SceneView::big_leaf): a lane whose next entry starts a leaf of at least
+// big_leaf entries parks there (TF_PARK) instead of walking it alone; the wave then tests that
+// leaf for that one ray with all 64 lanes (big_turn).  big_at: the lane stands at the start of a
+// big left leaf, or at the start of a big right leaf; big_seg: that leaf (first record, entries).
+__device__ __forceinline__ bool big_at(const SceneView& sc, const TravLean& s) {
+    return (s.k < s.na) ? (s.k == 0 && s.na >= sc.big_leaf) : (s.k == s.na && s.k < s.nt && s.nt - s.na >= sc.big_leaf);
+}
+__device__ __forceinline__ void big_seg(const TravLean& s, int& rec0, int& n) {
+    const bool left = s.k < s.na;
+    rec0 = left ? s.la : s.lb;
+    n = left ? s.na : s.nt - s.na;
+}
+
 template <int K, bool COUNT, bool FAST_RCP, bool PIPE, bool BIG = false>
 __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
+    if constexpr (BIG) {  // park at a big leaf: now, or where this turn would enter it
+        if (big_at(sc, s)) { s.fl |= TF_PARK; return false; }
+    }
     if constexpr (!PIPE) {
+        // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
+        const int lim = (BIG && s.k < s.na && s.nt - s.na >= sc.big_leaf) ? s.na : s.nt;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const bool live = j == 0 || s.k < s.nt;  // the first test always is
-            if (j > 0 && !__any(live)) break;        // every lane's leaf pair is done
-            int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
-            bool big = false;
-            int seg0 = 0, segn = 0;
-            if constexpr (BIG) {
-                const bool left = s.k < s.na;
-                seg0 = left ? s.la : s.lb;
-                segn = left ? s.na : s.nt - s.na;
-                const int i = left ? s.k : s.k - s.na;  // position in the leaf
-                big = segn >= sc.big_leaf;
-                if (big && i == 0) s.rot = (int)((s.step + (uint32_t)j) % (uint32_t)segn);
-                int e = s.rot + i;
-                e -= (e >= segn) ? segn : 0;
-                idx = big ? seg0 + e : idx;
-            }
+            const bool live = j == 0 || s.k < lim;  // the first test always is
+            if (j > 0 && !__any(live)) break;      // every lane's leaf pair is done
+            const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
             float t;
-            const bool hit = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live;
-            bool take = hit & ((s.best_t < 0.0f) | (t < s.best_t));
-            if constexpr (BIG)
-                take |= hit & big & (t == s.best_t) & (s.best >= seg0) & (s.best < seg0 + segn) & (idx < s.best);
+            const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
+                              ((s.best_t < 0.0f) | (t < s.best_t));
             s.best_t = take ? t : s.best_t;
             s.best = take ? idx : s.best;
             if (COUNT) cnt.tri_tests += live ? 1 : 0;
@@ -383,6 +372,7 @@ __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r
     }
     const bool decide = s.k == s.nt;
     s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
+    if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
     return decide;
 }
 
@@ -397,6 +387,59 @@ __device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int str
     s.sp += (tl & tr) ? 1 : (pop ? -1 : 0);  // sp < 0 only once done
 }
 
+// One cooperative big-leaf turn for the first parked lane f of the wave: the leaf's n entries are
+// dealt to the 64 lanes (lane l tests entries l, l + 64, ... against f's ray, read from f's
+// registers; the records of one step are 64 consecutive ones, a coalesced load), each lane keeps
+// the first of its smallest-t hits, and a wave reduction picks the smallest (t, entry) — the
+// first entry in leaf order among the leaf's smallest-t hits, which is what the reference's
+// sequential strict-< loop ends with, when that t beats f's closest t so far (strict <, so an
+// equal t from an earlier leaf stays).  The ray's walk over the leaf takes n / 64 steps instead of
+// n, and the wave's lanes do all of it instead of idling while one lane walks.
+template <bool COUNT, bool FAST_RCP>
+__device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, int32_t* stack,
+                                         int stride, Counters& cnt) {
+    const int f = (int)__builtin_ctzll(parked);
+    int my0 = 0, myn = 0;
+    big_seg(s, my0, myn);
+    const int rec0 = __builtin_amdgcn_readlane(my0, f), n = __builtin_amdgcn_readlane(myn, f);
+    auto bc = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), f)); };
+    Ray q;
+    q.o = mk(bc(r.o.x), bc(r.o.y), bc(r.o.z));
+    q.d = mk(bc(r.d.x), bc(r.d.y), bc(r.d.z));
+    q.inv = mk(bc(r.inv.x), bc(r.inv.y), bc(r.inv.z));
+    const int lane = (int)(threadIdx.x & 63u);
+    float bt = 0.0f;
+    int bk = 0x7fffffff;  // none
+    for (int c = lane; c < n; c += 64) {
+        float t;
+        const bool take = tri_hit<FAST_RCP>(sc.tris, rec0 + c, q, t) & ((bk == 0x7fffffff) | (t < bt));
+        bt = take ? t : bt;
+        bk = take ? c : bk;
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float ot = __shfl_xor(bt, off, 64);
+        const int ok = __shfl_xor(bk, off, 64);
+        const bool better = (ok != 0x7fffffff) & ((bk == 0x7fffffff) | (ot < bt) | ((ot == bt) & (ok < bk)));
+        bt = better ? ot : bt;
+        bk = better ? ok : bk;
+    }
+    if (lane == f) {
+        const bool take = (bk != 0x7fffffff) & ((s.best_t < 0.0f) | (bt < s.best_t));
+        s.best_t = take ? bt : s.best_t;
+        s.best = take ? rec0 + bk : s.best;
+        if (COUNT) cnt.tri_tests += n;
+        s.k += n;
+        s.fl &= ~TF_PARK;
+        if (s.k == s.nt) {
+            s.fl &= ~TF_LEAF;
+            lean_decide(s, stack, stride);
+        } else if (big_at(sc, s)) {
+            s.fl |= TF_PARK;  // its right leaf is big too
+        }
+    }
+}
+
 // IFIF = false: each iteration runs ONE unit type for the whole wave — a leaf turn (up to K
 // triangle tests) when leaf lanes >= node_bias * node lanes, else a node turn.  IFIF = true:
 // each iteration runs a node step for every lane that wants one and then the leaf loop for
@@ -405,7 +448,14 @@ __device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int str
 template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false, bool IFIF = false, bool BIG = false>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
                                                int stride, Counters& cnt) {
-    const int state = s.fl & (TF_LEAF | TF_DONE);
+    const int state = s.fl & (TF_LEAF | TF_DONE | (BIG ? TF_PARK : 0));
+    if constexpr (BIG) {  // a parked lane's big leaf goes first: the wave tests it for that ray
+        const uint64_t parked = __ballot((state & TF_PARK) != 0);
+        if (parked) {  // wave-uniform
+            big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);
+            return true;
+        }
+    }
     const uint64_t want_leaf = __ballot(state == TF_LEAF);
     const uint64_t want_node = __ballot(state == 0);
     if ((want_leaf | want_node) == 0) return false;
@@ -417,9 +467,6 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     } else {
         if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
             if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE, BIG>(sc, r, s, cnt);
-            // every lane still in a big leaf ran all K steps of the turn (the turn ends early only
-            // when no lane is live), so the wave's step counter advances by K for all lanes alike
-            if constexpr (BIG) s.step += K;
         } else if (state == 0) {
             decide = lean_node_unit<COUNT>(sc, r, s, cnt);
         }
