@@ -30,6 +30,15 @@ namespace pt {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// k_wf_trace hands out its 32-entry windows dynamically: wave w takes the next window of group
+// w % kTraceGroups from that group's counter (one cache line each, in wb.rfetch: slot in_q of the
+// launch; the launch zeroes the other slot for the next trace, k_wf_generate both for a batch's
+// first).  A group's windows are one contiguous range of the queue.
+constexpr uint32_t kTraceGroups = 64;
+__device__ __forceinline__ uint32_t* trace_counter(uint32_t* rfetch, int slot, uint32_t g) {
+    return rfetch + ((uint32_t)slot * kRegions + g) * kFetchStride;
+}
+
 // number of set bits of m below this lane
 __device__ __forceinline__ uint32_t rank_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -104,6 +113,9 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
         wb.rcnt[p] = n == 0 ? 0u : n * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
         wb.rcnt[kRegions + p] = 0;
     }
+    // k_wf_trace's window counters, both slots, for the batch's first trace (trace_counter)
+    if (blockIdx.x == 0 && threadIdx.x < 2 * kTraceGroups)
+        wb.rfetch[((threadIdx.x / kTraceGroups) * kRegions + threadIdx.x % kTraceGroups) * kFetchStride] = 0;
     Counters c = {};
     if (p < P) {
         uint32_t x, y, f;
@@ -125,15 +137,19 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
 // (or prefetch) in the loop makes the next use of any loaded register wait for it.
 constexpr uint32_t kWinRays = 32;
 constexpr uint32_t kHitRing = 128;  // entries; power of two, multiple of kWinRays
-constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8;
+constexpr uint32_t kWinTab = 8;  // window ids of the windows between the last flushed and the prefetched one
+constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8 + kWinTab * 4;
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 
-// Work split: the queue is cut into windows of 32 entries and wave w of N takes windows
-// w, w+N, w+2N, ...  Interleaving (not contiguous chunks) balances the waves: queue order is
-// spatially coherent (camera rays in pixel order, survivors compacted block by block), so a
-// contiguous chunk is an image region whose cost differs systematically from the others.
-// Inside a wave, window j's entries have the wave-local sequence numbers 32j .. 32j+31, which
-// index the hit ring.
+// Work split: the queue is cut into windows of 32 entries, dealt to kTraceGroups groups
+// round-robin (group g: windows g, g+G, g+2G, ...; interleaving, not contiguous chunks, because
+// queue order is spatially coherent — camera rays in pixel order, survivors compacted block by
+// block — so a contiguous chunk is an image region whose cost differs systematically from the
+// others), and a group's waves take its windows one at a time from its counter: a wave that drew
+// cheap rays takes more windows, so the waves of a launch finish together (a static split left
+// the boat's trace waves resident for ~12 % of the launch).  Inside a wave, its
+// j-th window's entries have the wave-local sequence numbers 32j .. 32j+31, which index the hit
+// ring; wtab keeps the ids of the windows between the last written back and the prefetched one.
 // PT_TRACE_WAVES (build-time A/B): cap the traversal kernel's VGPRs for this many waves per SIMD
 #ifndef PT_TRACE_WAVES
 #define PT_TRACE_WAVES 0
@@ -152,30 +168,49 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
     char* stage = stage_base + (threadIdx.x / 64u) * kStageBytes;
     float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
     int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [kHitRing]
+    uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32 + kHitRing * 8);  // [kWinTab] window ids
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
+    if (blockIdx.x == 0 && threadIdx.x < kTraceGroups) *trace_counter(wb.rfetch, in_q ^ 1, threadIdx.x) = 0;  // next trace's
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip
     // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
     const uint32_t nwin = (count + kWinRays - 1) / kWinRays;
     if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * kStageBytes);
-    if (w >= nwin) return;  // wave-uniform
-    const uint32_t J = (nwin - w + nwaves - 1) / nwaves;  // windows of this wave
-    auto wbase = [&](uint32_t j) { return (w + j * nwaves) * kWinRays; };
-    auto wcount = [&](uint32_t j) { return min(kWinRays, count - wbase(j)); };
-    // lanes 0..31 load the first halves of a window's ray records, lanes 32..63 the second
+    // windows: group g owns windows g, g + G, g + 2G, ... (interleaved over the whole queue, whose
+    // order is spatially coherent, so every group's share costs about the same), handed out one
+    // at a time from the group's counter to the group's waves
+    const uint32_t G = min(kTraceGroups, nwaves), g = w % G;
+    uint32_t* ctr = trace_counter(wb.rfetch, in_q, g);
     const uint32_t lane = lane_id();
+    constexpr uint32_t kNone = 0xffffffffu;
+    auto fetch = [&]() {  // the group's next window (wave-uniform), or kNone
+        uint32_t i = 0;
+        if (lane == 0) i = atomicAdd(ctr, 1u);
+        i = __builtin_amdgcn_readfirstlane(__shfl(i, 0, 64));
+        const uint64_t wid = (uint64_t)i * G + g;
+        return wid < nwin ? (uint32_t)wid : kNone;
+    };
+    auto wcount = [&](uint32_t wid) { return min(kWinRays, count - wid * kWinRays); };
+    const uint32_t w0 = g < nwin ? fetch() : kNone;
+    if (w0 == kNone) return;  // wave-uniform
+    // lanes 0..31 load the first halves of a window's ray records, lanes 32..63 the second
     const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
     const float4* q = in_q ? wb.shd.ray : wb.ext.ray;
     Counters c = {};
-    // window jl sits in LDS; window jl + 1 is in flight in registers
-    uint32_t jl = 0, wv = wcount(0);
-    if (wl < wv) wray[2 * wl + half] = q[2 * (size_t)(wbase(0) + wl) + half];
+    // local window jl (id wtab[jl % kWinTab]) sits in LDS; window jl + 1 is in flight in registers
+    uint32_t jl = 0, wv = wcount(w0);
+    if (lane == 0) wtab[0] = w0;
+    if (wl < wv) wray[2 * wl + half] = q[2 * (size_t)(w0 * kWinRays + wl) + half];
     uint32_t nv = 0;
     float4 na = make_float4(0, 0, 0, 0);
-    if (J > 1) {
-        nv = wcount(1);
-        if (wl < nv) na = q[2 * (size_t)(wbase(1) + wl) + half];
+    {
+        const uint32_t w1 = fetch();
+        if (w1 != kNone) {
+            nv = wcount(w1);
+            if (lane == 0) wtab[1] = w1;
+            if (wl < nv) na = q[2 * (size_t)(w1 * kWinRays + wl) + half];
+        }
     }
     uint32_t cur = 0;      // sequence number of the next entry to hand out (in window jl)
     uint32_t flushed = 0;  // sequence numbers below this are written back to wb.hitq
@@ -195,34 +230,38 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
             if (lane == 0) {
                 atomicOr(&wb.ctl[WF_WATCHDOG], 1u);
                 if (atomicCAS(&wb.ctl[WF_SNAP_CLAIM], 0u, 1u) == 0u) {
-                    const uint32_t v[WF_SNAP_WORDS] = {count, nwaves, w, J, jl, wv, nv, cur, flushed,
+                    const uint32_t v[WF_SNAP_WORDS] = {count, nwaves, w, g, jl, wv, nv, cur, flushed,
                                                        (uint32_t)__popcll(hm), (uint32_t)hm, (uint32_t)(hm >> 32),
-                                                       (uint32_t)in_q, 0u, 0u, 0u};
+                                                       (uint32_t)in_q, G, 0u, 0u};
                     for (int i = 0; i < WF_SNAP_WORDS; ++i) wb.ctl[WF_SNAP + i] = v[i];
                 }
             }
             break;
         }
         // write back every window whose entries are all handed out and traced (coalesced)
-        while (flushed < J * kWinRays) {
+        while (flushed < (jl + 1) * kWinRays) {
             const uint32_t jf = flushed / kWinRays;
-            const bool handed = jf < jl || (jf == jl && cur == jl * kWinRays + wv);
+            const bool handed = jf < jl || cur == jl * kWinRays + wv;
             if (!handed || __any(has && sq < flushed + kWinRays)) break;
-            const uint32_t fv = wcount(jf);
-            if (lane < fv) wb.hitq[wbase(jf) + lane] = ring[(flushed + lane) & (kHitRing - 1)];
+            const uint32_t wf = wtab[jf % kWinTab];
+            const uint32_t fv = wcount(wf);
+            if (lane < fv) wb.hitq[wf * kWinRays + lane] = ring[(flushed + lane) & (kHitRing - 1)];
             flushed += kWinRays;
         }
         // hand the next entries to idle lanes (wave-uniform control)
         const uint64_t need = __ballot(!has);
         if (need) {
-            if (cur == jl * kWinRays + wv && jl + 1 < J && (jl + 2) * kWinRays - flushed <= kHitRing) {
+            if (cur == jl * kWinRays + wv && nv > 0 && (jl + 2) * kWinRays - flushed <= kHitRing) {
                 if (wl < nv) wray[2 * wl + half] = na;  // next window, if the hit ring has room
                 ++jl;
                 wv = nv;
                 cur = jl * kWinRays;
-                if (jl + 1 < J) {
-                    nv = wcount(jl + 1);
-                    if (wl < nv) na = q[2 * (size_t)(wbase(jl + 1) + wl) + half];
+                nv = 0;
+                const uint32_t wn = fetch();
+                if (wn != kNone) {
+                    nv = wcount(wn);
+                    if (lane == 0) wtab[(jl + 1) % kWinTab] = wn;
+                    if (wl < nv) na = q[2 * (size_t)(wn * kWinRays + wl) + half];
                 }
             }
             const uint32_t wend = jl * kWinRays + wv;
@@ -239,7 +278,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
             }
         }
         if (!__any(has)) {
-            if (jl + 1 >= J && cur == jl * kWinRays + wv && flushed >= J * kWinRays) break;  // all done
+            if (nv == 0 && cur == jl * kWinRays + wv && flushed >= (jl + 1) * kWinRays) break;  // all done
             continue;  // ring full with nothing in flight: the flush above frees it
         }
         trav_advance<TRAV, COUNT>(sc, r, s, stack, blockDim.x, c);
