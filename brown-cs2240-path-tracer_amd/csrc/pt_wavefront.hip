@@ -146,8 +146,7 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 // queue order is spatially coherent — camera rays in pixel order, survivors compacted block by
 // block — so a contiguous chunk is an image region whose cost differs systematically from the
 // others), and a group's waves take its windows one at a time from its counter: a wave that drew
-// cheap rays takes more windows, so the waves of a launch finish together (a static split left
-// the boat's trace waves resident for ~12 % of the launch).  Inside a wave, its
+// cheap rays takes more windows, so the waves of a launch finish closer together.  Inside a wave, its
 // j-th window's entries have the wave-local sequence numbers 32j .. 32j+31, which index the hit
 // ring; wtab keeps the ids of the windows between the last written back and the prefetched one.
 // PT_TRACE_WAVES (build-time A/B): cap the traversal kernel's VGPRs for this many waves per SIMD
