@@ -661,7 +661,7 @@ LaunchOpts launch_opts(int mode, uint64_t paths) {
 // paths in flight per wavefront batch (kWfBytesPerPath = 188 B of queue state per path: 8 M
 // paths ~ 1.6 GB, plus the queue slack of the region layout)
 constexpr uint64_t kWfTargetPaths = 8ull << 20;
-constexpr int kBigLeafDefault = 64;
+constexpr int kBigLeafDefault = 128;
 
 // radiance of finished paths: the batch's (capacity), or with streaming regeneration a whole
 // group of frames, up to kRadMaxPaths (12 B per path: 3.2 GB)
@@ -790,8 +790,9 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     SceneView view = s->view;
     if (const char* e = std::getenv("PT_NODE_BIAS")) view.node_bias = std::max(1, std::atoi(e));  // A/B runs
     // big leaves (lean traversal): a ray reaching a leaf of >= big_leaf entries has it tested by the
-    // whole wave (pt_device.h big_turn); default 64 (MedievalBoat 2.3x, in-process A/B; scenes whose
-    // leaves are all smaller run unchanged); PT_BIG_LEAF=n sets it, 0 turns it off
+    // whole wave (pt_device.h big_turn); default 128 (MedievalBoat 2.3x, in-process A/B; 64 is 1.5 %
+    // faster there but 12 % slower on the 1M-triangle synthetic scene, whose many 64..127-entry
+    // leaves waste half a cooperative step each); PT_BIG_LEAF=n sets it, 0 turns it off
     {
         int big = kBigLeafDefault;
         if (const char* e = std::getenv("PT_BIG_LEAF")) big = std::max(0, std::atoi(e));

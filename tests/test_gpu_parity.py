@@ -72,7 +72,7 @@ KERNELS = {
     "wavefront_gen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1"},
     "wavefront_nogen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "0"},
     "wavefront_gen_cull_1block": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1", "PT_CULL": "2", "PT_WF_TRACE_BLOCKS": "1"},
-    # big leaves tested by the whole wave (default from 64 entries: the boat; forced onto small leaves
+    # big leaves tested by the whole wave (default from 128 entries: the boat; forced onto small leaves
     # here so every scene runs many cooperative turns), and off
     "wavefront_big8": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0"},
     "wavefront_big4_lean8_div": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_TRAV": "lean8", "PT_FASTRCP": "0",
