@@ -160,7 +160,7 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 #endif
 template <bool LDS, int TRAV, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
-                                                          uint32_t watchdog) {
+                                                          uint32_t watchdog, int dyn) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
@@ -183,15 +183,28 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
     uint32_t* ctr = trace_counter(wb.rfetch, in_q, g);
     const uint32_t lane = lane_id();
     constexpr uint32_t kNone = 0xffffffffu;
-    auto fetch = [&]() {  // the group's next window (wave-uniform), or kNone
-        uint32_t i = 0;
-        if (lane == 0) i = atomicAdd(ctr, 1u);
-        i = __builtin_amdgcn_readfirstlane(__shfl(i, 0, 64));
+    // the counter's atomic for the window after next is issued one window ahead, so its latency
+    // hides behind the current window instead of stalling the hand-out
+    // (dyn = 0, PT_TRACE_DYN=0: the static split — wave w takes windows w, w + nwaves, ... — for A/B)
+    uint32_t ticket = 0;  // lane 0: the group counter's value for the next fetch
+    uint32_t nstatic = 0;
+    auto issue = [&]() {
+        if (dyn && lane == 0) ticket = atomicAdd(ctr, 1u);
+    };
+    auto fetch = [&]() {  // the group's next window (wave-uniform), or kNone; issues the one after
+        if (!dyn) {
+            const uint64_t wid = (uint64_t)(nstatic++) * nwaves + w;
+            return wid < nwin ? (uint32_t)wid : kNone;
+        }
+        const uint32_t i = __builtin_amdgcn_readfirstlane(__shfl(ticket, 0, 64));
+        issue();
         const uint64_t wid = (uint64_t)i * G + g;
         return wid < nwin ? (uint32_t)wid : kNone;
     };
     auto wcount = [&](uint32_t wid) { return min(kWinRays, count - wid * kWinRays); };
-    const uint32_t w0 = g < nwin ? fetch() : kNone;
+    if ((dyn ? g : w) >= nwin) return;  // wave-uniform: nothing for this wave
+    issue();
+    const uint32_t w0 = fetch();
     if (w0 == kNone) return;  // wave-uniform
     // lanes 0..31 load the first halves of a window's ray records, lanes 32..63 the second
     const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
@@ -1354,6 +1367,8 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     if (const char* e = std::getenv("PT_WF_TRACE_BLOCKS")) tblocks = std::max(1, std::min(tblocks, std::atoi(e)));  // tests
     const int iters = 2 * (fp.max_depth + 1);
     uint32_t watchdog = kTraceWatchdog;  // PT_TRACE_WATCHDOG: tests of the failure report
+    int trace_dyn = 1;  // PT_TRACE_DYN=0: k_wf_trace's static window split (A/B)
+    if (const char* e = std::getenv("PT_TRACE_DYN")) trace_dyn = std::atoi(e) != 0 ? 1 : 0;
     if (const char* e = std::getenv("PT_TRACE_WATCHDOG")) watchdog = (uint32_t)std::max(1L, std::atol(e));
     int bf_slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
     if (const char* e = std::getenv("PT_BF_SLOTS")) bf_slots = std::max(0, std::min(kBfSlots, std::atoi(e)));
@@ -1446,7 +1461,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                               dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
                 else
                     PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc,
-                              w, in_q, cnt, watchdog);
+                              w, in_q, cnt, watchdog, trace_dyn);
                 if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
                 if ((it & 1) == 0)
                     PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--synthetic", type=int, default=0, help="bench.py's N-triangle synthetic scene instead of --scene")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--profile", action="store_true", help="one more render per variant with per-launch events")
     ap.add_argument("variants", nargs="+")
@@ -33,7 +34,7 @@ def main():
     import bench
     import pt_amd
     with tempfile.TemporaryDirectory() as td:
-        tri, bvh, meta = bench.pack_scene(a.scene, td, a.width, a.height, a.spp)
+        tri, bvh, meta = bench.pack_scene(a.scene, td, a.width, a.height, a.spp, a.synthetic)
     W, H = int(meta[0]), int(meta[1])
     scene = pt_amd.Scene(tri, bvh)
     st = torch.cuda.Stream()
