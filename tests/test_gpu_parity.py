@@ -87,6 +87,9 @@ KERNELS = {
     "mega_bf_stack_replay": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1", "PT_BF_STACKLESS": "0"},
     # traversal pipeline: survivors grouped by 8 / 64 coherence keys per shade block (queue order only; 64 is the default)
     "wavefront_sort8": {"PT_KERNEL": "wavefront", "PT_SORT": "8"},
+    # traversal kernel with windows from group counters (PT_TRACE_DYN=1), also on a 1-block grid
+    "wavefront_trace_dyn": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_MAILBOX": "0"},
+    "wavefront_trace_dyn_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_WF_TRACE_BLOCKS": "1"},
     "wavefront_nosort_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "0", "PT_MAILBOX": "0"},
     "wavefront_sort64": {"PT_KERNEL": "wavefront", "PT_SORT": "64"},
     "wavefront_sort64_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_SORT": "64", "PT_MAILBOX": "0",
@@ -97,7 +100,7 @@ KERNELS = {
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
             "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
-            "PT_BIG_LEAF", "PT_BIG_RATIO", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT")
+            "PT_BIG_LEAF", "PT_BIG_RATIO", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN")
 
 
 @pytest.fixture(params=list(KERNELS))
