@@ -408,21 +408,44 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
     q.d = mk(bc(r.d.x), bc(r.d.y), bc(r.d.z));
     q.inv = mk(bc(r.inv.x), bc(r.inv.y), bc(r.inv.z));
     const int lane = (int)(threadIdx.x & 63u);
+    // the lanes running this turn: all 64 in the wavefront kernels; the megakernel's paths call the
+    // traversal with finished lanes switched off, and the entries are dealt over the lanes that run
+    const uint64_t act = __ballot(1);
+    const int na = __popcll(act), me = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
     float bt = 0.0f;
     int bk = 0x7fffffff;  // none
-    for (int c = lane; c < n; c += 64) {
+    for (int c = me; c < n; c += na) {
         float t;
         const bool take = tri_hit<FAST_RCP>(sc.tris, rec0 + c, q, t) & ((bk == 0x7fffffff) | (t < bt));
         bt = take ? t : bt;
         bk = take ? c : bk;
     }
+    auto better = [](float ot, int ok, float t, int k) {
+        return (ok != 0x7fffffff) & ((k == 0x7fffffff) | (ot < t) | ((ot == t) & (ok < k)));
+    };
+    if (act == ~0ull) {  // butterfly: every lane ends with the wave's smallest (t, entry)
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const float ot = __shfl_xor(bt, off, 64);
-        const int ok = __shfl_xor(bk, off, 64);
-        const bool better = (ok != 0x7fffffff) & ((bk == 0x7fffffff) | (ot < bt) | ((ot == bt) & (ok < bk)));
-        bt = better ? ot : bt;
-        bk = better ? ok : bk;
+        for (int off = 1; off < 64; off <<= 1) {
+            const float ot = __shfl_xor(bt, off, 64);
+            const int ok = __shfl_xor(bk, off, 64);
+            const bool b = better(ot, ok, bt, bk);
+            bt = b ? ot : bt;
+            bk = b ? ok : bk;
+        }
+    } else {  // some lanes off (their registers are stale): read the running lanes one by one
+        float rt = 0.0f;
+        int rk = 0x7fffffff;
+        for (uint64_t m = act; m; m &= m - 1) {
+            const int l = (int)__builtin_ctzll(m);
+            const float ot = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bt), l));
+            const int ok = __builtin_amdgcn_readlane(bk, l);
+            const bool b = better(ot, ok, rt, rk);
+            rt = b ? ot : rt;
+            rk = b ? ok : rk;
+        }
+        bt = rt;
+        bk = rk;
     }
     if (lane == f) {
         const bool take = (bk != 0x7fffffff) & ((s.best_t < 0.0f) | (bt < s.best_t));

@@ -238,13 +238,15 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& scene, const
     // for lean2 with majority turns and the division; scripts/perf_variants.py)
     const int trav0 = lo.trav < 0 ? 5 : std::min(lo.trav, 5);
     const bool fast = lo.fast_rcp != 0 && sc.fast_rcp;
-    const int trav = trav0 + ((trav0 >= 3 && fast) ? 10 : 0);
+    // + 160: cooperative big-leaf turns (SceneView::big_leaf; lean4 with the fast reciprocal)
+    const bool big = sc.big_leaf > 0 && trav0 == 5 && fast;
+    const int trav = trav0 + ((trav0 >= 3 && fast) ? 10 : 0) + (big ? 160 : 0);
 #define RA(L, T) launch_regen_a<L, T>(sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream)
 #define RA_T(L, T) else if (trav == T) RA(L, T);
     if (lds) {
-        if (trav == 0) RA(true, 0); RA_T(true, 1) RA_T(true, 2) RA_T(true, 3) RA_T(true, 4) RA_T(true, 5) RA_T(true, 13) RA_T(true, 14) RA_T(true, 15)
+        if (trav == 0) RA(true, 0); RA_T(true, 1) RA_T(true, 2) RA_T(true, 3) RA_T(true, 4) RA_T(true, 5) RA_T(true, 13) RA_T(true, 14) RA_T(true, 15) RA_T(true, 175)
     } else {
-        if (trav == 0) RA(false, 0); RA_T(false, 1) RA_T(false, 2) RA_T(false, 3) RA_T(false, 4) RA_T(false, 5) RA_T(false, 13) RA_T(false, 14) RA_T(false, 15)
+        if (trav == 0) RA(false, 0); RA_T(false, 1) RA_T(false, 2) RA_T(false, 3) RA_T(false, 4) RA_T(false, 5) RA_T(false, 13) RA_T(false, 14) RA_T(false, 15) RA_T(false, 175)
     }
 #undef RA_T
 #undef RA

@@ -78,6 +78,8 @@ KERNELS = {
     "wavefront_big4_lean8_div": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_TRAV": "lean8", "PT_FASTRCP": "0",
                                  "PT_MAILBOX": "0"},
     "wavefront_nobig": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "0"},
+    "mega_big8": {"PT_KERNEL": "mega", "PT_BIG_LEAF": "8"},
+    "mega_nobig": {"PT_KERNEL": "mega", "PT_BIG_LEAF": "0"},
     # streaming path regeneration (opt-in): one and four parts, a small in-flight target
     "wavefront_regen": {"PT_KERNEL": "wavefront", "PT_REGEN": "1"},
     "wavefront_regen_4parts_small": {"PT_KERNEL": "wavefront", "PT_REGEN": "1", "PT_PARTS": "4",
