@@ -626,12 +626,17 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 // PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
 // PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32, PT_FASTRCP=0|1.
 // AUTO picks the wavefront pipeline once a call has this many paths: below it the fixed
-// cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.
-constexpr uint64_t kWfAutoMinPaths = 1ull << 20;
+// cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.  Measured per
+// scene type (round 2, depth 16, ms megakernel / wavefront): mailbox scenes (the fused kernel)
+// gain at every size (CornellBox 128^2 x 1: 1.43 / 0.66), so do scenes with cooperative big
+// leaves (MedievalBoat 256^2 x 1: 62 / 35); other scenes from about 2^19 paths (Glossy 512^2 x 1:
+// 7.1 / 9.1, 512^2 x 2: 13.1 / 9.6).
+constexpr uint64_t kWfAutoMinPaths = 1ull << 19;
 
-LaunchOpts launch_opts(int mode, uint64_t paths) {
+LaunchOpts launch_opts(int mode, uint64_t paths, const SceneView& view) {
     LaunchOpts lo;
-    lo.wavefront = mode == PT_MODE_WAVEFRONT || (mode == PT_MODE_AUTO && paths >= kWfAutoMinPaths);
+    const uint64_t auto_min = (view.mailbox || view.big_leaf > 0) ? 1 : kWfAutoMinPaths;
+    lo.wavefront = mode == PT_MODE_WAVEFRONT || (mode == PT_MODE_AUTO && paths >= auto_min);
     if (const char* e = std::getenv("PT_KERNEL")) {
         lo.literal = !std::strcmp(e, "literal");
         if (!std::strcmp(e, "wavefront")) lo.wavefront = true;
@@ -782,7 +787,6 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     HIP_TRY(hipSetDevice(s->device));
     if (nframes == 0) return PT_OK;
     const uint64_t npix = (uint64_t)fp.width * fp.height;
-    const LaunchOpts lo = launch_opts(mode, npix * (accum ? nframes : 1));
     struct ProfScope {  // attach the scene's profiler to this thread for the launches below
         explicit ProfScope(KernelProfiler* p) { t_prof = p; }
         ~ProfScope() { t_prof = nullptr; }
@@ -801,6 +805,7 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     // the brute-force replay walks the BfNode tree without a stack (PT_BF_STACKLESS=0: the stack walk; A/B)
     if (const char* e = std::getenv("PT_BF_STACKLESS"))
         if (!std::strcmp(e, "0")) view.bfnode = nullptr;
+    const LaunchOpts lo = launch_opts(mode, npix * (accum ? nframes : 1), view);
     if (lo.wavefront) {
         uint64_t target = kWfTargetPaths;
         if (const char* e = std::getenv("PT_WF_PATHS")) target = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));  // A/B

@@ -349,19 +349,28 @@ def test_profile_records_every_launch(packed, monkeypatch):
 
 
 def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
+    """AUTO (pt_capi.hip launch_opts): the wavefront pipeline at every size on mailbox scenes (the
+    fused kernel) and on scenes with cooperative big leaves, from 2^19 paths on the others."""
     for k in ENV_KEYS:
         monkeypatch.delenv(k, raising=False)
-    p = packed["CornellBox"]
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        s.profile_enable(True)
-        s.render(p.meta_for(64, 64), 0, 2, 1, 2, pt_amd.MODE_AUTO)
-        small = s.profile_read()
-        s.profile_enable(True)
-        s.render(p.meta_for(512, 512), 0, 4, 1, 2, pt_amd.MODE_AUTO)  # 2^20 paths
-        large = s.profile_read()
-        s.profile_enable(False)
-    assert "k_regen" in small and "k_wf_trace" not in small and "k_wf_step" not in small
-    assert "k_wf_step" in large and "k_regen" not in large  # mailbox scene: fused trace + shade
+
+    def kernels(name, W, H, nframes):
+        p = packed[name]
+        with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+            s.profile_enable(True)
+            s.render(p.meta_for(W, H), 0, nframes, 1, 2, pt_amd.MODE_AUTO)
+            prof = s.profile_read()
+            s.profile_enable(False)
+        return prof
+
+    small = kernels("CornellBox", 64, 64, 2)
+    assert "k_wf_step" in small and "k_regen" not in small  # mailbox scene: fused trace + shade
+    glossy_small = kernels("CornellBox-Glossy", 64, 64, 2)
+    assert "k_regen" in glossy_small and "k_wf_trace" not in glossy_small
+    glossy_large = kernels("CornellBox-Glossy", 512, 512, 2)  # 2^19 paths
+    assert "k_wf_trace" in glossy_large and "k_regen" not in glossy_large
+    boat_small = kernels("MedievalBoat", 32, 24, 1)  # big leaves: cooperative turns in the wavefront
+    assert "k_wf_trace" in boat_small and "k_regen" not in boat_small
 
 
 def test_auto_large_render_matches_megakernel(packed, monkeypatch):
