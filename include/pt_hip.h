@@ -43,7 +43,7 @@ typedef enum {
 } pt_status;
 
 typedef enum {
-    PT_MODE_AUTO = 0,       /* wavefront when a call has >= 2^20 paths (W*H*nframes), else megakernel */
+    PT_MODE_AUTO = 0,       /* wavefront at every size on <= 64-entry (mailbox) and big-leaf scenes, else from 2^19 paths (W*H*nframes); megakernel below */
     PT_MODE_MEGAKERNEL = 1, /* one lane per pixel, frames looped in-lane */
     PT_MODE_WAVEFRONT = 2   /* SoA path/ray queues, per-bounce kernels, wave64 compaction */
 } pt_mode;
