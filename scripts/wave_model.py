@@ -39,7 +39,6 @@ def bbox(o,inv,mn,mx):
     tmin=max(-3e38,*np.minimum(t1,t2)); tmax=min(3e38,*np.maximum(t1,t2))
     if tmax>max(tmin,0): return tmin if tmin>0 else tmax
     return -1
-lo=np.array")])
 lo=np.array(B[0:3]); hi=np.array(B[3:6])
 rng=np.random.default_rng(1)
 seqs=[]
