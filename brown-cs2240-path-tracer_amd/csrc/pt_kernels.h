@@ -73,7 +73,7 @@ struct LaunchOpts {
     int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
     int regen = -1;        // fused kernel: streaming path regeneration (every extension launch refills): -1 default (off)
     long regen_target = 0; // paths in flight per part with regeneration (0 = the batch capacity)
-    int sort = -1;         // traversal pipeline: survivors grouped per shade block by 8 / 64 coherence keys (0 off): -1 default (64)
+    int sort = -1;         // traversal pipeline: survivors grouped per shade block by 8 / 64 / 512 coherence keys (0 off): -1 default (512)
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -145,7 +145,7 @@ struct WfStreams {
     // host polling of the regeneration loop: pinned words (2 per part) and their events
     uint32_t* h_poll = nullptr;
     hipEvent_t poll_ev[kMaxParts][2] = {};
-    int sort_bins = 0;     // LaunchOpts::sort: k_wf_shade groups a block's survivors by a coherence key of 8 / 64 values (0: off)
+    int sort_bins = 0;     // LaunchOpts::sort: k_wf_shade groups a block's survivors by a coherence key of 8 / 64 / 512 values (0: off)
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

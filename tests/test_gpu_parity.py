@@ -87,13 +87,14 @@ KERNELS = {
     # brute-force replay: the stack walk instead of the stackless pre-order walk (the default)
     "wavefront_bf_stack_replay": {"PT_KERNEL": "wavefront", "PT_BF_STACKLESS": "0"},
     "mega_bf_stack_replay": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1", "PT_BF_STACKLESS": "0"},
-    # traversal pipeline: survivors grouped by 8 / 64 coherence keys per shade block (queue order only; 64 is the default)
+    # traversal pipeline: survivors grouped by 8 / 64 / 512 coherence keys per shade block (queue order only; 512 is the default)
     "wavefront_sort8": {"PT_KERNEL": "wavefront", "PT_SORT": "8"},
     # traversal kernel with windows from group counters (PT_TRACE_DYN=1), also on a 1-block grid
     "wavefront_trace_dyn": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_MAILBOX": "0"},
     "wavefront_trace_dyn_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_WF_TRACE_BLOCKS": "1"},
     "wavefront_nosort_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "0", "PT_MAILBOX": "0"},
     "wavefront_sort64": {"PT_KERNEL": "wavefront", "PT_SORT": "64"},
+    "wavefront_sort512_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "512", "PT_MAILBOX": "0"},
     "wavefront_sort64_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_SORT": "64", "PT_MAILBOX": "0",
                                           "PT_WF_TRACE_BLOCKS": "1"},
 }
