@@ -206,7 +206,8 @@ __device__ __forceinline__ bool tri_hit(const TriRec& tr, const Ray& r, float& t
     // !(u < 0) & !(v < 0) & !(u > 1) & !(u + v > 1), NaN passing each test as in the early-out
     // chain: minNum/maxNum return the non-NaN operand, so the folded forms are the same
     // predicate in two compares
-    const bool ok_uv = !(fminf(u, v) < 0.0f) & !(fmaxf(u, u + v) > 1.0f);
+    const float lo = fminf(u, v), hi = fmaxf(u, u + v);
+    const bool ok_uv = !(lo < 0.0f) & !(hi > 1.0f);
     return ok_det & ok_uv & (t > eps);
 }
 template <bool FAST_RCP = false>

@@ -332,9 +332,9 @@ constexpr bool kBfPacked = false;  // (k_regen_bf, itself opt-in, uses bf_pairs:
 #ifndef PT_PHASE_TIMING
 #define PT_PHASE_TIMING 0
 #endif
+#if PT_PHASE_TIMING
 constexpr int kPhaseSlots = 16;
 constexpr int kPhaseWaves = 16384;
-#if PT_PHASE_TIMING
 __device__ unsigned long long g_phase[kPhaseWaves * kPhaseSlots];
 #endif
 __device__ __forceinline__ uint64_t phase_clock() {
