@@ -336,19 +336,25 @@ __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r
     if constexpr (!PIPE) {
         // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
         const int lim = (BIG && s.k < s.na && s.nt - s.na >= sc.big_leaf) ? s.na : s.nt;
+        // test j of the turn is entry k0 + j (a lane stops at lim): the position is not counted
+        // up per test (v_cndmask + v_add per test and lane), it follows from k0 once the turn ends
+        const int k0 = s.k;
+        const int bl = s.la + k0, br = s.lb - s.na + k0;  // record of entry k0 + j: (left ? bl : br) + j
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const bool live = j == 0 || s.k < lim;  // the first test always is
-            if (j > 0 && !__any(live)) break;      // every lane's leaf pair is done
-            const int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
+            const bool live = j == 0 || k0 + j < lim;  // the first test always is
+            if (j > 0 && !wave_any(live)) break;        // every lane's leaf pair is done
+            const int idx = (k0 + j < s.na ? bl : br) + j;
             float t;
             const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
                               ((s.best_t < 0.0f) | (t < s.best_t));
             s.best_t = take ? t : s.best_t;
             s.best = take ? idx : s.best;
             if (COUNT) cnt.tri_tests += live ? 1 : 0;
-            s.k += live ? 1 : 0;
         }
+        // tests made: 1, then one per j >= 1 with k0 + j < lim (a break comes only once every
+        // lane has k0 + j >= lim, so the count is the same with or without it)
+        s.k = max(k0 + 1, min(k0 + K, lim));
     } else {
         // the record of test j+1 is loaded (LDS) while test j computes; a lane whose leaf
         // pair ends loads a valid record it will not use
@@ -357,7 +363,7 @@ __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const bool live = j == 0 || s.k < s.nt;
-            if (j > 0 && !__any(live)) break;
+            if (j > 0 && !wave_any(live)) break;
             const int k1 = s.k + 1;
             const int idx1 = k1 < s.nt ? (k1 < s.na ? s.la + k1 : s.lb + (k1 - s.na)) : idx;
             TriRec nxt;
@@ -487,7 +493,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     if constexpr (IFIF) {
         if (want_node && state == 0) decide = lean_node_unit<COUNT>(sc, r, s, cnt);
         const bool in_leaf = (s.fl & (TF_LEAF | TF_DONE)) == TF_LEAF;
-        if (__any(in_leaf) && in_leaf) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE>(sc, r, s, cnt);
+        if (wave_any(in_leaf) && in_leaf) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE>(sc, r, s, cnt);
     } else {
         if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
             if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE, BIG>(sc, r, s, cnt);
@@ -547,7 +553,7 @@ __device__ __forceinline__ bool mb_leaf_loop(const SceneView& sc, const Ray& r, 
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const bool live = j == 0 || s.rem != 0;  // the first test always is
-        if (j > 0 && !__any(live)) break;
+        if (j > 0 && !wave_any(live)) break;
         const int uid = live ? (int)__builtin_ctzll(s.rem) : 0;
         s.rem &= s.rem - 1;
         const int rec = sc.mb_base + uid;

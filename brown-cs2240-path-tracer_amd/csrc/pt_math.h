@@ -51,6 +51,11 @@ PT_HD f3 reflect(f3 wi, f3 n) {
 }
 PT_HD f3 rcp3(f3 d) { return f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z}; }
 
+// Wave vote: true when the predicate holds on any active lane.  The ballot intrinsic keeps a
+// compare's lane mask in SGPRs (s_and with exec, branch on SCC); HIP's __any materialises the
+// bool in a VGPR and compares it again (v_cndmask + v_cmp: two VALU slots per vote).
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
 // Correctly rounded 1/x without the IEEE division sequence: the hardware reciprocal
 // (v_rcp_f32, about 1 ulp) refined by kRcpSteps Newton steps e = 1 - x*y, y += y*e, each an
 // exact-residual FMA pair.  Valid for 2^-126 <= |x| <= kRcpHi, where it equals 1.0f / x bit

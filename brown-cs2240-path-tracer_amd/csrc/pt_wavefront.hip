@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
         while (flushed < (jl + 1) * kWinRays) {
             const uint32_t jf = flushed / kWinRays;
             const bool handed = jf < jl || cur == jl * kWinRays + wv;
-            if (!handed || __any(has && sq < flushed + kWinRays)) break;
+            if (!handed || wave_any(has && sq < flushed + kWinRays)) break;
             const uint32_t wf = wtab[jf % kWinTab];
             const uint32_t fv = wcount(wf);
             if (lane < fv) wb.hitq[wf * kWinRays + lane] = ring[(flushed + lane) & (kHitRing - 1)];
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
                 cur = min(cur + (uint32_t)__popcll(need), wend);
             }
         }
-        if (!__any(has)) {
+        if (!wave_any(has)) {
             if (nv == 0 && cur == jl * kWinRays + wv && flushed >= (jl + 1) * kWinRays) break;  // all done
             continue;  // ring full with nothing in flight: the flush above frees it
         }
@@ -458,7 +458,7 @@ __device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool
         const fv2 bu = inv * fma2(sz, rz, fma2(sy, ry, sx * rx));
         const bool ok0 = valid & !(det.x > -1e-8f && det.x < 1e-8f) & !(bu.x < 0.0f) & !(bu.x > 1.0f);
         const bool ok1 = valid & !(det.y > -1e-8f && det.y < 1e-8f) & !(bu.y < 0.0f) & !(bu.y > 1.0f);
-        if (!__any(ok0 | ok1)) continue;  // wave-uniform
+        if (!wave_any(ok0 | ok1)) continue;  // wave-uniform
         const fv2 cx = fma2(sy, e1z, -(sz * e1y)), cy = fma2(sz, e1x, -(sx * e1z)), cz = fma2(sx, e1y, -(sy * e1x));
         const fv2 bv = inv * fma2(dz, cz, fma2(dy, cy, dx * cx));
         const fv2 t = inv * fma2(e2z, cz, fma2(e2y, cy, e2x * cx));
@@ -509,7 +509,7 @@ __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ra
     uint64_t tested = 0;
     int best = -1;
     float best_t = -1.0f;
-    while (__any(pend != 0)) {
+    while (wave_any(pend != 0)) {
         if (pend != 0) {
             const int n = (int)__builtin_ctzll(pend);
             pend &= pend - 1;
@@ -562,6 +562,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     // ray-triangle-intersection.wgsl:15-24) the rest cannot make a hit and is skipped for the wave
     uint64_t hits = 0;
     int nh = 0;
+    const uint64_t vmask = __builtin_amdgcn_ballot_w64(valid);  // loop-invariant part of phase 1's vote
     float tmin = 3.0e38f;  // smallest t of any entry this ray hits
     if (PK && todo == ~0ull) {  // every entry: in pairs, packed f32 (bf_pairs)
         bf_pairs<FAST_RCP>(sc, r, valid, slot, nslots, hits, nh, tmin);
@@ -575,8 +576,13 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
         const f3 sv = r.o - v0;
         const float bu = inv_det * dot(sv, rce2);
-        const bool ok_u = valid & !(det > -1e-8f && det < 1e-8f) & !(bu < 0.0f) & !(bu > 1.0f);
-        if (!__any(ok_u)) return;  // wave-uniform
+        const bool ok_det = !(det > -1e-8f && det < 1e-8f), ok_lo = !(bu < 0.0f), ok_hi = !(bu > 1.0f);
+        const bool ok_u = valid & ok_det & ok_lo & ok_hi;
+        // the vote as SGPR masks of the single compares (one ballot of the combined bool costs
+        // two VALU slots per entry: v_cndmask + v_cmp)
+        if ((vmask & __builtin_amdgcn_ballot_w64(ok_det) &
+             __builtin_amdgcn_ballot_w64(ok_lo) & __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
+            return;  // wave-uniform
         const f3 sce1 = cross(sv, e1);
         const float bv = inv_det * dot(r.d, sce1);
         const float t = inv_det * dot(e2, sce1);
@@ -625,7 +631,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     }
     TravLean s;
     trav_init(s, valid && (COUNT || hits != 0));
-    while (__any(!trav_finished(s))) {
+    while (wave_any(!trav_finished(s))) {
         if (!trav_finished(s)) {
             mb_node_unit<COUNT>(sc, r, s, c);
             uint64_t rh = s.rem & hits;
@@ -1019,7 +1025,7 @@ void k_regen_bf(SceneView sc, FrameParams fp, uint32_t frame0, uint32_t nframes,
             if (COUNT) { c.samples++; c.ext_queries++; }
         }
         const bool live = phase != kIdle;
-        if (!__any(live)) break;  // wave-uniform: every lane's frames are done
+        if (!wave_any(live)) break;  // wave-uniform: every lane's frames are done
         float t;
         const int rec = bf_closest<FAST_RCP, COUNT, true>(sc, gtris, ray, live, l.slot, nslots, l.stack, blockDim.x, c, t);
         if (live) {
