@@ -591,7 +591,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
             if (nh < nslots) slot[64 * nh] = t;
             ++nh;
             hits |= 1ull << u;
-            tmin = fminf(tmin, t);
+            tmin = t < tmin ? t : tmin;  // = fminf here (t > 1e-8, never NaN) without its two canonicalising v_max
         }
     };
     if (todo == ~0ull) {  // every entry (a constant in the instances without the cull)
