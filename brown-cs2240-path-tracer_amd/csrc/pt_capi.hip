@@ -95,6 +95,10 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
         std::memset(&o, 0, sizeof o);
         o.Ns = m[0]; o.Ni = m[1]; o.illum = m[2];
         for (int c = 0; c < 3; ++c) { o.Kd[c] = m[6 + c]; o.Ks[c] = m[9 + c]; o.Ke[c] = m[12 + c]; }
+        // the material's constant quotients, once per scene instead of per path and bounce: the
+        // same correctly rounded f32 divisions the device would make (no contraction, no FTZ)
+        o.kd_pi0 = o.Kd[0] / kPI; o.kd_pi1 = o.Kd[1] / kPI; o.kd_pi2 = o.Kd[2] / kPI;
+        o.phong = (o.Ns + 2.0f) / (2.0f * kPI);
     }
     L.info.materials = (uint32_t)nobj;
 

@@ -661,6 +661,8 @@ __device__ __forceinline__ Hit hit_data(const SceneView& sc, const Ray& r, int r
 struct Mat {
     float Ns, illum;
     f3 Kd, Ks, Ke;
+    f3 Kd_pi;     // Kd / kPI (Material::kd_pi*, made by pt_scene_create)
+    float phong;  // (Ns + 2) / (2 kPI) (Material::phong)
 };
 __device__ __forceinline__ Mat load_mat(const SceneView& sc, int id) {
     const float4* mp = reinterpret_cast<const float4*>(sc.mats + id);
@@ -668,6 +670,7 @@ __device__ __forceinline__ Mat load_mat(const SceneView& sc, int id) {
     Mat m;
     m.Ns = a.x; m.illum = a.z;
     m.Kd = mk(b.x, b.y, b.z); m.Ks = mk(c.x, c.y, c.z); m.Ke = mk(e.x, e.y, e.z);
+    m.Kd_pi = mk(b.w, c.w, e.w); m.phong = a.w;
     return m;
 }
 

@@ -65,10 +65,10 @@ inline void tri_set(Tri& t, const float v0[3], const float e1[3], const float e2
 static_assert(sizeof(Tri) == 48, "tri record is 3 x 16 B");
 
 struct alignas(16) Material {
-    float Ns, Ni, illum, pad0;
-    float Kd[3], pad1;
-    float Ks[3], pad2;
-    float Ke[3], pad3;
+    float Ns, Ni, illum, phong;  // phong = (Ns + 2) / (2 pi), f32, as program-raymarch.wgsl:271
+    float Kd[3], kd_pi0;         // kd_pi* = Kd / pi per channel, f32 (program-raymarch.wgsl:165,279)
+    float Ks[3], kd_pi1;
+    float Ke[3], kd_pi2;
 };
 static_assert(sizeof(Material) == 64, "material is 4 x 16 B");
 

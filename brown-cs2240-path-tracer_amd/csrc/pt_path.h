@@ -37,7 +37,7 @@ __device__ __forceinline__ f3 nee_contrib(const Mat& m, f3 wi, f3 hp, f3 hn, f3 
             brdf = m.Ks * sf;
         }
     } else {
-        brdf = m.Kd / kPI;
+        brdf = m.Kd_pi;  // = m.Kd / kPI, bit for bit (precomputed per material)
     }
     float d1 = dot(sh.n, -ldir);
     float d2 = dot(hn, ldir);
@@ -97,12 +97,12 @@ __device__ __forceinline__ void bsdf_continue(const Mat& m, f3 hp, f3 hn, Ray& r
         if (q < 0.0f) {
             brdf = mk(0.0f, 0.0f, 0.0f);
         } else {
-            float sf = ((m.Ns + 2.0f) / (2.0f * kPI)) * pow_p(q, m.Ns);
+            float sf = m.phong * pow_p(q, m.Ns);  // m.phong = (m.Ns + 2) / (2 kPI)
             brdf = m.Ks * sf;
             if (depth == 0) spec = true;
         }
     } else {
-        brdf = m.Kd / kPI;
+        brdf = m.Kd_pi;  // = m.Kd / kPI, bit for bit (precomputed per material)
     }
     float cosn = dot(nr.d, hn) + 0.0f;  // vec4 dot: + w*w (= +0)
     f3 f = (brdf * cosn) / (pdf * rr);
