@@ -120,6 +120,21 @@ def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int
     return sum(cands[k][field] for k in timed) / len(timed), src
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: run this same command as N ranks
+    under torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) and return its exit
+    code.  The parent has not touched the GPU (torch is not even imported yet): the ranks are
+    fresh child processes, so no process that initialised HIP is replaced."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
 def metric_name(scene: str, W: int, H: int, depth: int) -> str:
     """BASELINE.json's metric, for the workload actually run (its headline is CornellBox 1024^2 depth 8)."""
     return f"Msamples/s (paths/s) {scene} {W}x{H} depth {depth}"
@@ -139,6 +154,8 @@ def native_multi(args):
                                     args.all_meshes)
     W, H = int(meta[0]), int(meta[1])
     mode = {"auto": pt_amd.MODE_AUTO, "megakernel": pt_amd.MODE_MEGAKERNEL, "wavefront": pt_amd.MODE_WAVEFRONT}[args.mode]
+    if args.reduce:
+        pt_amd.set_option("reduce", args.reduce)
     scenes = [pt_amd.Scene(tri, bvh, device=g) for g in range(n)]
     acc = np.zeros((H, W, 3), np.float32)
     for _ in range(args.warmup):
@@ -163,7 +180,7 @@ def native_multi(args):
                                   f"round-robin over {n} devices in one process (pt_render_multi), host accumulator "
                                   f"(PCIe upload + read-back in the step)",
                       "mode": args.mode, "samples_per_step": total,
-                      "reduce": os.environ.get("PT_REDUCE", "rccl" if n > 1 else "none")}}
+                      "reduce": (args.reduce or "rccl") if n > 1 else "none"}}
     print(json.dumps(out), flush=True)
 
 
@@ -183,17 +200,26 @@ def main():
     ap.add_argument("--all-meshes", action="store_true", help="every primitive of the scene (reference: first only)")
     ap.add_argument("--native-multi", action="store_true",
                     help="one process drives --gpus devices through pt_render_multi (RCCL reduce inside the library)")
+    ap.add_argument("--reduce", choices=["rccl", "ordered"], help="--native-multi: pt_render_multi's reduction")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch HIP events")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the rank plumbing (launch, sharding, reduce, timing, JSON line); renders "
+                         "nothing and reports no value")
     args = ap.parse_args()
+
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None and not args.native_multi:
+        sys.exit(launch_ranks(args.gpus))  # N ranks of this command; nothing here touched the GPU
+    world = int(world_env or "1")
+    if args.gpus > 1 and world != args.gpus and not args.native_multi:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: n_gpus must be the ranks that render")
 
     import torch
     import torch.distributed as dist
 
-    import pt_amd
     from pt_amd.shard import frames_for_rank, reduce_accum
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.native_multi:
         if world != 1:
             raise SystemExit("--native-multi is single-process (it drives --gpus devices itself)")
@@ -202,9 +228,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # PT_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with several ranks on fewer GPUs (the
     # reduce then goes through host memory); the driver's runs use RCCL, one rank per GPU
-    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+    backend = os.environ.get("PT_BENCH_BACKEND", "gloo" if args.dry_run else "nccl")
     if world > 1:
         dist.init_process_group(backend)
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    if args.dry_run:
+        return dry_run(args, rank, world, ranks_seen, backend, dist, frames_for_rank, reduce_accum)
+    import pt_amd
     if backend == "gloo":
         local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
@@ -313,7 +343,7 @@ def main():
             "metric": metric_name(args.scene, W, H, args.depth),
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
@@ -330,6 +360,7 @@ def main():
                                                                          f", {backend} sum-reduce through host memory (rehearsal)")
                                                                         if world > 1 else ""),
                        "mode": args.mode, "bvh": args.bvh, "samples_per_step": total_samples,
+                       "ranks": ranks_seen, "backend": backend if world > 1 else None,
                        "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -358,6 +389,37 @@ def main():
             out["cpu_baseline"] = cpu_baseline(tri, bvh, meta, args.depth)
         print(json.dumps(out), flush=True)
     scene.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run(args, rank, world, ranks_seen, backend, dist, frames_for_rank, reduce_accum):
+    """--dry-run: the N > 1 plumbing without a GPU (CPU tests): each rank takes its frame share,
+    a CPU accumulator holding its frame count goes through the same reduce, the step is timed
+    with the same barrier + max-over-ranks, and rank 0 prints the line (value null)."""
+    import torch
+    W, H = args.width, args.height
+    frame0, nframes, fstride = frames_for_rank(rank, world, args.spp)
+    acc = torch.zeros((H, W, 3), dtype=torch.float32)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        acc.fill_(float(nframes))
+        reduce_accum(acc, dist)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        frames_total = float(acc[0, 0, 0])  # the reduce summed every rank's frame count
+        print(json.dumps({"metric": metric_name(args.scene, W, H, args.depth), "value": None, "unit": "Msamples/s",
+                          "n_gpus": ranks_seen, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "dry run (no render)",
+                          "dry_run": True, "config": {"ranks": ranks_seen, "backend": backend if world > 1 else None,
+                                                      "frames_reduced": frames_total}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -55,6 +55,81 @@ struct Packed {
     }
 };
 
+// ---------------------------------------------------------------------------------------------
+// Options (pt_set_option): the process-wide table of kernel-selection switches.  Nothing is read
+// from the environment; tests and A/B scripts set these explicitly.
+// ---------------------------------------------------------------------------------------------
+enum OptKind { OPT_BOOL, OPT_INT, OPT_ENUM };
+struct OptSpec {
+    const char* name;
+    OptKind kind;
+    const char* choices;  // OPT_ENUM: '|'-separated values
+};
+constexpr OptSpec kOptSpecs[] = {
+    {"kernel", OPT_ENUM, "auto|mega|wavefront|literal"},
+    {"trav", OPT_ENUM, "nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32"},
+    {"lds", OPT_BOOL, nullptr},          {"fastrcp", OPT_BOOL, nullptr},     {"pipe", OPT_BOOL, nullptr},
+    {"ifif", OPT_BOOL, nullptr},         {"dual", OPT_BOOL, nullptr},        {"stagger", OPT_BOOL, nullptr},
+    {"fuse", OPT_BOOL, nullptr},         {"fuse_gen", OPT_BOOL, nullptr},    {"bf", OPT_BOOL, nullptr},
+    {"mailbox", OPT_BOOL, nullptr},      {"persist", OPT_BOOL, nullptr},     {"regen", OPT_BOOL, nullptr},
+    {"regen_bf", OPT_BOOL, nullptr},     {"bf_stackless", OPT_BOOL, nullptr}, {"trace_dyn", OPT_BOOL, nullptr},
+    {"packet", OPT_BOOL, nullptr},
+    {"parts", OPT_INT, nullptr},         {"cull", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
+    {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
+    {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr},
+    {"regen_target", OPT_INT, nullptr},  {"trace_watchdog", OPT_INT, nullptr},
+    {"mb_uid_order", OPT_ENUM, "forward|reverse"},
+    {"reduce", OPT_ENUM, "rccl|ordered"},
+};
+constexpr int kNumOpts = (int)(sizeof(kOptSpecs) / sizeof(kOptSpecs[0]));
+
+std::mutex g_opt_mu;
+std::string g_opt_val[kNumOpts];  // "" = default
+
+int opt_index(const char* name) {
+    for (int i = 0; i < kNumOpts; ++i)
+        if (!std::strcmp(name, kOptSpecs[i].name)) return i;
+    return -1;
+}
+
+bool opt_valid(const OptSpec& s, const char* v) {
+    if (!*v) return false;
+    if (s.kind == OPT_BOOL) return !std::strcmp(v, "0") || !std::strcmp(v, "1");
+    if (s.kind == OPT_INT) {
+        char* end = nullptr;
+        const long long x = std::strtoll(v, &end, 10);
+        return *end == 0 && x >= 0 && x <= 0x7fffffffLL;
+    }
+    const size_t n = std::strlen(v);
+    for (const char* c = s.choices; *c;) {
+        const char* bar = std::strchr(c, '|');
+        const size_t len = bar ? (size_t)(bar - c) : std::strlen(c);
+        if (len == n && !std::strncmp(c, v, n)) return true;
+        c += len + (bar ? 1 : 0);
+    }
+    return false;
+}
+
+// Snapshot of the table, taken once per call (a concurrent pt_set_option affects later calls only).
+struct Opts {
+    std::string v[kNumOpts];
+    const std::string& get(const char* name) const {
+        static const std::string empty;
+        const int i = opt_index(name);
+        return i >= 0 ? v[i] : empty;
+    }
+    bool has(const char* name) const { return !get(name).empty(); }
+    long num(const char* name, long def) const { return has(name) ? std::atol(get(name).c_str()) : def; }
+    int flag(const char* name, int def) const { return has(name) ? (get(name) == "1" ? 1 : 0) : def; }
+    bool is(const char* name, const char* val) const { return get(name) == val; }
+};
+Opts opts_snapshot() {
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    Opts o;
+    for (int i = 0; i < kNumOpts; ++i) o.v[i] = g_opt_val[i];
+    return o;
+}
+
 struct HostLayout {
     std::vector<Node> nodes;
     std::vector<Tri> tris;
@@ -190,7 +265,7 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
     // Mailboxing: a leaf entry tested twice by one query gives the same t both
     // times and the closest-hit update is strict-<, so repeats never change the result.  With
     // at most 64 distinct entries a query keeps the set it has tested in one 64-bit mask.
-    // uids follow first appearance (PT_MB_UID_ORDER=reverse numbers them backwards: tests
+    // uids follow first appearance (option mb_uid_order=reverse numbers them backwards: tests
     // use it to exercise the tie-break of the uid-ordered leaf loop).
     {
         std::map<std::array<int32_t, 4>, int32_t> ids;
@@ -207,8 +282,7 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
         const int32_t U = (int32_t)first.size();
         L.mailbox = U >= 1 && U <= 64;
         if (L.mailbox) {
-            const char* order = std::getenv("PT_MB_UID_ORDER");
-            const bool rev = order && !std::strcmp(order, "reverse");
+            const bool rev = opts_snapshot().is("mb_uid_order", "reverse");
             for (auto& u : uid) u = rev ? U - 1 - u : u;
             for (size_t r = 0; r < entry.size(); ++r) L.tris[r].uid = uid[r];
             L.mb_base = (int32_t)L.tris.size();
@@ -330,6 +404,42 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 }  // namespace
+
+extern "C" {
+
+int pt_set_option(const char* name, const char* value) {
+    if (!name) return fail(PT_ERR_INVALID, "option name is NULL");
+    const int i = opt_index(name);
+    if (i < 0) return fail(PT_ERR_INVALID, std::string("unknown option '") + name + "'");
+    if (value && !opt_valid(kOptSpecs[i], value))
+        return fail(PT_ERR_INVALID, std::string("bad value '") + value + "' for option '" + name + "'");
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    g_opt_val[i] = value ? value : "";
+    return PT_OK;
+}
+
+int pt_get_option(const char* name, char* buf, size_t cap) {
+    if (!name || !buf || cap == 0) return fail(PT_ERR_INVALID, "null argument");
+    const int i = opt_index(name);
+    if (i < 0) return fail(PT_ERR_INVALID, std::string("unknown option '") + name + "'");
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    if (g_opt_val[i].size() + 1 > cap) return fail(PT_ERR_INVALID, "buffer too small");
+    std::memcpy(buf, g_opt_val[i].c_str(), g_opt_val[i].size() + 1);
+    return PT_OK;
+}
+
+void pt_reset_options(void) {
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    for (auto& v : g_opt_val) v.clear();
+}
+
+#ifndef PT_SOURCE_HASH
+#define PT_SOURCE_HASH "unknown"
+#endif
+const char* pt_build_id(void) { return PT_SOURCE_HASH; }
+
+}  // extern "C"
+
 
 struct pt_scene {
     int device = 0;
@@ -627,8 +737,8 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
     return PT_OK;
 }
 
-// PT_MODE_* -> pipeline.  A/B overrides: PT_KERNEL=literal|mega|wavefront, PT_LDS=0|1,
-// PT_TRAV=nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32, PT_FASTRCP=0|1.
+// PT_MODE_* -> pipeline.  A/B overrides (pt_set_option): kernel=literal|mega|wavefront, lds=0|1,
+// trav=nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32, fastrcp=0|1, ...
 // AUTO picks the wavefront pipeline once a call has this many paths: below it the fixed
 // cost of its ~2(D+1) launches per batch outweighs its better SIMD utilisation.  Measured per
 // scene type (round 2, depth 16, ms megakernel / wavefront): mailbox scenes (the fused kernel)
@@ -637,33 +747,42 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 // 7.1 / 9.1, 512^2 x 2: 13.1 / 9.6).
 constexpr uint64_t kWfAutoMinPaths = 1ull << 19;
 
-LaunchOpts launch_opts(int mode, uint64_t paths, const SceneView& view) {
+LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView& view) {
     LaunchOpts lo;
     const uint64_t auto_min = (view.mailbox || view.big_leaf > 0) ? 1 : kWfAutoMinPaths;
     lo.wavefront = mode == PT_MODE_WAVEFRONT || (mode == PT_MODE_AUTO && paths >= auto_min);
-    if (const char* e = std::getenv("PT_KERNEL")) {
-        lo.literal = !std::strcmp(e, "literal");
-        if (!std::strcmp(e, "wavefront")) lo.wavefront = true;
-        if (!std::strcmp(e, "mega") || lo.literal) lo.wavefront = false;
+    if (o.has("kernel")) {
+        lo.literal = o.is("kernel", "literal");
+        if (o.is("kernel", "wavefront")) lo.wavefront = true;
+        if (o.is("kernel", "mega") || lo.literal) lo.wavefront = false;
     }
-    if (const char* e = std::getenv("PT_LDS")) lo.lds = std::strcmp(e, "0") != 0;
-    if (const char* e = std::getenv("PT_FASTRCP")) lo.fast_rcp = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_PIPE")) lo.pipe = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_IFIF")) lo.ifif = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_PARTS")) lo.parts = std::atoi(e);
-    if (const char* e = std::getenv("PT_CULL")) lo.cull = std::atoi(e);
-    if (const char* e = std::getenv("PT_FUSE_GEN")) lo.fuse_gen = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_DUAL")) lo.dual = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_STAGGER")) lo.stagger = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_REGEN_BF")) lo.regen_bf = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_PERSIST")) lo.persist = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_FUSE")) lo.fuse = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_BF")) lo.bf = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_MAILBOX")) lo.mailbox = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_REGEN")) lo.regen = std::strcmp(e, "0") != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_REGEN_TARGET")) lo.regen_target = std::atol(e);
-    if (const char* e = std::getenv("PT_SORT")) lo.sort = std::atoi(e);  // 1 / 8: direction octant; 64: + origin octant
-    if (const char* e = std::getenv("PT_TRAV")) lo.trav = !std::strcmp(e, "nested") ? 0 : !std::strcmp(e, "pred") ? 2 : !std::strcmp(e, "flat1") ? 1 : !std::strcmp(e, "lean") ? 3 : !std::strcmp(e, "lean2") ? 4 : !std::strcmp(e, "lean4") ? 5 : !std::strcmp(e, "lean8") ? 6 : !std::strcmp(e, "lean16") ? 7 : !std::strcmp(e, "lean32") ? 8 : -1;
+    lo.lds = o.flag("lds", 1) != 0;
+    lo.fast_rcp = o.flag("fastrcp", lo.fast_rcp);
+    lo.pipe = o.flag("pipe", lo.pipe);
+    lo.ifif = o.flag("ifif", lo.ifif);
+    lo.parts = (int)o.num("parts", lo.parts);
+    lo.cull = (int)o.num("cull", lo.cull);
+    lo.fuse_gen = o.flag("fuse_gen", lo.fuse_gen);
+    lo.dual = o.flag("dual", lo.dual);
+    lo.stagger = o.flag("stagger", lo.stagger);
+    lo.regen_bf = o.flag("regen_bf", lo.regen_bf);
+    lo.persist = o.flag("persist", lo.persist);
+    lo.fuse = o.flag("fuse", lo.fuse);
+    lo.bf = o.flag("bf", lo.bf);
+    lo.mailbox = o.flag("mailbox", lo.mailbox);
+    lo.regen = o.flag("regen", lo.regen);
+    lo.regen_target = o.num("regen_target", lo.regen_target);
+    lo.sort = (int)o.num("sort", lo.sort);  // 1 / 8: direction octant; 64: + origin octant; 512: + 4^3 origin cells
+    lo.packet = o.flag("packet", lo.packet);
+    lo.trace_dyn = o.flag("trace_dyn", lo.trace_dyn);
+    lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
+    lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
+    lo.bf_slots = (int)o.num("bf_slots", -1);
+    if (o.has("trav")) {
+        static const char* const names[] = {"nested", "flat1", "pred", "lean", "lean2", "lean4", "lean8", "lean16", "lean32"};
+        for (int k = 0; k < 9; ++k)
+            if (o.is("trav", names[k])) lo.trav = k;
+    }
     return lo;
 }
 
@@ -758,24 +877,27 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
 // kTraceWatchdogTicks) sets ctl[WF_WATCHDOG] and leaves its state in ctl[WF_SNAP..]; later
 // launches of the scene skip their work.  The pinned mirror h_ctl receives the control words
 // after every wavefront render on its stream; once that copy has landed (the caller synchronised,
-// or the blocking calls' own synchronisation) the flag is reported here and cleared on the device
-// (ordered on `stream`) and in the mirror.
-int take_watchdog(pt_scene* s, hipStream_t stream) {
+// or the blocking calls' own synchronisation) the flag is reported here — by whichever call of
+// the scene comes next, megakernel or wavefront — and cleared.  The failure path waits for the
+// device first, so no mirror copy still in flight can bring the flag back after the clear and
+// report the same failure twice.
+int take_watchdog(pt_scene* s) {
     if (!s->h_ctl) return PT_OK;
     int h = 0;
     while (h < kMaxParts && !__atomic_load_n(&s->h_ctl[h * WF_CTL_WORDS + WF_WATCHDOG], __ATOMIC_ACQUIRE)) ++h;
     if (h == kMaxParts) return PT_OK;
+    HIP_TRY(hipDeviceSynchronize());  // every pending mirror copy of the scene has landed
     uint32_t v[WF_SNAP_WORDS];
     std::memcpy(v, s->h_ctl + h * WF_CTL_WORDS + WF_SNAP, sizeof v);
     for (int k = 0; k < kMaxParts; ++k)
-        HIP_TRY(hipMemsetAsync(s->wf.ctl + k * WF_CTL_WORDS + WF_WATCHDOG, 0,
-                               (WF_SNAP + WF_SNAP_WORDS - WF_WATCHDOG) * sizeof(uint32_t), stream));
+        HIP_TRY(hipMemset(s->wf.ctl + k * WF_CTL_WORDS + WF_WATCHDOG, 0,
+                          (WF_SNAP + WF_SNAP_WORDS - WF_WATCHDOG) * sizeof(uint32_t)));
     std::memset(s->h_ctl, 0, 4 * kMaxParts * WF_CTL_WORDS);
-    char msg[320];
+    char msg[360];
     std::snprintf(msg, sizeof(msg),
-                  "wavefront trace gave up after kTraceWatchdog iterations (result invalid); first wave: count=%u "
-                  "nwaves=%u w=%u J=%u jl=%u wv=%u nv=%u cur=%u flushed=%u in_flight=%u mask=%08x%08x queue=%u",
-                  v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[11], v[10], v[12]);
+                  "wavefront trace gave up after its watchdog limit (result invalid); first wave: count=%u "
+                  "nwaves=%u w=%u g=%u G=%u jl=%u wv=%u nv=%u cur=%u flushed=%u in_flight=%u mask=%08x%08x queue=%u",
+                  v[0], v[1], v[2], v[3], v[13], v[4], v[5], v[6], v[7], v[8], v[9], v[11], v[10], v[12]);
     return fail(PT_ERR_HIP, msg);
 }
 
@@ -796,36 +918,37 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         ~ProfScope() { t_prof = nullptr; }
     } prof_scope(s->prof_on ? &s->prof : nullptr);
     SceneView view = s->view;
-    if (const char* e = std::getenv("PT_NODE_BIAS")) view.node_bias = std::max(1, std::atoi(e));  // A/B runs
+    const Opts o = opts_snapshot();
+    if (o.has("node_bias")) view.node_bias = std::max(1L, o.num("node_bias", 1));  // A/B runs
     // big leaves (lean traversal): a ray reaching a leaf of >= big_leaf entries has it tested by the
     // whole wave (pt_device.h big_turn); default 128 (MedievalBoat 2.3x, in-process A/B; 64 is 1.5 %
     // faster there but 12 % slower on the 1M-triangle synthetic scene, whose many 64..127-entry
-    // leaves waste half a cooperative step each); PT_BIG_LEAF=n sets it, 0 turns it off
+    // leaves waste half a cooperative step each); option big_leaf=n sets it, 0 turns it off
     {
-        int big = kBigLeafDefault;
-        if (const char* e = std::getenv("PT_BIG_LEAF")) big = std::max(0, std::atoi(e));
-        view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? big : 0;
+        const long big = o.num("big_leaf", kBigLeafDefault);
+        view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? (int32_t)big : 0;
     }
-    // the brute-force replay walks the BfNode tree without a stack (PT_BF_STACKLESS=0: the stack walk; A/B)
-    if (const char* e = std::getenv("PT_BF_STACKLESS"))
-        if (!std::strcmp(e, "0")) view.bfnode = nullptr;
-    const LaunchOpts lo = launch_opts(mode, npix * (accum ? nframes : 1), view);
+    // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
+    if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
+    const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);
+    if ((rc = take_watchdog(s)) != PT_OK) return rc;  // an earlier asynchronous render failed
     if (lo.wavefront) {
-        uint64_t target = kWfTargetPaths;
-        if (const char* e = std::getenv("PT_WF_PATHS")) target = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));  // A/B
+        const uint64_t target = (uint64_t)std::max(1L, o.num("wf_paths", (long)kWfTargetPaths));  // A/B
         // at least two frames per batch when the call has two (images above the target, e.g.
         // 4096^2): the batch's parts run on their own streams and overlap (+29 % at 4096^2)
         const uint64_t all = npix * (accum ? nframes : 1);
         const uint64_t two = 2 * npix <= 0x7fffffffull ? 2 * npix : npix;
         const uint64_t want = std::max<uint64_t>(std::min<uint64_t>(all, two), std::min<uint64_t>(all, target));
-        if ((rc = take_watchdog(s, stream)) != PT_OK) return rc;  // an earlier asynchronous render failed
         int rc2 = ensure_wavefront(s, want);
         // the two-frame minimum doubles the state of images above the batch target (~188 B/path):
         // fall back to one frame per batch when that does not fit
         if (rc2 == PT_ERR_NOMEM && want > std::min<uint64_t>(all, npix)) rc2 = ensure_wavefront(s, std::min<uint64_t>(all, npix));
         if (rc2 != PT_OK) return rc2;
-        // radiance: the batch's paths, or (regeneration) the call's frames up to kRadMaxPaths, whole frames
-        const uint64_t rad_want = std::max<uint64_t>(s->wf.capacity, std::min<uint64_t>(all, std::max<uint64_t>(npix, kRadMaxPaths / npix * npix)));
+        // radiance: the batch's paths; with streaming regeneration (opt-in, when it can run) the
+        // call's frames up to kRadMaxPaths, whole frames
+        const bool regen = lo.regen > 0 && s->ws.h_poll != nullptr;
+        const uint64_t rad_want = regen ? std::max<uint64_t>(s->wf.capacity, std::min<uint64_t>(all, std::max<uint64_t>(npix, kRadMaxPaths / npix * npix)))
+                                        : s->wf.capacity;
         rc2 = ensure_rad(s, rad_want);
         if (rc2 == PT_ERR_NOMEM && rad_want > s->wf.capacity) rc2 = ensure_rad(s, s->wf.capacity);
         if (rc2 != PT_OK) return rc2;
@@ -860,19 +983,13 @@ int pt_render_async(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t
 }
 
 // After a synchronised call: a trace wave that hit kTraceWatchdog left a flag (cleared here).
-static int check_watchdog(pt_scene* s) {
-    int rc = take_watchdog(s, s->stream);
-    if (rc != PT_OK) hipStreamSynchronize(s->stream);  // the flag reset is done before the error returns
-    return rc;
-}
+static int check_watchdog(pt_scene* s) { return take_watchdog(s); }
 
 int pt_scene_check(pt_scene* s) {
     if (!s) return fail(PT_ERR_INVALID, "null scene");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipDeviceSynchronize());  // every render of the scene, on whatever stream, has finished
-    int rc = take_watchdog(s, nullptr);
-    if (rc != PT_OK) hipDeviceSynchronize();
-    return rc;
+    return take_watchdog(s);
 }
 
 // The blocking calls' own stream, created on first use: asynchronous callers never pay for a
@@ -1037,6 +1154,7 @@ namespace {
 struct RcclApi {
     bool ok = false;
     ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
@@ -1045,29 +1163,51 @@ struct RcclApi {
 
 std::mutex g_rccl_mu;
 
-// librccl: the copy already in the process (e.g. torch's) if there is one, else the system's
+// librccl: the copy already in the process (e.g. torch's) if there is one, else the system's.
+// Resolved once (a function-local static: thread-safe initialisation).
 const RcclApi& rccl_api() {
-    static RcclApi a;
-    static bool tried = false;
-    if (tried) return a;
-    tried = true;
-    void* h = nullptr;
-    for (const char* n : {"librccl.so.1", "librccl.so"})
-        if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD))) break;
-    for (const char* n : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
-        if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
-    if (!h) return a;
-    a.comm_init_all = reinterpret_cast<decltype(a.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
-    a.reduce = reinterpret_cast<decltype(a.reduce)>(dlsym(h, "ncclReduce"));
-    a.group_start = reinterpret_cast<decltype(a.group_start)>(dlsym(h, "ncclGroupStart"));
-    a.group_end = reinterpret_cast<decltype(a.group_end)>(dlsym(h, "ncclGroupEnd"));
-    a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
-    a.ok = a.comm_init_all && a.reduce && a.group_start && a.group_end && a.error_string;
-    return a;
+    static const RcclApi api = [] {
+        RcclApi a;
+        void* h = nullptr;
+        for (const char* n : {"librccl.so.1", "librccl.so"})
+            if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD))) break;
+        for (const char* n : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
+            if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return a;
+        a.comm_init_all = reinterpret_cast<decltype(a.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+        a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        a.reduce = reinterpret_cast<decltype(a.reduce)>(dlsym(h, "ncclReduce"));
+        a.group_start = reinterpret_cast<decltype(a.group_start)>(dlsym(h, "ncclGroupStart"));
+        a.group_end = reinterpret_cast<decltype(a.group_end)>(dlsym(h, "ncclGroupEnd"));
+        a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
+        a.ok = a.comm_init_all && a.comm_destroy && a.reduce && a.group_start && a.group_end && a.error_string;
+        return a;
+    }();
+    return api;
 }
 
-// one communicator set per device list, made on first use and kept for the process
+// one communicator set per device list, made on first use and kept until pt_release_communicators
+// or process exit (an atexit handler registered after the HIP runtime started runs before the
+// runtime's own teardown)
 std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+
+int destroy_comms_locked() {
+    const RcclApi& a = rccl_api();
+    ncclResult_t bad = ncclSuccess;
+    for (auto& kv : g_comms)
+        for (ncclComm_t c : kv.second) {
+            const ncclResult_t r = a.comm_destroy(c);
+            if (r != ncclSuccess) bad = r;
+        }
+    g_comms.clear();
+    if (bad != ncclSuccess) return fail(PT_ERR_HIP, std::string("ncclCommDestroy: ") + a.error_string(bad));
+    return PT_OK;
+}
+
+void destroy_comms_at_exit() {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (!g_comms.empty()) destroy_comms_locked();
+}
 
 int rccl_reduce(pt_scene* const* sc, int n, size_t count) {
     std::lock_guard<std::mutex> lk(g_rccl_mu);
@@ -1076,6 +1216,8 @@ int rccl_reduce(pt_scene* const* sc, int n, size_t count) {
     for (int g = 0; g < n; ++g) devs[g] = sc[g]->device;
     auto it = g_comms.find(devs);
     if (it == g_comms.end()) {
+        static bool registered = false;
+        if (!registered) registered = std::atexit(destroy_comms_at_exit) == 0;
         std::vector<ncclComm_t> c(n);
         const ncclResult_t r = a.comm_init_all(c.data(), n, devs.data());
         if (r != ncclSuccess) return fail(PT_ERR_HIP, std::string("ncclCommInitAll: ") + a.error_string(r));
@@ -1139,11 +1281,10 @@ extern "C" int pt_render_multi(pt_scene* const* scenes, int n, const float meta[
     bool distinct = true;
     for (int g = 0; g < n; ++g)
         for (int h = 0; h < g; ++h) distinct &= scenes[g]->device != scenes[h]->device;
-    const char* red = std::getenv("PT_REDUCE");
-    const bool want_rccl = !(red && !std::strcmp(red, "ordered"));
-    if (red && std::strcmp(red, "ordered") && std::strcmp(red, "rccl")) return fail(PT_ERR_INVALID, "PT_REDUCE: rccl|ordered");
-    if (red && !std::strcmp(red, "rccl") && (!distinct || !rccl_api().ok))
-        return fail(PT_ERR_INVALID, "PT_REDUCE=rccl needs distinct devices and librccl.so.1");
+    const Opts o = opts_snapshot();
+    const bool want_rccl = !o.is("reduce", "ordered");
+    if (o.is("reduce", "rccl") && (!distinct || !rccl_api().ok))
+        return fail(PT_ERR_INVALID, "option reduce=rccl needs distinct devices and librccl.so.1");
     const bool use_rccl = want_rccl && distinct && rccl_api().ok;
     for (int g = 0; g < n; ++g) {  // accumulators: scenes[0]'s from accum, the others zero
         pt_scene* s = scenes[g];
@@ -1192,4 +1333,10 @@ extern "C" int pt_render_multi(pt_scene* const* scenes, int n, const float meta[
         *counters = sum;
     }
     return PT_OK;
+}
+
+extern "C" int pt_release_communicators(void) {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (g_comms.empty()) return PT_OK;
+    return destroy_comms_locked();
 }

@@ -52,7 +52,7 @@ constexpr int kMegaBlock = 256;
 // dynamic LDS a workgroup may use for traversal stacks + a staged scene copy
 constexpr size_t kLdsSceneBudget = 64 * 1024;
 
-// Kernel selection (PT_KERNEL / PT_LDS / PT_TRAV environment overrides for A/B runs).
+// Kernel selection (pt_set_option overrides for tests and A/B runs; pt_capi.hip launch_opts).
 struct LaunchOpts {
     bool wavefront = false;  // wavefront pipeline (pt_wavefront.hip)
     bool literal = false;  // k_mega: the reference's control flow
@@ -74,6 +74,11 @@ struct LaunchOpts {
     int regen = -1;        // fused kernel: streaming path regeneration (every extension launch refills): -1 default (off)
     long regen_target = 0; // paths in flight per part with regeneration (0 = the batch capacity)
     int sort = -1;         // traversal pipeline: survivors grouped per shade block by 8 / 64 / 512 coherence keys (0 off): -1 default (512)
+    int bf_slots = -1;     // brute-force kernels: hit slots per lane (< kBfSlots: tests of the recompute path): -1 default
+    int trace_blocks = 0;  // traversal / step kernels: cap on the grid (tests): 0 = occupancy-derived
+    int trace_dyn = 0;     // k_wf_trace takes its windows from group counters (1) or the static split (0)
+    uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
+    int packet = -1;       // traversal scenes: packet superset walk + replay (k_wf_trace_pk): -1 default
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -146,6 +151,12 @@ struct WfStreams {
     uint32_t* h_poll = nullptr;
     hipEvent_t poll_ev[kMaxParts][2] = {};
     int sort_bins = 0;     // LaunchOpts::sort: k_wf_shade groups a block's survivors by a coherence key of 8 / 64 / 512 values (0: off)
+    // per-call launch shape (LaunchOpts, filled by launch_wavefront)
+    int trace_blocks = 0;  // cap on the trace / step grid (0: occupancy-derived)
+    int trace_dyn = 0;     // k_wf_trace window hand-out from group counters
+    int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
+    uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
+    int packet = 0;        // traversal scenes: packet walk + replay (k_wf_trace_pk)
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

@@ -144,7 +144,7 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 // Work split: the queue is cut into windows of 32 entries; wave w of N takes windows w, w+N,
 // w+2N, ... (interleaving, not contiguous chunks, because queue order is spatially coherent —
 // camera rays in pixel order, survivors compacted block by block — so a contiguous chunk is an
-// image region whose cost differs systematically from the others).  dyn (PT_TRACE_DYN=1): chunks
+// image region whose cost differs systematically from the others).  dyn (option trace_dyn=1): chunks
 // of 8 windows are dealt to kTraceGroups groups of blocks round-robin and a group's waves take
 // them one window at a time from its counter, so a wave that drew cheap rays takes more windows
 // (one stream: +8 %; two: static 4 % faster).  Inside a wave, its
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
     constexpr uint32_t kNone = 0xffffffffu;
     // the counter's atomic for the window after next is issued one window ahead, so its latency
     // hides behind the current window instead of stalling the hand-out
-    // (dyn = 0, PT_TRACE_DYN=0: the static split — wave w takes windows w, w + nwaves, ... — for A/B)
+    // (dyn = 0, trace_dyn=0: the static split — wave w takes windows w, w + nwaves, ... — for A/B)
     uint32_t ticket = 0;  // lane 0: the group counter's value for the next fetch
     uint32_t nstatic = 0;
     auto issue = [&]() {
@@ -807,7 +807,7 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
 #endif
 }
 
-// Trace + shade in one launch per iteration (mailbox scenes; PT_PERSIST=0): queues are cut
+// Trace + shade in one launch per iteration (mailbox scenes; persist=0): queues are cut
 // into wb.nreg regions (64-path batches dealt round-robin: camera batch j to region j mod nreg);
 // the waves w ≡ r (mod nreg) serve region r of the input and append to region r of the output,
 // one atomicAdd per wave and batch on that region's counter (a counter shared by all waves
@@ -989,7 +989,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_persist_bf(SceneView sc, Fra
     if (COUNT) flush_counters(c, cnt_out);
 }
 
-// Megakernel with brute force + replay (mailbox scenes, PT_KERNEL=mega with PT_REGEN_BF=1): the
+// Megakernel with brute force + replay (mailbox scenes, kernel=mega with regen_bf=1): the
 // layout of k_regen — lane = pixel of an 8x8 tile, the pixel's frames in order, a lane whose
 // path ended starts its next frame at once, clamp(L) accumulated in registers — with every
 // query of the wave resolved by bf_closest.  Extension and shadow rays of different lanes share
@@ -1054,8 +1054,7 @@ hipError_t launch_regen_bf(const LaunchOpts& lo, const SceneView& sc_in, const F
     if (!count && sc.bfnode) sc.max_stack = 0;  // the stackless replay (bf_view)
     const bool lds = lo.lds && scene_fits_lds(sc);
     const bool fast = lo.fast_rcp != 0 && sc.fast_rcp;
-    int slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
-    if (const char* e = std::getenv("PT_BF_SLOTS")) slots = std::max(0, std::min(kBfSlots, std::atoi(e)));
+    const int slots = lo.bf_slots >= 0 ? std::min(kBfSlots, lo.bf_slots) : kBfSlots;  // < kBfSlots: tests of the recompute path
     dim3 grid((fp.width + 15) / 16, (fp.height + 15) / 16), block(kRegenBfBlock);
     const size_t shm = (size_t)sc.max_stack * kRegenBfBlock * 4 + (kRegenBfBlock / 64) * (kBfSlots * 64 * 4) +
                        (lds ? sc.span_bytes : 0);
@@ -1385,16 +1384,15 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     const uint32_t F = np * std::max<uint32_t>(1, std::min<uint32_t>((nframes + np - 1) / np, (uint32_t)(wb.capacity / np / npix)));
     const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc);
     int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
-    if (const char* e = std::getenv("PT_WF_TRACE_BLOCKS")) tblocks = std::max(1, std::min(tblocks, std::atoi(e)));  // tests
+    if (ws.trace_blocks > 0) tblocks = std::min(tblocks, ws.trace_blocks);  // option wf_trace_blocks (tests)
     const int iters = 2 * (fp.max_depth + 1);
-    uint32_t watchdog = kTraceWatchdog;  // PT_TRACE_WATCHDOG: tests of the failure report
-    // PT_TRACE_DYN=1: k_wf_trace takes its windows from group counters (opt-in: with two parts the
+    // option trace_watchdog: tests of the failure report
+    const uint32_t watchdog = ws.watchdog > 0 ? ws.watchdog : kTraceWatchdog;
+    // option trace_dyn=1: k_wf_trace takes its windows from group counters (opt-in: with two parts the
     // static split is 4 % faster on Glossy and the 100k synthetic scene, the counters 2 % on the boat)
-    int trace_dyn = 0;
-    if (const char* e = std::getenv("PT_TRACE_DYN")) trace_dyn = std::atoi(e) != 0 ? 1 : 0;
-    if (const char* e = std::getenv("PT_TRACE_WATCHDOG")) watchdog = (uint32_t)std::max(1L, std::atol(e));
-    int bf_slots = kBfSlots;  // PT_BF_SLOTS < kBfSlots: tests of the recompute path
-    if (const char* e = std::getenv("PT_BF_SLOTS")) bf_slots = std::max(0, std::min(kBfSlots, std::atoi(e)));
+    const int trace_dyn = ws.trace_dyn;
+    // option bf_slots < kBfSlots: tests of the recompute path
+    const int bf_slots = ws.bf_slots >= 0 ? std::min(kBfSlots, ws.bf_slots) : kBfSlots;
     if constexpr (TRAV >= 500) {  // one workgroup-local launch per batch (k_wf_persist_bf), one stream
         const uint32_t Fp = std::max<uint32_t>(1, std::min<uint32_t>(nframes, wb.capacity / npix));
         const uint32_t nblk = std::min<uint32_t>((uint32_t)tblocks, kPersistMaxBlocks);
@@ -1453,7 +1451,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                           dim3((std::max(pv[h].P, pv[h].w.nreg) + 255) / 256), dim3(256), 0, pv[h].st,
                           fp, pv[h].w, frame0, stride, pv[h].fbase, pv[h].P, !accum, cnt);
         }
-        // Optional staggering (PT_STAGGER=1, two parts; measured slower: 1026 vs 1231 Msamples/s):
+        // Optional staggering (option stagger=1, two parts; measured slower: 1026 vs 1231 Msamples/s):
         // part 1's trace i waits for part 0's trace i and part 0's trace i+1 for part 1's trace i,
         // so the persistent trace kernels never share the machine.  Default: parts overlap freely.
         const bool stagger = nh == 2 && ws.stagger;
@@ -1516,13 +1514,17 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.nparts = std::max(1, std::min(kMaxParts, lo.parts > 0 ? lo.parts : 2));
     ws.stagger = lo.stagger > 0;
     ws.fuse_gen = lo.fuse_gen != 0;
-    ws.regen = lo.regen > 0 && ws.h_poll != nullptr;  // PT_REGEN=1 (measured slower so far)
+    ws.regen = lo.regen > 0 && ws.h_poll != nullptr;  // option regen=1 (measured slower so far)
     ws.regen_target = lo.regen_target > 0 ? (uint32_t)std::min<long>(lo.regen_target, 0x7fffffffL) : 0u;
     // survivors grouped per shade block by direction octant and origin cell (PT_SORT; default 512
     // keys = 8 octants x 4^3 cells: CornellBox-Glossy +4.7 % with 64 keys, +1.2 % more with 512,
     // MedievalBoat unchanged, in-process A/B)
     const int sort = lo.sort >= 0 ? lo.sort : 512;
     ws.sort_bins = sort > 0 ? (sort >= 512 ? 512 : sort >= 64 ? 64 : 8) : 0;
+    ws.trace_blocks = lo.trace_blocks;
+    ws.trace_dyn = lo.trace_dyn;
+    ws.bf_slots = lo.bf_slots;
+    ws.watchdog = lo.watchdog;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     // turn policy of the lean16 traversal: 4 since the queues are grouped by coherence keys (in
@@ -1540,9 +1542,9 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     // or if-if steps were asked for (those have no mailboxed form)
     const bool mb = lo.mailbox != 0 && sc.mailbox && base >= 5 && base <= 8 && !pipe && !ifif;
     // brute force + replay (k_wf_trace_bf) by default for mailbox scenes; an explicit PT_TRAV
-    // or PT_BF=0 keeps the traversal kernels
+    // or bf=0 keeps the traversal kernels
     const bool bf = lo.bf != 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0;
-    // k_wf_persist_bf (PT_PERSIST=1) measured slower: 1771 vs 2207 Msamples/s (its workgroups idle
+    // k_wf_persist_bf (option persist=1) measured slower: 1771 vs 2207 Msamples/s (its workgroups idle
     // at the per-iteration barrier once a region's queue is down to a few batches)
     // big-leaf cooperation (+160) for lean<4..16> on scenes with leaves of >= big_leaf entries
     const bool big = !bf && !mb && sc.big_leaf > 0 && base >= 5 && base <= 7 && !pipe && !ifif;

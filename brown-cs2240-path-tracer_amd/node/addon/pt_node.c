@@ -114,6 +114,37 @@ static napi_value js_abi_version(napi_env env, napi_callback_info info) {
     return r;
 }
 
+/* setOption(name, value | null) — pt_set_option (kernel-selection switches; null = default) */
+static napi_value js_set_option(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    char name[64], value[64];
+    size_t n = 0;
+    if (argc < 1 || napi_get_value_string_utf8(env, argv[0], name, sizeof name, &n) != napi_ok) {
+        napi_throw_type_error(env, NULL, "setOption(name: string, value: string | number | null)");
+        return NULL;
+    }
+    const char* v = NULL;
+    napi_valuetype t = napi_undefined;
+    if (argc >= 2) CHECK_NAPI(env, napi_typeof(env, argv[1], &t));
+    if (t == napi_string) {
+        if (napi_get_value_string_utf8(env, argv[1], value, sizeof value, &n) != napi_ok) return NULL;
+        v = value;
+    } else if (t == napi_number) {
+        int64_t x = 0;
+        CHECK_NAPI(env, napi_get_value_int64(env, argv[1], &x));
+        snprintf(value, sizeof value, "%lld", (long long)x);
+        v = value;
+    } else if (t != napi_null && t != napi_undefined) {
+        napi_throw_type_error(env, NULL, "setOption: value must be a string, a number or null");
+        return NULL;
+    }
+    int rc = pt_set_option(name, v);
+    if (rc) return throw_pt(env, rc);
+    return NULL;
+}
+
 /* deviceCount() -> number */
 static napi_value js_device_count(napi_env env, napi_callback_info info) {
     (void)info;
@@ -600,6 +631,7 @@ static napi_value init(napi_env env, napi_value exports) {
     napi_property_descriptor props[] = {
         {"abiVersion", NULL, js_abi_version, NULL, NULL, NULL, napi_enumerable, NULL},
         {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
+        {"setOption", NULL, js_set_option, NULL, NULL, NULL, napi_enumerable, NULL},
         {"sceneCreate", NULL, js_scene_create, NULL, NULL, NULL, napi_enumerable, NULL},
         {"sceneInfo", NULL, js_scene_info, NULL, NULL, NULL, napi_enumerable, NULL},
         {"sceneDestroy", NULL, js_scene_destroy, NULL, NULL, NULL, napi_enumerable, NULL},

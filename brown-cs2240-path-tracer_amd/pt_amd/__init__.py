@@ -20,14 +20,21 @@ from ._lib import (  # noqa: F401
     Scene,
     SceneInfo,
     abi_version,
+    build_id,
     bvh_build,
     device_count,
+    get_option,
     lib_path,
     load_library,
+    options,
+    release_communicators,
     render_multi,
+    reset_options,
     selftest_math,
     selftest_rcp,
     set_hw_queues,
+    set_option,
+    source_hash,
     tonemap,
 )
 from .host import PackedScene, load_scene, program_entry  # noqa: F401

@@ -9,7 +9,11 @@ import numpy as np
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _LIB_FILE = os.path.join(_PKG_ROOT, "lib", "libpt_hip.so")
 
-ABI_VERSION = 2  # include/pt_hip.h PT_ABI_VERSION
+ABI_VERSION = 3  # include/pt_hip.h PT_ABI_VERSION
+_CSRC = os.path.join(_PKG_ROOT, "csrc")
+# csrc/Makefile BUILD_SRCS: the sources whose SHA-256 the library carries as pt_build_id()
+_BUILD_SRCS = ["pt_kernels.hip", "pt_wavefront.hip", "pt_image.hip", "pt_capi.hip", "pt_math.h", "pt_layout.h",
+               "pt_device.h", "pt_path.h", "pt_kernels.h", "../../include/pt_hip.h", "pt_bvh.cpp", "Makefile"]
 MODE_AUTO, MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1, 2
 MATH_FNS = ["sin", "cos", "tan", "acos", "log2", "exp2", "pow", "sqrt", "div", "hash1u", "hash1", "hash2x",
             "hash2y", "min", "max"]
@@ -67,8 +71,20 @@ def _bind_torch_hip_runtime():
         pass
 
 
+def source_hash() -> str:
+    """SHA-256 of the library's sources as csrc/Makefile computes it (names sorted, contents
+    concatenated); pt_build_id() of a library built from this tree returns the same digest."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in sorted(_BUILD_SRCS):
+        with open(os.path.join(_CSRC, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def load_library():
-    """Load libpt_hip.so; raise if it was not built (no silent fallback)."""
+    """Load libpt_hip.so; raise if it was not built, or was built from other sources than the
+    tree it sits in (no silent fallback, no stale binary)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -78,6 +94,11 @@ def load_library():
     L = ctypes.CDLL(_LIB_FILE)
     if L.pt_abi_version() != ABI_VERSION:
         raise PtError(-1, f"{_LIB_FILE} has ABI {L.pt_abi_version()}, this binding expects {ABI_VERSION} (rebuild)")
+    L.pt_build_id.restype = ctypes.c_char_p
+    built, here = L.pt_build_id().decode(), source_hash()
+    if built != here:
+        raise PtError(-1, f"{_LIB_FILE} was built from other sources (build id {built[:16]}, tree {here[:16]}): "
+                          f"run __graft_entry__.build()")
     p, i, u32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_size_t
     L.pt_abi_version.restype = i
     L.pt_last_error.restype = ctypes.c_char_p
@@ -104,7 +125,11 @@ def load_library():
     L.pt_scene_check.argtypes = [p]
     L.pt_render_multi.argtypes = [ctypes.POINTER(p), i, p, u32, u32, u32, i, i, p, p]
     L.pt_set_hw_queues.argtypes = [i]
-    for fn in ("pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+    L.pt_set_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    L.pt_get_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
+    L.pt_reset_options.argtypes = []
+    L.pt_reset_options.restype = None
+    for fn in ("pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
                "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
@@ -119,6 +144,56 @@ def _check(rc: int):
 
 def abi_version() -> int:
     return int(load_library().pt_abi_version())
+
+
+def build_id() -> str:
+    return load_library().pt_build_id().decode()
+
+
+def _opt_name(name: str) -> str:
+    """Option keys: the C names ("kernel", "trav", ...); the old environment spellings
+    ("PT_KERNEL") are accepted and mapped."""
+    return name[3:].lower() if name.startswith("PT_") else name
+
+
+def set_option(name: str, value) -> None:
+    """pt_set_option: process-wide kernel-selection switch (value None = default)."""
+    v = None if value is None else str(value).encode()
+    _check(load_library().pt_set_option(_opt_name(name).encode(), v))
+
+
+def get_option(name: str) -> str:
+    buf = ctypes.create_string_buffer(64)
+    _check(load_library().pt_get_option(_opt_name(name).encode(), buf, 64))
+    return buf.value.decode()
+
+
+def reset_options() -> None:
+    load_library().pt_reset_options()
+
+
+class options:
+    """Context manager: `with pt_amd.options(kernel="wavefront", trav="lean16"): ...` sets the
+    options for the block and restores the previous values after it."""
+
+    def __init__(self, mapping=None, **kv):
+        self.kv = {_opt_name(k): v for k, v in {**(mapping or {}), **kv}.items()}
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.saved[k] = get_option(k)
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *a):
+        for k, v in self.saved.items():
+            set_option(k, v or None)
+
+
+def release_communicators() -> None:
+    """pt_release_communicators: destroy the RCCL communicators pt_render_multi cached."""
+    _check(load_library().pt_release_communicators())
 
 
 def set_hw_queues(n: int = 8):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2
+#define PT_ABI_VERSION 3
 
 typedef enum {
     PT_OK = 0,
@@ -141,6 +141,31 @@ int pt_scene_check(pt_scene* scene);
  * wavefront's two part streams (e.g. torch) want 8 so the parts do not share a queue. */
 int pt_set_hw_queues(int n);
 
+/* Options (process-wide; the library reads no environment variable).  Every value renders the
+ * same bits — the parity suite checks each — so they choose kernels and batch shapes only; the
+ * defaults are the measured best.  value NULL = back to the default; unknown names and malformed
+ * values fail with PT_ERR_INVALID.  Render calls read the options when they start.
+ *   "kernel"        auto | mega | wavefront | literal    pipeline (auto = PT_MODE_* and the scene)
+ *   "trav"          nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32   traversal flavour
+ *   "lds" "fastrcp" "pipe" "ifif" "dual" "stagger" "fuse" "fuse_gen" "bf" "mailbox" "persist"
+ *   "regen" "regen_bf" "bf_stackless" "trace_dyn" "packet"                  0 | 1 switches
+ *   "parts" "cull" "sort" "node_bias" "big_leaf" "bf_slots" "wf_paths" "wf_trace_blocks"
+ *   "regen_target" "trace_watchdog"                                         integers
+ *   "mb_uid_order"  forward | reverse   (read by pt_scene_create: uid numbering of mailbox scenes)
+ *   "reduce"        rccl | ordered      (pt_render_multi's reduction)
+ * DESIGN.md §6 describes each.  pt_get_option writes the current value ("" = default) into buf. */
+int pt_set_option(const char* name, const char* value);
+int pt_get_option(const char* name, char* buf, size_t cap);
+void pt_reset_options(void);
+
+/* Destroys the RCCL communicators pt_render_multi made (they are cached per device list; the
+ * library also destroys them when the process exits).  Not concurrent with pt_render_multi. */
+int pt_release_communicators(void);
+
+/* Identity of the build: the SHA-256 of the sources it was compiled from (csrc/Makefile), so a
+ * host can refuse a library that was not built from the tree it runs in. */
+const char* pt_build_id(void);
+
 /* Multi-GPU render of one image (the `n_gpus` of §8(b)): scenes[g] is the same
  * packed scene uploaded to device g (pt_scene_create per device, any devices, repeats allowed).
  * Frames k = frame0 + i*frame_stride (i < nframes) are dealt round-robin: scene g renders the i
@@ -148,7 +173,7 @@ int pt_set_hw_queues(int n);
  * an f32 accumulator on its own device (scenes[0]'s starts from accum, the others from zero), on
  * one host thread per device; the partial accumulators are then summed onto scenes[0]'s device
  * and copied to accum (host f32 [H][W][3], in/out).
- * Reduction (environment PT_REDUCE): "rccl" (default when the devices are distinct and
+ * Reduction (option "reduce"): "rccl" (default when the devices are distinct and
  * librccl.so.1 loads) = ONE ncclReduce(sum, f32) to device 0 over a communicator made once per
  * device list (ncclCommInitAll, single process) — the summation order is RCCL's; "ordered" (and
  * always with repeated devices) = peer copies added on device 0 in device order,

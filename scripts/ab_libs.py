@@ -5,8 +5,9 @@ through the C ABI only.
 
 usage: ab_libs.py LIB[@ENV=VAL,ENV=VAL] ... [--scene CornellBox] [--res 1024] [--spp 64] [--depth 8]
                  [--rounds 5] [--mode 0]
-The optional @ENV list is set around that variant's renders (the library reads its PT_* A/B
-switches on every call), so one build can be compared with itself under different switches.
+The optional @OPT list is set around that variant's renders through the library's own
+pt_set_option (keys "kernel" or "PT_KERNEL"; builds older than the option API read PT_* environment
+variables instead), so one build can be compared with itself under different switches.
 """
 import argparse
 import ctypes
@@ -47,8 +48,18 @@ def main():
     runs = []
     loaded = {}
 
-    def with_env(env, fn):
-        old = {k: os.environ.get(k) for k in env}
+    def with_env(L, env, fn):
+        if hasattr(L, "pt_set_option"):  # the option API
+            name = lambda k: (k[3:].lower() if k.startswith("PT_") else k).encode()  # noqa: E731
+            L.pt_set_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+            for k, v in env.items():
+                assert L.pt_set_option(name(k), v.encode()) == 0, L.pt_last_error()
+            try:
+                return fn()
+            finally:
+                for k in env:
+                    L.pt_set_option(name(k), None)
+        old = {k: os.environ.get(k) for k in env}  # older builds: PT_* environment variables
         os.environ.update(env)
         try:
             return fn()
@@ -75,7 +86,7 @@ def main():
         h = ctypes.c_void_p()
         assert L.pt_scene_create(p(tri), tri.size, p(bvh), bvh.size, 0, ctypes.byref(h)) == 0, L.pt_last_error()
         acc = np.zeros((a.res, a.res, 3), np.float32)
-        rc = with_env(env, lambda: L.pt_render(h, p(meta), 0, a.spp, 1, a.depth, a.mode, p(acc), None))  # warm-up
+        rc = with_env(L, env, lambda: L.pt_render(h, p(meta), 0, a.spp, 1, a.depth, a.mode, p(acc), None))  # warm-up
         assert rc == 0, L.pt_last_error()
         runs.append({"lib": spec, "L": L, "h": h, "acc": acc, "ms": [], "ref": acc.copy(), "env": env})
     if a.async_torch:
@@ -90,14 +101,14 @@ def main():
                     r["dacc"].zero_()
                 st.synchronize()
                 t = time.perf_counter()
-                rc = with_env(r["env"], lambda: r["L"].pt_render_async(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode,
+                rc = with_env(r["L"], r["env"], lambda: r["L"].pt_render_async(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode,
                                                                       ctypes.c_void_p(r["dacc"].data_ptr()), None,
                                                                       ctypes.c_void_p(st.cuda_stream)))
                 st.synchronize()
             else:
                 r["acc"][:] = 0
                 t = time.perf_counter()
-                rc = with_env(r["env"], lambda: r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode,
+                rc = with_env(r["L"], r["env"], lambda: r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode,
                                                                  p(r["acc"]), None))
             assert rc == 0
             r["ms"].append((time.perf_counter() - t) * 1e3)

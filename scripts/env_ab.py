@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""In-process A/B of render settings read from the environment on every call (PT_* switches of
-csrc/pt_capi.hip launch_opts).  Each variant renders the same workload; results must be
+"""In-process A/B of render options (pt_set_option switches read by every render call, csrc/pt_capi.hip
+launch_opts; keys as "kernel" or the old spelling "PT_KERNEL").  Each variant renders the same workload; results must be
 bit-identical to the first variant's; times are medians of --reps renders, variants interleaved.
 usage: env_ab.py [--scene S --width W --height H --spp N --depth D --reps R] 'A=1,B=2' 'A=0' ..."""
 import argparse
@@ -40,15 +40,14 @@ def main():
     st = torch.cuda.Stream()
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
     variants = [dict(kv.split("=", 1) for kv in v.split(",") if kv) for v in a.variants]
-    keys = sorted({k for v in variants for k in v})
     times = {i: [] for i in range(len(variants))}
     ref = None
     for rep in range(a.reps + 1):
         order = list(range(len(variants))) if rep % 2 == 0 else list(reversed(range(len(variants))))
         for i in order:
-            for k in keys:
-                os.environ.pop(k, None)
-            os.environ.update(variants[i])
+            pt_amd.reset_options()
+            for k, v in variants[i].items():
+                pt_amd.set_option(k, v)
             with torch.cuda.stream(st):
                 acc.zero_()
                 st.synchronize()
@@ -69,9 +68,9 @@ def main():
         ms = float(np.median(times[i])) * 1e3
         rec = {"variant": v, "scene": a.scene, "ms": round(ms, 3), "msamples_s": round(W * H * a.spp / ms / 1e3, 1)}
         if a.profile:
-            for k in keys:
-                os.environ.pop(k, None)
-            os.environ.update(variants[i])
+            pt_amd.reset_options()
+            for k, v in variants[i].items():
+                pt_amd.set_option(k, v)
             scene.profile_enable(True)
             with torch.cuda.stream(st):
                 acc.zero_()

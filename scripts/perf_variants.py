@@ -107,9 +107,10 @@ VARIANTS = {
 
 
 def set_variant(v):
-    for k in ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_NODE_BIAS", "PT_WF_TRACE_BLOCKS", "PT_PIPE", "PT_IFIF", "PT_DUAL", "PT_MAILBOX", "PT_BF", "PT_BF_SLOTS", "PT_WF_PATHS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF", "PT_CULL", "PT_FUSE_GEN"):
-        os.environ.pop(k, None)
-    os.environ.update(VARIANTS[v])
+    import pt_amd
+    pt_amd.reset_options()  # the library's options (pt_set_option), not the environment
+    for k, val in VARIANTS[v].items():
+        pt_amd.set_option(k, val)
 
 
 def main():

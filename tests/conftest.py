@@ -44,6 +44,28 @@ class Packed:
         return m
 
 
+class PtOptions:
+    """pt_set_option switches for one test (the library reads no environment variable).  Keys may
+    use the old environment spelling ("PT_KERNEL") or the option name ("kernel")."""
+
+    def set(self, name, value):
+        import pt_amd
+        pt_amd.set_option(name, value)
+
+    def unset(self, name, raising=False):
+        import pt_amd
+        pt_amd.set_option(name, None)
+
+
+@pytest.fixture
+def ptopts():
+    """Every option at its default before and after the test."""
+    import pt_amd
+    pt_amd.reset_options()
+    yield PtOptions()
+    pt_amd.reset_options()
+
+
 def pack_with_node(src: str, out_dir: str, *extra) -> Packed:
     """Run the product's Node scene pipeline (node/bin/pt-pack.js)."""
     subprocess.run(["node", PACK_JS, src, out_dir, *extra], check=True, capture_output=True)

@@ -46,7 +46,47 @@ def test_kernels_built_for_gfx950():
 
 
 def test_abi_version():
-    assert pt_amd.abi_version() == 2 == pt_amd.ABI_VERSION
+    assert pt_amd.abi_version() == 3 == pt_amd.ABI_VERSION
+
+
+def test_build_id_is_this_trees_source_hash():
+    """The library carries the SHA-256 of its sources (csrc/Makefile); pt_amd refuses another."""
+    assert re.fullmatch(r"[0-9a-f]{64}", pt_amd.build_id())
+    assert pt_amd.build_id() == pt_amd.source_hash()
+
+
+def test_no_environment_switches_in_the_library():
+    """Kernel selection is explicit (pt_set_option): the library reads no environment variable."""
+    csrc = os.path.join(ROOT, "brown-cs2240-path-tracer_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h", ".cpp")):
+            assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+    out = subprocess.run(["nm", "-D", "--undefined-only", pt_amd.lib_path()], capture_output=True, text=True).stdout
+    assert not re.search(r"\bgetenv\b", out)
+
+
+def test_options_set_get_reset_and_validate():
+    pt_amd.reset_options()
+    try:
+        assert pt_amd.get_option("kernel") == ""
+        pt_amd.set_option("kernel", "wavefront")
+        pt_amd.set_option("PT_TRAV", "lean8")  # the old environment spelling maps to the option
+        pt_amd.set_option("parts", 3)
+        assert (pt_amd.get_option("kernel"), pt_amd.get_option("trav"), pt_amd.get_option("parts")) == \
+            ("wavefront", "lean8", "3")
+        with pt_amd.options(kernel="mega", sort=64):
+            assert pt_amd.get_option("kernel") == "mega" and pt_amd.get_option("sort") == "64"
+        assert pt_amd.get_option("kernel") == "wavefront" and pt_amd.get_option("sort") == ""
+        pt_amd.set_option("kernel", None)
+        assert pt_amd.get_option("kernel") == ""
+        for name, value in (("nosuch", "1"), ("kernel", "fast"), ("parts", "x"), ("lds", "2"), ("parts", "-1"),
+                            ("trav", ""), ("reduce", "nccl")):
+            with pytest.raises(pt_amd.PtError) as e:
+                pt_amd.set_option(name, value)
+            assert e.value.code == -1
+    finally:
+        pt_amd.reset_options()
+    assert pt_amd.get_option("trav") == "" and pt_amd.get_option("parts") == ""
 
 
 def test_kernel_time_struct_matches_header():

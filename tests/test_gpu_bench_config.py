@@ -28,15 +28,15 @@ pytestmark = pytest.mark.gpu
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS",
             "PT_REGEN_BF", "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
-            "PT_BIG_LEAF", "PT_BIG_RATIO", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN")
+            "PT_BIG_LEAF", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN")
 ORACLE_THREADS = 16  # the GPU box's CPU share
 
 
 @pytest.fixture
-def clean_env(monkeypatch):
+def clean_env(ptopts):
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
-    return monkeypatch
+        ptopts.unset(k, raising=False)
+    return ptopts
 
 
 def bits(a):
@@ -92,9 +92,9 @@ def test_multi_batch_ragged_parts_vs_oracle(packed, clean_env, parts):
     ragged last batch with fewer frames than parts, accumulation across batches."""
     p = packed["CornellBox"]
     meta = p.meta_for(64, 64)
-    clean_env.setenv("PT_KERNEL", "wavefront")
-    clean_env.setenv("PT_WF_PATHS", "12288")  # 3 frames per batch: 7 frames = 3 + 3 + 1
-    clean_env.setenv("PT_PARTS", parts)
+    clean_env.set("PT_KERNEL", "wavefront")
+    clean_env.set("PT_WF_PATHS", "12288")  # 3 frames per batch: 7 frames = 3 + 3 + 1
+    clean_env.set("PT_PARTS", parts)
     init = np.random.default_rng(7).uniform(0, 1, (64, 64, 3)).astype(np.float32)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         gpu = s.render(meta, 2, 7, 3, 8, pt_amd.MODE_AUTO, accum=init.copy())

@@ -1,0 +1,103 @@
+"""Oracle parity at the real sizes of BASELINE.json configs[2..4], and the negative control that
+pins which BVH the reference builds.
+
+* Row bands, bit for bit: the product renders the WHOLE image at the config's size through
+  AUTO (so the large-grid paths run: two-part batches on their own streams, several batches per
+  call with a ragged last one, coherence-sorted traversal queues, cooperative big-leaf turns on
+  the boat's 7,327-entry leaf), and bands of rows of that accumulator are compared with the C
+  oracle (oracle/pt_oracle.c) rendering the same rows (po_render's y0/y1):
+    - CornellBox-Mirror and CornellBox-Glossy 1024^2, depth 16 (the reference default), 16 frames
+      (configs[2]; 16 M paths = two 8 M-path batches of two parts each);
+    - MedievalBoat 1920x1080, depth 16, 5 frames (configs[3]; a 4-frame batch of two parts and a
+      ragged 1-frame batch), a band through the hull and one through the lit deck;
+    - CornellBox 4096^2, depth 8, 4 frames (configs[4]'s image on one GPU; a frame is 16.8 M
+      paths, so the batch holds two frames as two parts).
+* Negative control for the tree: js-geometry's `Bounds` strides are read as fixed
+  at construction (`bvh.ts:46-52` with the child boxes cloned from the parent at `:72-73,
+  113-114`).  The other reading — live strides — builds a different tree, and with it the
+  exit-distance pruning quirk drops different geometry.  The product's tree must pass the
+  noise-calibrated L2 test against the reference's own renders (test_gpu_bench_config.py) AND
+  the live-stride tree, rendered by the same kernels, must FAIL it on 4x4 blocks for the two
+  scenes where the readings differ visibly (full_lighting, mirror).  If a later change lost the
+  test's power to tell the trees apart, this test fails.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import pt_amd
+import scene_oracle as so
+from conftest import SCENES
+from test_gpu_bench_config import K_SETS, L2_TOL, ORACLE_THREADS, assert_same_bits, block4, rms
+
+pytestmark = pytest.mark.gpu
+
+
+def _render_bands(p, W, H, frames, depth, bands):
+    meta = p.meta_for(W, H)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        gpu = s.render(meta, 0, frames, 1, depth, pt_amd.MODE_AUTO)
+        prof = s.profile_read()
+        s.profile_enable(False)
+    for y0, y1 in bands:
+        ref, _ = oracle.render(p.triangle_data, p.bvh_data, meta, 0, frames, 1, depth, y0=y0, y1=y1,
+                               nthreads=ORACLE_THREADS)
+        assert_same_bits(gpu[y0:y1], ref, f"{W}x{H} rows {y0}..{y1}")
+        assert float(ref.mean()) > 0.0, (y0, y1)  # the band sees light
+    return gpu, prof
+
+
+@pytest.mark.parametrize("scene", ["CornellBox-Mirror", "CornellBox-Glossy"])
+def test_config3_1024_depth16_rows_bitexact(packed, scene):
+    # upper walls (Glossy's camera sees no ceiling above row ~220), the centre (mirror box / glossy
+    # spheres), the floor
+    _, prof = _render_bands(packed[scene], 1024, 1024, 16, 16, [(260, 276), (500, 516), (900, 916)])
+    want = "k_wf_step" if scene == "CornellBox-Mirror" else "k_wf_trace"  # mailbox scene / traversal scene
+    assert want in prof, prof
+
+
+def test_config4_boat_1080p_depth16_rows_bitexact(packed):
+    _, prof = _render_bands(packed["MedievalBoat"], 1920, 1080, 5, 16, [(680, 696), (560, 568)])
+    assert "k_wf_trace" in prof and prof["k_wf_accum"]["launches"] == 2, prof  # two batches
+
+
+def test_config5_image_4096_depth8_rows_bitexact(packed):
+    _, prof = _render_bands(packed["CornellBox"], 4096, 4096, 4, 8, [(400, 416), (2040, 2056), (3700, 3708)])
+    assert "k_wf_step" in prof, prof
+
+
+def _l2_ratios(tri, bvh, meta, spp, ref):
+    with pt_amd.Scene(tri, bvh) as s:
+        ours = [s.render_image(meta, k * 1000, spp, 1, 16) for k in range(K_SETS)]
+    pairs = [(a, b) for a in range(K_SETS) for b in range(a + 1, K_SETS)]
+    out = {}
+    for label, f in (("pixel", lambda x: x), ("block4", block4)):
+        self_d = max(rms(f(ours[a]), f(ours[b])) for a, b in pairs)
+        ref_d = max(rms(f(o), f(ref)) for o in ours)
+        out[label] = ref_d / self_d
+    return out
+
+
+@pytest.mark.parametrize("name,xml", [("cornell_box_full_lighting", "CornellBox"), ("mirror", "CornellBox-Mirror")])
+def test_live_stride_tree_fails_the_reference_l2_test(name, xml):
+    from PIL import Image
+    ini = os.path.join(SCENES, "scene_files", "final", name + ".ini")
+    product = pt_amd.load_scene(ini, web_root=SCENES)
+    spp = int(product.settings["samplesPerPixel"])
+    ref = np.array(Image.open(os.path.join(SCENES, "student_outputs", "final", name + ".png")))
+    assets = os.path.join(SCENES, "scene_assets")
+    _, live = so.load_scene(os.path.join(assets, xml + ".xml"), assets, live_strides=True)
+    _, ctor = so.load_scene(os.path.join(assets, xml + ".xml"), assets)
+    # the triangle buffer does not depend on the tree; the trees differ
+    assert np.array_equal(live.triangle_data.view(np.uint32), product.triangle_data.view(np.uint32))
+    assert np.array_equal(ctor.bvh_data.view(np.uint32), product.bvh_data.view(np.uint32))
+    assert not np.array_equal(live.bvh_data, product.bvh_data)
+    good = _l2_ratios(product.triangle_data, product.bvh_data, product.meta, spp, ref)
+    bad = _l2_ratios(live.triangle_data, live.bvh_data, product.meta, spp, ref)
+    print(f"{name}: product tree pixel {good['pixel']:.4f} block4 {good['block4']:.4f}; "
+          f"live-stride tree pixel {bad['pixel']:.4f} block4 {bad['block4']:.4f}")
+    assert good["pixel"] <= L2_TOL and good["block4"] <= L2_TOL, good
+    assert bad["block4"] > L2_TOL, bad

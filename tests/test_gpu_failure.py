@@ -17,11 +17,11 @@ KEYS = ("PT_KERNEL", "PT_TRAV", "PT_TRACE_WATCHDOG", "PT_WF_PATHS", "PT_PARTS", 
 
 
 @pytest.fixture
-def env(monkeypatch):
+def env(ptopts):
     for k in KEYS:
-        monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv("PT_KERNEL", "wavefront")
-    return monkeypatch
+        ptopts.unset(k, raising=False)
+    ptopts.set("PT_KERNEL", "wavefront")
+    return ptopts
 
 
 def _torch():
@@ -34,13 +34,13 @@ def test_async_watchdog_reported_by_scene_check(packed, env):
     meta = p.meta_for(64, 64)
     acc = torch.zeros((64, 64, 3), dtype=torch.float32, device="cuda")
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        env.setenv("PT_TRACE_WATCHDOG", "4")
+        env.set("PT_TRACE_WATCHDOG", "4")
         s.render_async(meta, 0, 2, 1, 8, pt_amd.MODE_WAVEFRONT, acc.data_ptr(), 0)  # returns without a report
         with pytest.raises(pt_amd.PtError) as e:
             s.check()
         assert "gave up" in str(e.value) and e.value.code == -4
         s.check()  # reported once, then cleared
-        env.delenv("PT_TRACE_WATCHDOG")
+        env.unset("PT_TRACE_WATCHDOG")
         good = s.render(meta, 0, 2, 1, 8, pt_amd.MODE_WAVEFRONT)
     ref, _ = oracle.render(p.triangle_data, p.bvh_data, meta, 0, 2, 1, 8)
     assert np.array_equal(good.view(np.uint32), ref.view(np.uint32))
@@ -52,10 +52,10 @@ def test_async_watchdog_reported_by_next_call(packed, env):
     meta = p.meta_for(64, 64)
     acc = torch.zeros((64, 64, 3), dtype=torch.float32, device="cuda")
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        env.setenv("PT_TRACE_WATCHDOG", "4")
+        env.set("PT_TRACE_WATCHDOG", "4")
         s.render_async(meta, 0, 2, 1, 8, pt_amd.MODE_WAVEFRONT, acc.data_ptr(), 0)
         torch.cuda.synchronize()
-        env.delenv("PT_TRACE_WATCHDOG")
+        env.unset("PT_TRACE_WATCHDOG")
         with pytest.raises(pt_amd.PtError) as e:  # the completed render's flag surfaces here
             s.render_async(meta, 0, 2, 1, 8, pt_amd.MODE_WAVEFRONT, acc.data_ptr(), 0)
         assert "gave up" in str(e.value)
@@ -70,8 +70,8 @@ def test_blocking_render_reports_watchdog(packed, env):
     p = packed["CornellBox-Glossy"]
     meta = p.meta_for(48, 48)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        env.setenv("PT_TRACE_WATCHDOG", "4")
+        env.set("PT_TRACE_WATCHDOG", "4")
         with pytest.raises(pt_amd.PtError):
             s.render(meta, 0, 1, 1, 8, pt_amd.MODE_WAVEFRONT)
-        env.delenv("PT_TRACE_WATCHDOG")
+        env.unset("PT_TRACE_WATCHDOG")
         s.render(meta, 0, 1, 1, 8, pt_amd.MODE_WAVEFRONT)  # cleared: renders again

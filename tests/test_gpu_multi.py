@@ -17,10 +17,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def env(monkeypatch):
+def env(ptopts):
     for k in ("PT_KERNEL", "PT_REDUCE", "PT_PARTS", "PT_WF_PATHS", "PT_REGEN"):
-        monkeypatch.delenv(k, raising=False)
-    return monkeypatch
+        ptopts.unset(k, raising=False)
+    return ptopts
 
 
 def bits(a):
@@ -73,7 +73,7 @@ def test_repeated_device_ordered_reduction_vs_oracle(packed, env, n, mode):
 
 def test_rccl_mode_rejects_repeated_devices(packed, env):
     p = packed["CornellBox"]
-    env.setenv("PT_REDUCE", "rccl")
+    env.set("PT_REDUCE", "rccl")
     scenes = [pt_amd.Scene(p.triangle_data, p.bvh_data, device=0) for _ in range(2)]
     try:
         with pytest.raises(pt_amd.PtError):
@@ -81,3 +81,38 @@ def test_rccl_mode_rejects_repeated_devices(packed, env):
     finally:
         for s in scenes:
             s.close()
+
+
+@pytest.mark.parametrize("ndev", [2, 8])
+def test_rccl_reduce_distinct_devices_vs_oracle(packed, env, ndev):
+    """The RCCL branch of pt_render_multi (ncclCommInitAll + ONE ncclReduce): the same partials as
+    the ordered reduction in another summation order, so within f32 rounding of the oracle's
+    ordered sum; the counters are exact.  Communicators are released afterwards."""
+    if pt_amd.device_count() < ndev:
+        pytest.skip(f"the RCCL reduction over {ndev} distinct GPUs needs {ndev} visible (the driver's 8-GPU node)")
+    n = ndev
+    p = packed["CornellBox"]
+    W = H = 64
+    meta = p.meta_for(W, H)
+    frame0, nframes, stride, depth = 1, 13, 1, 8
+    env.set("PT_REDUCE", "rccl")
+    scenes = [pt_amd.Scene(p.triangle_data, p.bvh_data, device=g) for g in range(n)]
+    try:
+        got, cnt = pt_amd.render_multi(scenes, meta, frame0, nframes, stride, depth, accum=np.zeros((H, W, 3), np.float32),
+                                       counters=True)
+    finally:
+        for s in scenes:
+            s.close()
+        pt_amd.release_communicators()
+    parts, total = [], {}
+    for g in range(n):
+        acc, c = oracle.render(p.triangle_data, p.bvh_data, meta, frame0 + g * stride, len(range(g, nframes, n)),
+                               n * stride, depth)
+        parts.append(acc)
+        for k, v in c.items():
+            total[k] = total.get(k, 0) + v
+    want = parts[0].copy()
+    for g in range(1, n):
+        want += parts[g]
+    assert np.allclose(got, want, rtol=1e-6, atol=1e-6)
+    assert cnt == total

@@ -103,16 +103,16 @@ KERNELS = {
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
             "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
-            "PT_BIG_LEAF", "PT_BIG_RATIO", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN")
+            "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN")
 
 
 @pytest.fixture(params=list(KERNELS))
-def kernel(request, monkeypatch):
+def kernel(request, ptopts):
     """Every kernel variant must give the same bits."""
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+        ptopts.unset(k, raising=False)
     for k, v in KERNELS[request.param].items():
-        monkeypatch.setenv(k, v)
+        ptopts.set(k, v)
     return request.param
 
 
@@ -299,10 +299,10 @@ def test_invalid_scene_rejected():
 # ---------------------------------------------------------------------------------------------
 # kernel timing (pt_profile_*) and the AUTO policy (megakernel below 2^20 paths per call)
 # ---------------------------------------------------------------------------------------------
-def test_profile_records_every_launch(packed, monkeypatch):
+def test_profile_records_every_launch(packed, ptopts):
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv("PT_FUSE_GEN", "0")  # camera paths from k_wf_generate (the GEN form: below)
+        ptopts.unset(k, raising=False)
+    ptopts.set("PT_FUSE_GEN", "0")  # camera paths from k_wf_generate (the GEN form: below)
     p = packed["CornellBox"]
     meta = p.meta_for(64, 64)
     depth = 8
@@ -322,22 +322,22 @@ def test_profile_records_every_launch(packed, monkeypatch):
     assert set(wf) == {"k_wf_generate", "k_wf_step", "k_wf_accum"}
     assert wf["k_wf_step"]["launches"] == 2 * 2 * (depth + 1)
     assert wf["k_wf_generate"]["launches"] == 2 and wf["k_wf_accum"]["launches"] == 1
-    monkeypatch.setenv("PT_FUSE_GEN", "1")  # the first step launch makes the camera paths
+    ptopts.set("PT_FUSE_GEN", "1")  # the first step launch makes the camera paths
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
         s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
         wfg = s.profile_read()
     assert set(wfg) == {"k_wf_step", "k_wf_accum"}
     assert wfg["k_wf_step"]["launches"] == 2 * 2 * (depth + 1) and wfg["k_wf_accum"]["launches"] == 1
-    monkeypatch.setenv("PT_PERSIST", "1")  # one workgroup-local trace + shade launch per batch
+    ptopts.set("PT_PERSIST", "1")  # one workgroup-local trace + shade launch per batch
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
         s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
         wf1 = s.profile_read()
     assert set(wf1) == {"k_wf_step", "k_wf_accum"}
     assert wf1["k_wf_step"]["launches"] == 1 and wf1["k_wf_accum"]["launches"] == 1
-    monkeypatch.delenv("PT_PERSIST")
-    monkeypatch.setenv("PT_FUSE", "0")  # separate trace and shade kernels
+    ptopts.unset("PT_PERSIST")
+    ptopts.set("PT_FUSE", "0")  # separate trace and shade kernels
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
         s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
@@ -349,11 +349,11 @@ def test_profile_records_every_launch(packed, monkeypatch):
         assert 0.0 < v["min_ms"] <= v["avg_ms"] <= v["max_ms"] and v["total_ms"] > 0.0
 
 
-def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
+def test_auto_mode_picks_pipeline_by_size(packed, ptopts):
     """AUTO (pt_capi.hip launch_opts): the wavefront pipeline at every size on mailbox scenes (the
     fused kernel) and on scenes with cooperative big leaves, from 2^19 paths on the others."""
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+        ptopts.unset(k, raising=False)
 
     def kernels(name, W, H, nframes):
         p = packed[name]
@@ -374,11 +374,11 @@ def test_auto_mode_picks_pipeline_by_size(packed, monkeypatch):
     assert "k_wf_trace" in boat_small and "k_regen" not in boat_small
 
 
-def test_auto_large_render_matches_megakernel(packed, monkeypatch):
+def test_auto_large_render_matches_megakernel(packed, ptopts):
     """At the AUTO switch point the wavefront result equals the megakernel's bit for bit
     (both equal the oracle on the smaller cases above)."""
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+        ptopts.unset(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(512, 512)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
@@ -422,12 +422,12 @@ def packed_tie(tmp_path_factory):
                                  {"PT_BF_STACKLESS": "0", "PT_MB_UID_ORDER": "reverse"}],
                          ids=["bf", "bf_reverse_uids", "no_mailbox", "bf_reverse_1slot", "mb_lean16_reverse",
                               "bf_nofuse_reverse", "persist_reverse", "bf_stack_reverse"])
-def test_mailbox_exact_ties(packed_tie, monkeypatch, env):
+def test_mailbox_exact_ties(packed_tie, ptopts, env):
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv("PT_KERNEL", "wavefront")
+        ptopts.unset(k, raising=False)
+    ptopts.set("PT_KERNEL", "wavefront")
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        ptopts.set(k, v)
     p = packed_tie
     meta = p.meta_for(48, 40)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
@@ -447,11 +447,11 @@ def test_mailbox_exact_ties(packed_tie, monkeypatch, env):
                                        ("MedievalBoat", 24, 16), ("CornellBox", 32, 24)])
 @pytest.mark.parametrize("env", [{"PT_KERNEL": "mega"}, {"PT_KERNEL": "wavefront"},
                                  {"PT_KERNEL": "wavefront", "PT_FUSE": "0"}], ids=["mega", "wavefront", "wf_nofuse"])
-def test_vertex_normals_bitexact(packed, monkeypatch, scene, W, H, env):
+def test_vertex_normals_bitexact(packed, ptopts, scene, W, H, env):
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+        ptopts.unset(k, raising=False)
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        ptopts.set(k, v)
     p = packed[scene]
     meta = p.meta_for(W, H)
     oracle.set_vertex_normals(True)
@@ -474,42 +474,42 @@ def test_vertex_normals_bitexact(packed, monkeypatch, scene, W, H, env):
         assert not same_bits(gpu, plain)
 
 
-def test_large_image_single_part_matches_megakernel(packed, monkeypatch):
+def test_large_image_single_part_matches_megakernel(packed, ptopts):
     """4096^2 (config 5's image): more pixels than the default batch target, so the batch holds
     two frames, one per part on its own stream (and with PT_PARTS=1 one part holding both); the
     fused wavefront still equals the megakernel bit for bit (both equal the oracle on the small
     cases)."""
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+        ptopts.unset(k, raising=False)
     p = packed["CornellBox"]
     meta = p.meta_for(4096, 4096)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         a = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_WAVEFRONT)
-        monkeypatch.setenv("PT_PARTS", "1")
+        ptopts.set("PT_PARTS", "1")
         a1 = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_WAVEFRONT)
-        monkeypatch.delenv("PT_PARTS")
+        ptopts.unset("PT_PARTS")
         m = s.render(meta, 0, 2, 1, 2, pt_amd.MODE_MEGAKERNEL)
     assert same_bits(a, m), mismatch_report(a, m)
     assert same_bits(a1, m), mismatch_report(a1, m)
 
 
 @pytest.mark.parametrize("scene", ["CornellBox", "CornellBox-Mirror"])
-def test_entry_cull_full_size(packed, monkeypatch, scene):
+def test_entry_cull_full_size(packed, ptopts, scene):
     """The entry cull (bf_cull_mask) at the bench's image size: every launch culled, the default
     launches culled and none culled give the same bits (1024^2, 2 frames, the full depth)."""
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv("PT_KERNEL", "wavefront")
+        ptopts.unset(k, raising=False)
+    ptopts.set("PT_KERNEL", "wavefront")
     p = packed[scene]
     meta = p.meta_for(1024, 1024)
     out = {}
     for cull in ("0", "2", "99"):
-        monkeypatch.setenv("PT_CULL", cull)
+        ptopts.set("PT_CULL", cull)
         with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
             out[cull] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
-    monkeypatch.setenv("PT_CULL", "0")
+    ptopts.set("PT_CULL", "0")
     for gen in ("0", "1"):  # camera paths from k_wf_generate / made in the first fused launch
-        monkeypatch.setenv("PT_FUSE_GEN", gen)
+        ptopts.set("PT_FUSE_GEN", gen)
         with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
             out["gen" + gen] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
     assert same_bits(out["2"], out["0"]), mismatch_report(out["2"], out["0"])
@@ -529,11 +529,11 @@ def packed_multi(tmp_path_factory):
 
 
 @pytest.mark.parametrize("env", [{}, {"PT_KERNEL": "wavefront"}, {"PT_KERNEL": "mega"}])
-def test_multi_mesh_frame_bitexact(packed_multi, monkeypatch, env):
+def test_multi_mesh_frame_bitexact(packed_multi, ptopts, env):
     for k in ENV_KEYS:
-        monkeypatch.delenv(k, raising=False)
+        ptopts.unset(k, raising=False)
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        ptopts.set(k, v)
     p = packed_multi
     meta = p.meta_for(32, 24)
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:

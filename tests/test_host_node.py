@@ -181,12 +181,16 @@ let err = null;
 try { pt.sceneCreate(new Float32Array(64), new Float32Array(64), 0); } catch (e) { err = e.message; }
 let terr = null;
 try { pt.render(1, 2); } catch (e) { terr = e.constructor.name; }
-console.log(JSON.stringify({abi: pt.abiVersion(), keys: Object.keys(pt).sort(), err, terr}));''')
-    assert r["abi"] == 2
+let oerr = null;
+pt.setOption('kernel', 'wavefront'); pt.setOption('parts', 2); pt.setOption('kernel', null);
+try { pt.setOption('nosuch', '1'); } catch (e) { oerr = e.message; }
+console.log(JSON.stringify({abi: pt.abiVersion(), keys: Object.keys(pt).sort(), err, terr, oerr}));''')
+    assert r["abi"] == 3
+    assert r["oerr"] and "unknown option" in r["oerr"]
     assert r["keys"] == sorted(["abiVersion", "deviceCount", "sceneCreate", "sceneDestroy", "sceneInfo", "render",
                                 "renderSync", "renderMulti", "frame",
                                 "tonemap", "profileEnable", "profileRead", "bvhBuild", "renderImage",
-                                "sceneSetVertexNormals"])
+                                "sceneSetVertexNormals", "setOption"])
     assert r["terr"] == "TypeError"
     assert r["err"] and "pt_hip error" in r["err"]
 
