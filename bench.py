@@ -135,6 +135,29 @@ def launch_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def traffic_note(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int, field: str):
+    """A text field of the render kernel's entry in profiles/traffic.json (e.g. the VALU calibration)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            t = json.load(f).get(f"{W}x{H}x{spp}x{depth}x{world}", {})
+    except (OSError, ValueError):
+        return None
+    for k, v in t.items():
+        if k.startswith(kernel_prefix) and isinstance(v, dict) and field in v:
+            return v[field]
+    return None
+
+
+def load_trace_union(W: int, H: int, spp: int, depth: int, world: int):
+    """The rocprofv3 kernel-trace busy time of the render kernel for this configuration
+    (scripts/trace_union.py -> profiles/trace_union.json), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "trace_union.json")) as f:
+            return json.load(f).get(f"{W}x{H}x{spp}x{depth}x{world}")
+    except (OSError, ValueError):
+        return None
+
+
 def metric_name(scene: str, W: int, H: int, depth: int) -> str:
     """BASELINE.json's metric, for the workload actually run (its headline is CornellBox 1024^2 depth 8)."""
     return f"Msamples/s (paths/s) {scene} {W}x{H} depth {depth}"
@@ -339,6 +362,10 @@ def main():
         pre = prefixes.get(kernel, (kernel + "<",))
         traffic = load_traffic(pre, W, H, args.spp, args.depth, world)
         valu = load_traffic(pre, W, H, args.spp, args.depth, world, field="valu_issue")
+        valu_cal = traffic_note(pre, W, H, args.spp, args.depth, world, "valu_issue_calibration")
+        tu = load_trace_union(W, H, args.spp, args.depth, world)
+        if tu and tu.get("kernel") != kernel:
+            tu = None
         out = {
             "metric": metric_name(args.scene, W, H, args.depth),
             "value": round(value, 3),
@@ -370,6 +397,12 @@ def main():
                          "traffic_source": traffic[1] if traffic else None,
                          "kernel": kernel, "kernel_avg_ms": round(k_ms, 4),
                          "kernel_busy_ms_per_step": round(busy_ms, 3),
+                         "rocprof_busy_ms_per_step": tu["busy_ms_per_step_rocprof"] if tu else None,
+                         "rocprof_achieved": (round(bytes_per_launch * launches_per_render /
+                                                    (tu["busy_ms_per_step_rocprof"] * 1e-3) / 1e9, 2) if tu else None),
+                         "rocprof_source": ("profiles/trace_union.json: union of the kernel's dispatch intervals in a "
+                                            "rocprofv3 --kernel-trace of bench.py (scripts/trace_union.py, " +
+                                            tu["source"] + ")") if tu else None,
                          "achieved_def": "algorithmic bytes per launch (SURVEY.md 8d model from the GPU's work counters) x "
                                          "launches per step / the kernel's busy time per step (union of its launches' "
                                          "HIP-event intervals on every part stream)",
@@ -378,8 +411,10 @@ def main():
                          "pipeline": {"bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
                                       "achieved": round(pipeline, 2), "frac": round(pipeline / HBM_PEAK_GBS, 4)},
                          "valu_issue": ({"bound": "valu_issue", "frac": round(valu[0], 4),
-                                         "def": "4 x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE): SIMD issue cycles "
-                                                "of VALU over all SIMD cycles, kernel alone (PMC pass)",
+                                         "def": "k x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE): VALU issue over "
+                                                "the SIMDs' peak issue rate, kernel alone (PMC pass); k calibrated so "
+                                                "that a kernel issuing v_fma_f32 at peak reads 1.0",
+                                         "calibration": valu_cal or "uncalibrated (k = 4)",
                                          "source": valu[1]} if valu else None),
                          "kernels_ms_warmup_step": {k: round(v["total_ms"] / max(args.warmup, 1), 3)
                                                     for k, v in prof_warm.items()},

@@ -1124,6 +1124,34 @@ int pt_selftest_math(int device, int fn, const float* a, const float* b, float* 
     return PT_OK;
 }
 
+int pt_selftest_valu(int device, int iters, int reps, int packed, double* ms_out, uint64_t* fma_wave_instr_out) {
+    if (iters < 1 || reps < 1 || !ms_out) return fail(PT_ERR_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(device));
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    const int blocks = cus * 8;  // 8 blocks of 4 waves per CU: 8 waves per SIMD
+    float* d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)blocks * 256 * sizeof(float)));
+    hipEvent_t a = nullptr, b = nullptr;
+    hipError_t e = hipEventCreate(&a);
+    if (e == hipSuccess) e = hipEventCreate(&b);
+    if (e == hipSuccess) e = launch_selftest_valu(iters, blocks, packed, d, nullptr);  // warm-up (clock ramp)
+    if (e == hipSuccess) e = hipEventRecord(a, nullptr);
+    for (int r = 0; r < reps && e == hipSuccess; ++r) e = launch_selftest_valu(iters, blocks, packed, d, nullptr);
+    if (e == hipSuccess) e = hipEventRecord(b, nullptr);
+    if (e == hipSuccess) e = hipEventSynchronize(b);
+    float ms = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
+    if (a) hipEventDestroy(a);
+    if (b) hipEventDestroy(b);
+    hipFree(d);
+    if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
+    *ms_out = ms;
+    // v_fma_f32 / v_pk_fma_f32 wave-instructions of the timed launches: 32 per iteration per wave
+    if (fma_wave_instr_out) *fma_wave_instr_out = (uint64_t)reps * blocks * 4 * (uint64_t)iters * 32;
+    return PT_OK;
+}
+
 int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
                     uint32_t* failing_bits) {
     if (!mismatches || steps < -1 || steps > 2 || lo_bits > hi_bits || hi_bits >= 0x80000000u)

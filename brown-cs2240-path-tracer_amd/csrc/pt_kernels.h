@@ -180,5 +180,6 @@ hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t 
 
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);
+hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, hipStream_t stream);
 
 }  // namespace pt

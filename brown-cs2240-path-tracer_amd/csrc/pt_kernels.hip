@@ -160,6 +160,56 @@ hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned lon
     return hipGetLastError();
 }
 
+// VALU issue calibration (pt_selftest_valu): every thread runs 8 independent v_fma_f32 chains,
+// 32 FMAs per loop iteration and no memory operation in the loop, at 8 waves per SIMD (the host
+// sizes the grid from the CU count), so the chains' latency is hidden and the SIMDs issue VALU at
+// their peak rate — the known rate against which scripts/summarize_traffic.py's PMC formula for
+// `valu_issue` is calibrated (scripts/calibrate_valu.sh).  The sum is stored only if it equals an
+// impossible value, so the chains stay live and nothing is written.
+__global__ __launch_bounds__(256) void k_selftest_valu(int iters, float seed, float m, float c, float* out) {
+    float a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = seed + (float)(threadIdx.x + k);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[k] = fmaf(a[k], m, c);
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += a[k];
+    if (s == -1.0f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// the same with packed f32: 8 independent v_pk_fma_f32 chains (two FMAs per lane each)
+typedef float fv2s __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_selftest_valu_pk(int iters, float seed, float m, float c, float* out) {
+    fv2s a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = fv2s{seed + (float)(threadIdx.x + k), seed - (float)(threadIdx.x + k)};
+    const fv2s mm = {m, m}, cc = {c, c};
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[k] = __builtin_elementwise_fma(a[k], mm, cc);
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += a[k].x + a[k].y;
+    if (s == -1.0f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, hipStream_t stream) {
+    // m, c as arguments: the FMAs read them from SGPRs (no literal-constant encodings in the loop)
+    if (packed)
+        hipLaunchKernelGGL(k_selftest_valu_pk, dim3(blocks), dim3(256), 0, stream, iters, 1.0f, 0.99999994f, 1.0e-7f, out);
+    else
+        hipLaunchKernelGGL(k_selftest_valu, dim3(blocks), dim3(256), 0, stream, iters, 1.0f, 0.99999994f, 1.0e-7f, out);
+    return hipGetLastError();
+}
+
 __global__ void k_selftest_math(int fn, const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ o,
                                 int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;

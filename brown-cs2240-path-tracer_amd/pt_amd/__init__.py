@@ -32,6 +32,7 @@ from ._lib import (  # noqa: F401
     reset_options,
     selftest_math,
     selftest_rcp,
+    selftest_valu,
     set_hw_queues,
     set_option,
     source_hash,

@@ -125,11 +125,12 @@ def load_library():
     L.pt_scene_check.argtypes = [p]
     L.pt_render_multi.argtypes = [ctypes.POINTER(p), i, p, u32, u32, u32, i, i, p, p]
     L.pt_set_hw_queues.argtypes = [i]
+    L.pt_selftest_valu.argtypes = [i, i, i, i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     L.pt_set_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     L.pt_get_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
     L.pt_reset_options.argtypes = []
     L.pt_reset_options.restype = None
-    for fn in ("pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+    for fn in ("pt_selftest_valu", "pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
                "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
@@ -372,6 +373,14 @@ def selftest_rcp(steps: int = -1, lo_bits: int = 0x00800000, hi_bits: int = 0x7E
     b = ctypes.c_uint32(0)
     _check(L.pt_selftest_rcp(device, steps, lo_bits, hi_bits, ctypes.byref(m), ctypes.byref(b)))
     return int(m.value), int(b.value)
+
+
+def selftest_valu(iters: int = 20000, reps: int = 5, packed: bool = False, device: int = 0):
+    """pt_selftest_valu: (ms of the timed launches, FMA wave-instructions they issued; packed: v_pk_fma_f32)."""
+    ms = ctypes.c_double(0.0)
+    n = ctypes.c_uint64(0)
+    _check(load_library().pt_selftest_valu(device, iters, reps, 1 if packed else 0, ctypes.byref(ms), ctypes.byref(n)))
+    return float(ms.value), int(n.value)
 
 
 def bvh_build(vertices, tris, sah: bool = False) -> np.ndarray:

@@ -246,6 +246,14 @@ int pt_selftest_math(int device, int fn, const float* a, const float* b, float* 
 int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
                     uint32_t* failing_bits);
 
+/* VALU issue calibration: `reps` timed launches (after one untimed) of a kernel whose threads run 8
+ * independent v_fma_f32 chains (packed != 0: v_pk_fma_f32, two FMAs per lane each; 32 instructions
+ * per iteration, `iters` iterations, no memory operation) at 8 waves per SIMD — the SIMDs issue VALU
+ * at their peak rate.  *ms_out = the timed launches' event time; *fma_wave_instr_out (nullable) =
+ * their FMA wave-instructions.  Profiled with rocprofv3 PMC it pins the counter formula for the
+ * fraction of VALU issue (scripts/calibrate_valu.sh). */
+int pt_selftest_valu(int device, int iters, int reps, int packed, double* ms_out, uint64_t* fma_wave_instr_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,16 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 rc=$?; echo "rocprof rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 cp gpurun_out/bench_kt/run_kernel_stats.csv gpurun_out/profiles/${TAG}_bench_kernel_stats.csv
 grep "^{" gpurun_out/bench_kt.log > gpurun_out/profiles/${TAG}_bench_under_rocprof.json || true
+# the kernel's busy time from the trace itself (union of its dispatch intervals), for bench.py
+cp profiles/trace_union.json gpurun_out/profiles/trace_union.json 2>/dev/null || true
+python3 scripts/trace_union.py gpurun_out/bench_kt/run_kernel_trace.csv gpurun_out/profiles/${TAG}_bench_under_rocprof.json \
+  gpurun_out/profiles/trace_union.json > gpurun_out/profiles/${TAG}_trace_union.log 2>&1
+rc=$?; echo "trace union rc=$rc"; grep busy_ms gpurun_out/profiles/${TAG}_trace_union.log
+cp gpurun_out/profiles/trace_union.json profiles/trace_union.json 2>/dev/null || true
+# VALU issue calibration (the traffic summary below applies it)
+timeout -k 10 400 bash scripts/calibrate_valu.sh > gpurun_out/profiles/${TAG}_valu_calibration.log 2>&1
+rc=$?; echo "valu calibration rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
+cp gpurun_out/profiles/valu_calibration.json profiles/valu_calibration.json
 timeout -k 10 900 bash scripts/collect_traffic.sh
 rc=$?; echo "traffic rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 # this box's copy of the tree: let the second bench read the traffic just measured

@@ -2,9 +2,11 @@
 """Summarize the rocprofv3 PMC passes of scripts/collect_traffic.sh (gpurun_out/traffic/{fetch,
 write,valu}) into traffic.json: per kernel instance and launch, HBM bytes (FETCH_SIZE x 2 for
 gfx950 + WRITE_SIZE, KB -> bytes) and the VALU issue fraction
-    valu_issue = 4 * SQ_ACTIVE_INST_VALU / (128 * GRBM_GUI_ACTIVE)
-(SQ_ACTIVE_INST_VALU in quad-cycles, ~1 per wave64 VALU instruction = 4 SIMD cycles;
-GRBM_GUI_ACTIVE summed over the 8 XCDs, each of 32 CUs x 4 SIMDs: SIMD-cycles = GRBM / 8 x 1024).
+    valu_issue = k * SQ_ACTIVE_INST_VALU / (128 * GRBM_GUI_ACTIVE)
+(GRBM_GUI_ACTIVE summed over the 8 XCDs, each of 32 CUs x 4 SIMDs: SIMD-cycles = GRBM / 8 x 1024),
+with k calibrated on a kernel that issues VALU at the SIMDs' peak by construction
+(profiles/valu_calibration.json, scripts/calibrate_valu.sh: that kernel reads 1.0).  Without the
+calibration file k = 4 (the uncalibrated quad-cycle reading, marked as such).
 PMC passes serialise the kernels, so these are per-launch figures of a kernel running alone.
 Usage: summarize_traffic.py [out.json]"""
 import collections
@@ -34,7 +36,17 @@ def load(tag, counters):
     return mean, ndisp
 
 
+def calibration():
+    path = "profiles/valu_calibration.json"
+    try:
+        c = json.load(open(path))
+        return c["k_active"], f"{path} (k = {c['k_active']:.3f}: pt_selftest_valu reads 1.0)"
+    except (OSError, KeyError, ValueError):
+        return 4.0, "uncalibrated (k = 4, quad-cycle reading)"
+
+
 def main():
+    k_valu, cal_src = calibration()
     fetch, ndisp = load("fetch", {"FETCH_SIZE"})
     write, _ = load("write", {"WRITE_SIZE"})
     valu, _ = load("valu", {"SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVE_CYCLES",
@@ -54,7 +66,8 @@ def main():
              "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KB -> bytes, mean per dispatch"}
         v = valu.get(k)
         if v and v.get("GRBM_GUI_ACTIVE"):
-            e["valu_issue"] = 4.0 * v["SQ_ACTIVE_INST_VALU"] / (128.0 * v["GRBM_GUI_ACTIVE"])
+            e["valu_issue"] = k_valu * v["SQ_ACTIVE_INST_VALU"] / (128.0 * v["GRBM_GUI_ACTIVE"])
+            e["valu_issue_calibration"] = cal_src
             e["valu_lane_util"] = v.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * v["SQ_ACTIVE_INST_VALU"]) if v.get("SQ_ACTIVE_INST_VALU") else None
             e["valu_counters"] = v
         t[key][short] = e
