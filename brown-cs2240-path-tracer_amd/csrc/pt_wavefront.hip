@@ -88,6 +88,34 @@ __device__ __forceinline__ void load_shading_point(const WfBuffers& wb, uint32_t
     ps.wi = mk(b.w, c.x, c.y);
 }
 
+// The fused kernels' shadow queue (bf_step_batch, its only writer and reader) holds 88 B per entry
+// instead of the 104 B of a ray + path state + shading point: the shadow ray's origin is not
+// stored — it is offset = madd(hp, hn, 1e-4), recomputed from the shading point with the very
+// operation path_after_ext made it with (the same bits) — and the words are packed into the
+// queue's arrays as
+//   ray[2i]   = (d.xyz, path)      ray[2i+1] = (depth | spec, L.xyz)   q2 = (seed, beta.xyz)
+//   q3        = (hp.xyz, material) sp0      = (hn.xyz, wi.x)          sp2 = (wi.y, wi.z)
+// (sp1 unused).  The traversal pipeline (k_wf_trace + k_wf_shade) keeps the full layout above.
+__device__ __forceinline__ void store_shadow_packed(const WfBuffers& wb, uint32_t i, const Ray& r, uint32_t p,
+                                                    const PathState& ps) {
+    const WfQueue& Q = wb.shd;
+    Q.ray[2 * (size_t)i] = make_float4(r.d.x, r.d.y, r.d.z, __builtin_bit_cast(float, p));
+    Q.ray[2 * (size_t)i + 1] = make_float4(__builtin_bit_cast(float, pack_dspec(ps)), ps.L.x, ps.L.y, ps.L.z);
+    Q.q2[i] = make_float4(__builtin_bit_cast(float, ps.seed), ps.beta.x, ps.beta.y, ps.beta.z);
+    Q.q3[i] = make_float4(ps.hp.x, ps.hp.y, ps.hp.z, __builtin_bit_cast(float, ps.mat_id));
+    wb.sp0[i] = make_float4(ps.hn.x, ps.hn.y, ps.hn.z, ps.wi.x);
+    wb.sp2[i] = make_float2(ps.wi.y, ps.wi.z);
+}
+// the ray of a packed shadow entry from its words (a = ray[2i], h = q3, n = sp0)
+__device__ __forceinline__ Ray unpack_shadow_ray(float4 a, float4 h, float4 n, uint32_t& p) {
+    Ray r;
+    r.o = madd(mk(h.x, h.y, h.z), mk(n.x, n.y, n.z), 1.0e-4f);  // = path_after_ext's offset, bit for bit
+    r.d = mk(a.x, a.y, a.z);
+    r.inv = rcp3(r.d);
+    p = __builtin_bit_cast(uint32_t, a.w);
+    return r;
+}
+
 // pixel of path p (row-major within its frame)
 __device__ __forceinline__ void path_pixel(uint32_t p, uint32_t npix, uint32_t W, uint32_t& x, uint32_t& y, uint32_t& f) {
     f = p / npix;
@@ -326,7 +354,11 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
 constexpr int kBfSlots = 8;
 // phase 1 in entry pairs with packed f32 (bf_pairs): bit-exact, measured no faster (fused kernel,
 // extension rays only: 2598 vs 2607 Msamples/s; both queues: 2446, VGPR spills in the shadow instance)
-constexpr bool kBfPacked = false;  // (k_regen_bf, itself opt-in, uses bf_pairs: tests cover it)
+#ifndef PT_BF_PACKED
+#define PT_BF_PACKED 0
+#endif
+constexpr bool kBfPacked = PT_BF_PACKED != 0;  // (k_regen_bf, itself opt-in, uses bf_pairs: tests cover it)
+constexpr bool kBfPackedShadow = PT_BF_PACKED >= 2;  // the shadow instances too
 // Diagnostic build only (EXTRA=-DPT_PHASE_TIMING=1, scripts/phase_timing.py): shader-clock
 // cycles per phase of bf_step_batch, summed per wave slot (8 phases x {extension, shadow}).
 #ifndef PT_PHASE_TIMING
@@ -439,6 +471,7 @@ template <bool FAST_RCP>
 __device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool valid, float* slot, int nslots,
                                          uint64_t& hits, int& nh, float& tmin) {
     const int NP = (sc.n_tris - sc.mb_base + 1) >> 1;
+    const uint64_t vmask = __builtin_amdgcn_ballot_w64(valid);
     for (int j = 0; j < NP; ++j) {
         const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(sc.bfpair + 20 * j);
         const fv2 v0x = {f[0], f[1]}, v0y = {f[2], f[3]}, v0z = {f[4], f[5]};
@@ -456,9 +489,13 @@ __device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool
         }
         const fv2 sx = sp2(r.o.x) - v0x, sy = sp2(r.o.y) - v0y, sz = sp2(r.o.z) - v0z;
         const fv2 bu = inv * fma2(sz, rz, fma2(sy, ry, sx * rx));
-        const bool ok0 = valid & !(det.x > -1e-8f && det.x < 1e-8f) & !(bu.x < 0.0f) & !(bu.x > 1.0f);
-        const bool ok1 = valid & !(det.y > -1e-8f && det.y < 1e-8f) & !(bu.y < 0.0f) & !(bu.y > 1.0f);
-        if (!wave_any(ok0 | ok1)) continue;  // wave-uniform
+        const bool d0 = !(det.x > -1e-8f && det.x < 1e-8f), l0 = !(bu.x < 0.0f), g0 = !(bu.x > 1.0f);
+        const bool d1 = !(det.y > -1e-8f && det.y < 1e-8f), l1 = !(bu.y < 0.0f), g1 = !(bu.y > 1.0f);
+        const bool ok0 = valid & d0 & l0 & g0, ok1 = valid & d1 & l1 & g1;
+        // the vote on SGPR masks of the single compares (as bf_closest's entry loop)
+        const uint64_t any0 = __builtin_amdgcn_ballot_w64(d0) & __builtin_amdgcn_ballot_w64(l0) & __builtin_amdgcn_ballot_w64(g0);
+        const uint64_t any1 = __builtin_amdgcn_ballot_w64(d1) & __builtin_amdgcn_ballot_w64(l1) & __builtin_amdgcn_ballot_w64(g1);
+        if ((vmask & (any0 | any1)) == 0) continue;  // wave-uniform
         const fv2 cx = fma2(sy, e1z, -(sz * e1y)), cy = fma2(sz, e1x, -(sx * e1z)), cz = fma2(sx, e1y, -(sy * e1x));
         const fv2 bv = inv * fma2(dz, cz, fma2(dy, cy, dx * cx));
         const fv2 t = inv * fma2(e2z, cz, fma2(e2y, cy, e2x * cx));
@@ -468,13 +505,13 @@ __device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool
             if (nh < nslots) slot[64 * nh] = t.x;
             ++nh;
             hits |= 1ull << (2 * j);
-            tmin = fminf(tmin, t.x);
+            tmin = t.x < tmin ? t.x : tmin;
         }
         if (h1) {
             if (nh < nslots) slot[64 * nh] = t.y;
             ++nh;
             hits |= 1ull << (2 * j + 1);
-            tmin = fminf(tmin, t.y);
+            tmin = t.y < tmin ? t.y : tmin;
         }
     }
 }
@@ -747,34 +784,57 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
             d3 = make_float4(g.beta.x, g.beta.y, g.beta.z, 0.0f);
             if (COUNT) { c.samples++; c.ext_queries++; }
         }
-    } else {
+    } else if (EXT) {
         a0 = in.ray[2 * e];
         a1 = in.ray[2 * e + 1];
         if (!valid) { a0 = make_float4(0, 0, 0, 1); a1 = make_float4(0, 0, 0, 0); }
     }
     uint32_t p;
-    Ray r = unpack_ray(a0, a1, p);
+    Ray r;
+    if (EXT || fresh) {
+        r = unpack_ray(a0, a1, p);
+    } else {  // packed shadow entry (store_shadow_packed): the origin from the shading point (its
+              // words are read again after the trace, from cache, rather than held across it)
+        a0 = valid ? in.ray[2 * e] : make_float4(0, 0, 1, 0);
+        r = unpack_shadow_ray(a0, valid ? in.q3[e] : make_float4(0, 0, 0, 0),
+                              valid ? wb.sp0[e] : make_float4(0, 0, 0, 0), p);
+    }
     const uint64_t todo = cull ? bf_cull_mask(sc, r, valid, sc.n_tris - sc.mb_base) : ~0ull;  // before the prefetch: fewer live VGPRs
     // the path state is loaded before the trace and arrives while it runs (kBfPrefetch)
-    if (!fresh && kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
+    if (!fresh && kBfPrefetch) {
+        if (EXT) { c2 = in.q2[e]; d3 = in.q3[e]; }
+        else { a1 = in.ray[2 * e + 1]; c2 = in.q2[e]; }
+    }
     float t;
     if (PT_PHASE_TIMING) tm[1] = phase_clock();
-    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t, todo,
+    const int rec = bf_closest<FAST_RCP, COUNT, EXT ? kBfPacked : kBfPackedShadow>(sc, gtris, r, valid, l.slot, nslots, l.stack, blockDim.x, c, t, todo,
                                                 PT_PHASE_TIMING ? &tm[2] : nullptr);
     if (PT_PHASE_TIMING) tm[3] = phase_clock();
     bool more = false;
     PathState ps;
     if (valid) {
-        if (!fresh && !kBfPrefetch) { c2 = in.q2[e]; d3 = in.q3[e]; }
-        unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
-        ps.L = mk(c2.x, c2.y, c2.z);
-        ps.seed = __builtin_bit_cast(uint32_t, c2.w);
-        ps.beta = mk(d3.x, d3.y, d3.z);
+        if (!fresh && !kBfPrefetch) {
+            if (EXT) { c2 = in.q2[e]; d3 = in.q3[e]; }
+            else { a1 = in.ray[2 * e + 1]; c2 = in.q2[e]; }
+        }
         if (EXT) {
+            unpack_dspec(__builtin_bit_cast(uint32_t, a1.w), ps);
+            ps.L = mk(c2.x, c2.y, c2.z);
+            ps.seed = __builtin_bit_cast(uint32_t, c2.w);
+            ps.beta = mk(d3.x, d3.y, d3.z);
             more = path_after_ext(sc, rec, t, r, ps);
             if (more && COUNT) c.shadow_queries++;
-        } else {
-            load_shading_point(wb, (uint32_t)e, ps);
+        } else {  // packed shadow entry
+            unpack_dspec(__builtin_bit_cast(uint32_t, a1.x), ps);
+            ps.L = mk(a1.y, a1.z, a1.w);
+            ps.seed = __builtin_bit_cast(uint32_t, c2.x);
+            ps.beta = mk(c2.y, c2.z, c2.w);
+            const float4 h3 = in.q3[e], n4 = wb.sp0[e];
+            ps.hp = mk(h3.x, h3.y, h3.z);
+            ps.mat_id = __builtin_bit_cast(int, h3.w);
+            const float2 w2 = wb.sp2[e];
+            ps.hn = mk(n4.x, n4.y, n4.z);
+            ps.wi = mk(n4.w, w2.x, w2.y);
             more = path_after_shadow(sc, fp, rec, t, r, ps);
             if (more && COUNT) c.ext_queries++;
         }
@@ -791,8 +851,8 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
         base = __shfl(base, 0, 64);
         if (more) {
             const uint32_t j = (uint32_t)rbase + base + rank_below(keep);
-            store_entry(out, j, r, p, ps);
-            if (EXT) store_shading_point(wb, j, ps);
+            if (EXT) store_shadow_packed(wb, j, r, p, ps);
+            else store_entry(out, j, r, p, ps);
         }
     }
 #if PT_PHASE_TIMING
