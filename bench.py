@@ -226,6 +226,8 @@ def main():
     ap.add_argument("--reduce", choices=["rccl", "ordered"], help="--native-multi: pt_render_multi's reduction")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch HIP events")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library option (pt_set_option) for A/B and profiling runs; repeatable")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the rank plumbing (launch, sharding, reduce, timing, JSON line); renders "
                          "nothing and reports no value")
@@ -258,6 +260,9 @@ def main():
     if args.dry_run:
         return dry_run(args, rank, world, ranks_seen, backend, dist, frames_for_rank, reduce_accum)
     import pt_amd
+    for kv in args.opt:
+        k, _, v = kv.partition("=")
+        pt_amd.set_option(k, v)
     if backend == "gloo":
         local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
@@ -388,6 +393,7 @@ def main():
                                                                         if world > 1 else ""),
                        "mode": args.mode, "bvh": args.bvh, "samples_per_step": total_samples,
                        "ranks": ranks_seen, "backend": backend if world > 1 else None,
+                       "options": dict(kv.partition("=")[::2] for kv in args.opt) or None,
                        "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

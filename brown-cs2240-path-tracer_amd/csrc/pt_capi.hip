@@ -73,7 +73,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"fuse", OPT_BOOL, nullptr},         {"fuse_gen", OPT_BOOL, nullptr},    {"bf", OPT_BOOL, nullptr},
     {"mailbox", OPT_BOOL, nullptr},      {"persist", OPT_BOOL, nullptr},     {"regen", OPT_BOOL, nullptr},
     {"regen_bf", OPT_BOOL, nullptr},     {"bf_stackless", OPT_BOOL, nullptr}, {"trace_dyn", OPT_BOOL, nullptr},
-    {"packet", OPT_BOOL, nullptr},
+    {"tiles", OPT_BOOL, nullptr},        {"packet", OPT_INT, nullptr},       {"packet_nodes", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"cull", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr},
@@ -281,6 +281,9 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
         }
         const int32_t U = (int32_t)first.size();
         L.mailbox = U >= 1 && U <= 64;
+        // every record carries its entry's uid (k_wf_trace_pk keys its phase-1 hits by it; the
+        // mailbox scenes renumber below)
+        for (size_t r = 0; r < entry.size(); ++r) L.tris[r].uid = uid[r];
         if (L.mailbox) {
             const bool rev = opts_snapshot().is("mb_uid_order", "reverse");
             for (auto& u : uid) u = rev ? U - 1 - u : u;
@@ -746,6 +749,7 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 // leaves (MedievalBoat 256^2 x 1: 62 / 35); other scenes from about 2^19 paths (Glossy 512^2 x 1:
 // 7.1 / 9.1, 512^2 x 2: 13.1 / 9.6).
 constexpr uint64_t kWfAutoMinPaths = 1ull << 19;
+constexpr int kTilesDefault = 0;
 
 LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView& view) {
     LaunchOpts lo;
@@ -773,7 +777,8 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.regen = o.flag("regen", lo.regen);
     lo.regen_target = o.num("regen_target", lo.regen_target);
     lo.sort = (int)o.num("sort", lo.sort);  // 1 / 8: direction octant; 64: + origin octant; 512: + 4^3 origin cells
-    lo.packet = o.flag("packet", lo.packet);
+    lo.packet = (int)o.num("packet", lo.packet);
+    lo.packet_nodes = (int)o.num("packet_nodes", 0);
     lo.trace_dyn = o.flag("trace_dyn", lo.trace_dyn);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
@@ -931,6 +936,8 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);
+    // camera paths of the wavefront batches in 8x8 pixel tiles (slot_path; every path's bits are the same)
+    fp.tiles = o.flag("tiles", kTilesDefault);
     if ((rc = take_watchdog(s)) != PT_OK) return rc;  // an earlier asynchronous render failed
     if (lo.wavefront) {
         const uint64_t target = (uint64_t)std::max(1L, o.num("wf_paths", (long)kWfTargetPaths));  // A/B

@@ -78,7 +78,8 @@ struct LaunchOpts {
     int trace_blocks = 0;  // traversal / step kernels: cap on the grid (tests): 0 = occupancy-derived
     int trace_dyn = 0;     // k_wf_trace takes its windows from group counters (1) or the static split (0)
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
-    int packet = -1;       // traversal scenes: packet superset walk + replay (k_wf_trace_pk): -1 default
+    int packet = -1;       // traversal scenes: packet walk + replay (k_wf_trace_pk) on 1 camera / 2 + shadow / 3 all launches: -1 default (off)
+    int packet_nodes = 0;  // k_wf_trace_pk's node budget per packet (0: kPkMaxNodes)
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -156,7 +157,8 @@ struct WfStreams {
     int trace_dyn = 0;     // k_wf_trace window hand-out from group counters
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
-    int packet = 0;        // traversal scenes: packet walk + replay (k_wf_trace_pk)
+    int packet = 0;        // traversal scenes: packet walk + replay (k_wf_trace_pk; pk_launch)
+    int packet_nodes = 0;  // its node budget (0: kPkMaxNodes)
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

@@ -54,7 +54,7 @@ struct alignas(16) Tri {
     float q1[4];   // e1.y e1.z e2.x e2.y
     float e2z;
     int32_t mat;
-    int32_t uid;   // mailbox scenes: id of this (i0, i1, i2, material) entry, < 64; else -1
+    int32_t uid;   // id of this (i0, i1, i2, material) entry (distinct entries numbered by first appearance; < 64 on mailbox scenes)
     int32_t pad;
 };
 inline void tri_set(Tri& t, const float v0[3], const float e1[3], const float e2[3]) {
@@ -147,6 +147,7 @@ struct FrameParams {
     uint32_t width, height;  // u32(meta[0]), u32(meta[1])
     int32_t direct_only;  // meta[46] > 0
     int32_t max_depth;    // literal 16 in `while(depth <= 16)`, program-raymarch.wgsl:118
+    int32_t tiles;        // wavefront camera paths generated in 8x8 pixel tiles (slot_path; results unchanged)
 };
 
 }  // namespace pt

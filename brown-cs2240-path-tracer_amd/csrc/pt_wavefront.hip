@@ -116,12 +116,40 @@ __device__ __forceinline__ Ray unpack_shadow_ray(float4 a, float4 h, float4 n, u
     return r;
 }
 
-// pixel of path p (row-major within its frame)
-__device__ __forceinline__ void path_pixel(uint32_t p, uint32_t npix, uint32_t W, uint32_t& x, uint32_t& y, uint32_t& f) {
-    f = p / npix;
-    const uint32_t pix = p - f * npix;
-    y = pix / W;
-    x = pix - y * W;
+// The camera path made for queue slot s (the s-th path of a batch part in generation order): its
+// frame f, pixel (x, y) and path id p = f * npix + y * W + x (row-major within its frame: the
+// radiance index k_wf_accum reads).  Row order (fp.tiles == 0): slot = path id.  Tile order
+// (fp.tiles != 0): a frame's slots walk 8x8 pixel tiles, so the 64 paths of a generation batch are
+// one tile (coherent camera rays in one wave) — the W8 x H8 part of the image (W8, H8 = W, H
+// rounded down to multiples of 8) in tiles, then the pixels right of it, then those below it, row
+// by row.  Only which slot a path starts in changes: every path computes the same bits.
+__device__ __forceinline__ uint32_t slot_path(uint32_t s, const FrameParams& fp, uint32_t& x, uint32_t& y, uint32_t& f) {
+    const uint32_t W = fp.width, npix = W * fp.height;
+    f = s / npix;
+    uint32_t q = s - f * npix;
+    if (!fp.tiles) {
+        y = q / W;
+        x = q - y * W;
+    } else {
+        const uint32_t TW = W >> 3, TH = fp.height >> 3, core = TW * TH * 64;
+        if (q < core) {
+            const uint32_t t = q >> 6, l = q & 63u, ty = t / TW;
+            x = (t - ty * TW) * 8 + (l & 7u);
+            y = ty * 8 + (l >> 3);
+        } else {
+            q -= core;
+            const uint32_t rw = W - TW * 8, nr = rw * TH * 8;
+            if (q < nr) {
+                y = q / rw;
+                x = TW * 8 + (q - y * rw);
+            } else {
+                q -= nr;
+                y = TH * 8 + q / W;
+                x = q - (y - TH * 8) * W;
+            }
+        }
+    }
+    return f * npix + y * W + x;
 }
 
 template <bool COUNT>
@@ -145,15 +173,15 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
     if (blockIdx.x == 0 && threadIdx.x < 2 * kTraceGroups)
         wb.rfetch[((threadIdx.x / kTraceGroups) * kRegions + threadIdx.x % kTraceGroups) * kFetchStride] = 0;
     Counters c = {};
-    if (p < P) {
+    if (p < P) {  // p: the queue slot; pid: the path made there (slot_path)
         uint32_t x, y, f;
-        path_pixel(p, fp.width * fp.height, fp.width, x, y, f);
+        const uint32_t pid = slot_path(p, fp, x, y, f);
         const uint32_t t = raw_salt ? frame0 : (uint32_t)(float)(frame0 + (fbase + f) * stride);
         PathState ps;
         Ray r = path_begin(fp, x, y, t, ps);
         const uint32_t j = p / 64;
         const uint32_t i = R ? (j % R) * wb.rstride + (j / R) * 64 + (p & 63) : p;
-        store_entry(wb.ext, i, r, p, ps);
+        store_entry(wb.ext, i, r, pid, ps);
         if (COUNT) { c.samples++; c.ext_queries++; }
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -738,6 +766,209 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
     if (COUNT) flush_counters(c, cnt_out);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Packet walk + replay (traversal scenes, option packet; verdict r02 item 3): brute force + replay
+// generalised past 64 distinct entries.  A wave takes 64 queue entries and
+//   phase 1  walks the reference tree ONCE for all of them as a packet: a node's child is entered
+//            when some lane that reached the node has dist > 0 for it (no closest-t pruning), with
+//            the mask of those lanes, so the packet visits the union of the lanes' UNPRUNED walks —
+//            a superset of every lane's reference walk (pruning only removes nodes).  Each leaf
+//            reached is tested wave-uniformly (records through s_load, as bf_closest's phase 1);
+//            per lane the hits of the lanes that reached the leaf are kept as (entry uid, t), up
+//            to kPkSlots distinct uids, with their smallest t (tmin);
+//   phase 2  replays each lane's reference traversal (node steps, exit-distance pruning, strict-<
+//            in leaf order) where a leaf entry costs a uid lookup instead of a triangle test.
+// Exact: a triangle test is a pure function of (ray, record) and duplicated records of an entry
+// hold the same floats, so phase 1's t is the test's t; every leaf of the lane's walk was tested
+// for the lane; entries phase 1 did not record are misses.  A lane stops once its closest t equals
+// tmin (no later entry is smaller, an equal one loses the strict <); a lane with more distinct
+// hits than slots replays with real tests.  A packet whose union exceeds `max_nodes` node visits
+// (incoherent rays: the union approaches the whole tree) gives up and every lane walks its own
+// tree with real tests (the same replay with the test switched on).
+constexpr int kPkSlots = 8;
+constexpr int kPkMaxNodes = 96;  // packet node visits before a wave gives up (incoherent rays)
+// which launches of a batch take the packet kernel: option packet = 1: the camera rays (launch 0),
+// 2: camera and shadow rays, 3: every launch
+__host__ __device__ inline bool pk_launch(int mode, int it) {
+    return mode >= 3 || (mode >= 1 && it == 0) || (mode == 2 && (it & 1));
+}
+constexpr int kPkStack = 64;  // (node, lane mask) entries per wave: <= 1 + depth of tree entries
+constexpr uint32_t kPkLdsPerWave = kPkStack * 16 + kPkSlots * 64 * 8;
+constexpr uint32_t kPkBlock = 256;  // 4 waves: per-lane replay stacks + 5 KB per wave of packet state
+
+__device__ __forceinline__ void load_node_scalar(const Node* nodes, int n, float4& a, float4& b, float4& c, int4& d) {
+    const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(nodes + n);
+    a = make_float4(f[0], f[1], f[2], f[3]);
+    b = make_float4(f[4], f[5], f[6], f[7]);
+    c = make_float4(f[8], f[9], f[10], f[11]);
+    const __attribute__((address_space(4))) int* q = (const __attribute__((address_space(4))) int*)(nodes + n);
+    d = make_int4(q[12], q[13], q[14], q[15]);
+}
+
+// every loop of the kernel is bounded: a wave that exceeds kPkGuard iterations in one loop (a bug,
+// never a correct walk: the replay visits each node at most once) reports like k_wf_trace's
+// watchdog (ctl[WF_WATCHDOG], state in ctl[WF_SNAP..]) and stops, so the grid always drains
+constexpr uint32_t kPkGuard = 1u << 22;
+__device__ __forceinline__ void pk_report(const WfBuffers& wb, uint32_t where, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if (lane_id() == 0) {
+        atomicOr(&wb.ctl[WF_WATCHDOG], 1u);
+        if (atomicCAS(&wb.ctl[WF_SNAP_CLAIM], 0u, 1u) == 0u) {
+            const uint32_t v[6] = {0xbad0000u | where, a, b, c, d, 0u};
+            for (int i = 0; i < 6; ++i) wb.ctl[WF_SNAP + i] = v[i];
+        }
+    }
+}
+
+template <bool LDS, bool FAST_RCP>
+__global__ __launch_bounds__(kPkBlock) void k_wf_trace_pk(SceneView sc, WfBuffers wb, int in_q, int max_nodes) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;  // replay: per-lane stack (lane-minor)
+    char* wbase = smem + (uint32_t)sc.max_stack * blockDim.x * 4u + (threadIdx.x / 64u) * kPkLdsPerWave;
+    int* pnode = reinterpret_cast<int*>(wbase);                                  // [kPkStack] packet stack: node
+    uint64_t* pmask = reinterpret_cast<uint64_t*>(wbase + kPkStack * 4);         // [kPkStack] lane mask
+    int2* slot = reinterpret_cast<int2*>(wbase + kPkStack * 16) + lane_id();     // slot k: slot[64 k] = (uid, t)
+    if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
+    const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
+    const Node* gnodes = sc.nodes;  // global copies for the uniform s_loads of phase 1
+    const Tri* gtris = sc.tris;
+    if (LDS) stage_scene_lds(sc, smem + (uint32_t)sc.max_stack * blockDim.x * 4u + (blockDim.x / 64u) * kPkLdsPerWave);
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+    const uint32_t lane = lane_id();
+    const uint32_t nb = (count + 63) / 64;
+    const float4* q = in_q ? wb.shd.ray : wb.ext.ray;
+    for (uint32_t bt = w; bt < nb; bt += nwaves) {  // batches of 64 entries, interleaved over waves
+        const uint32_t e = bt * 64 + lane;
+        const bool valid = e < count;
+        uint32_t p;
+        const Ray r = unpack_ray(valid ? q[2 * (size_t)e] : make_float4(0, 0, 0, 1),
+                                 valid ? q[2 * (size_t)e + 1] : make_float4(0, 0, 0, 0), p);
+        // ---- phase 1: the packet walk
+        int nh = 0;
+        bool ovf = false;
+        uint64_t bloom = 0;  // bit (uid & 63) of every recorded uid
+        float tmin = 3.0e38f;
+        int sp = 0, visits = 0;
+        const uint64_t vm = __builtin_amdgcn_ballot_w64(valid);
+        if (lane == 0) { pnode[0] = 0; pmask[0] = vm; }
+        sp = vm ? 1 : 0;
+        bool gave_up = false;
+        while (sp > 0) {  // wave-uniform
+            if (visits > (int)kPkGuard) { pk_report(wb, 1, sp, visits, bt, count); return; }
+            --sp;
+            const int n = __builtin_amdgcn_readfirstlane(pnode[sp]);
+            const uint64_t m = pmask[sp];
+            if (++visits > max_nodes) { gave_up = true; break; }
+            float4 a, b, c;
+            int4 d;
+            load_node_scalar(gnodes, n, a, b, c, d);
+            const bool in = (m >> lane) & 1ull;
+            const float ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
+            const float rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
+            const uint64_t lm = __builtin_amdgcn_ballot_w64(in && 0.0f < ld), rm = __builtin_amdgcn_ballot_w64(in && 0.0f < rd);
+            for (int side = 0; side < 2; ++side) {  // uniform
+                const uint64_t cm = side ? rm : lm;
+                const int ref = side ? d.y : d.x, cnt = side ? d.w : d.z;
+                if (!cm) continue;
+                if (cnt < 0) {  // internal child: the lanes that enter it
+                    if (sp >= kPkStack) { pk_report(wb, 3, sp, visits, bt, count); return; }
+                    if (lane == 0) { pnode[sp] = ref; pmask[sp] = cm; }
+                    ++sp;
+                    continue;
+                }
+                const bool mine = (cm >> lane) & 1ull;
+                for (int k = 0; k < cnt; ++k) {  // the leaf for the lanes in cm
+                    const TriRec tr = load_tri_scalar(gtris, ref + k);
+                    const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
+                    const f3 rce2 = cross(r.d, e2);
+                    const float det = dot(e1, rce2);
+                    const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
+                    const f3 sv = r.o - v0;
+                    const float bu = inv_det * dot(sv, rce2);
+                    const bool ok_det = !(det > -1e-8f && det < 1e-8f), ok_lo = !(bu < 0.0f), ok_hi = !(bu > 1.0f);
+                    if ((cm & __builtin_amdgcn_ballot_w64(ok_det) & __builtin_amdgcn_ballot_w64(ok_lo) &
+                         __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
+                        continue;  // wave-uniform: no lane of the leaf passes det and u
+                    const f3 sce1 = cross(sv, e1);
+                    const float bv = inv_det * dot(r.d, sce1);
+                    const float t = inv_det * dot(e2, sce1);
+                    const bool h = mine & ok_det & ok_lo & ok_hi & !(bv < 0.0f) & !(bu + bv > 1.0f) & (t > 1e-8f);
+                    if (h) {
+                        const int uid = (int)sload_u32(reinterpret_cast<const uint32_t*>(&gtris[ref + k].uid));
+                        bool seen = false;
+                        if ((bloom >> (uid & 63)) & 1ull)
+                            for (int j = 0; j < min(nh, kPkSlots); ++j) seen |= slot[64 * j].x == uid;
+                        if (!seen) {
+                            if (nh < kPkSlots) slot[64 * nh] = make_int2(uid, __builtin_bit_cast(int, t));
+                            else ovf = true;
+                            ++nh;
+                            bloom |= 1ull << (uid & 63);
+                            tmin = t < tmin ? t : tmin;
+                        }
+                    }
+                }
+            }
+        }
+        // ---- phase 2: each lane's reference walk; leaf entries from phase 1 (or real tests when the
+        // packet gave up / the lane overflowed its slots)
+        const bool real = gave_up || ovf;
+        int best = -1;
+        float best_t = -1.0f;
+        bool go = valid && (real || nh > 0);
+        int node = 0, rsp = 0;
+        for (uint32_t guard = 0; wave_any(go); ++guard) {
+            if (guard > kPkGuard) { pk_report(wb, 2, guard, (uint32_t)node, bt, count); return; }
+            if (go) {
+                const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * node;
+                const float4 a = np[0], b = np[1], c = np[2];
+                const int4 d = reinterpret_cast<const int4*>(np)[3];
+                const float ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
+                const float rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
+                const bool li = 0.0f < ld, ri = 0.0f < rd;
+                const bool lleaf = d.z >= 0, rleaf = d.w >= 0;
+                const int na = (li && lleaf) ? d.z : 0, nt = na + ((ri && rleaf) ? d.w : 0);
+                for (int k = 0; k < nt; ++k) {  // the leaf pair in the reference's order
+                    const int idx = k < na ? d.x + k : d.y + (k - na);
+                    float t = 0.0f;
+                    bool hit = false;
+                    if (real) {
+                        hit = tri_hit<FAST_RCP>(sc.tris, idx, r, t);
+                    } else {
+                        const int uid = sc.tris[idx].uid;
+                        if ((bloom >> (uid & 63)) & 1ull)
+                            for (int j = 0; j < nh; ++j) {
+                                const int2 sl = slot[64 * j];
+                                if (sl.x == uid) { hit = true; t = __builtin_bit_cast(float, sl.y); }
+                            }
+                    }
+                    if (hit && (best_t < 0.0f || t < best_t)) { best_t = t; best = idx; }
+                }
+                if (!real && best_t == tmin) {
+                    go = false;  // final: no later entry has a smaller t
+                } else {
+                    const bool tl = li && !lleaf && !(best_t > 0.0f && ld > best_t);
+                    const bool tr = ri && !rleaf && !(best_t > 0.0f && rd > best_t);
+                    if (tl && tr) {
+                        stack[rsp * blockDim.x] = d.x;
+                        ++rsp;
+                        node = d.y;
+                    } else if (tl) {
+                        node = d.x;
+                    } else if (tr) {
+                        node = d.y;
+                    } else if (rsp == 0) {
+                        go = false;
+                    } else {
+                        --rsp;
+                        node = stack[rsp * blockDim.x];
+                    }
+                }
+            }
+        }
+        if (valid) wb.hitq[e] = make_int2(best, __builtin_bit_cast(int, best_t));
+    }
+}
+
 // One batch of 64 entries of queue `in` (EXT: extension rays, else shadow rays) at entries
 // rbase + b * 64 + lane (valid: b * 64 + lane < count): bf_closest, then the path logic of
 // k_wf_shade (pt_path.h, so the same bits) in the same wave — the hit never goes through HBM
@@ -774,12 +1005,12 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     if (fresh) {
         if (valid) {
             uint32_t x, y, f;
-            path_pixel(pg, fp.width * fp.height, fp.width, x, y, f);
+            const uint32_t pid = slot_path(pg, fp, x, y, f);  // pg: the generation slot
             const uint32_t tt = gen.raw_salt ? gen.frame0 : (uint32_t)(float)(gen.frame0 + (gen.fbase + f) * gen.stride);
             PathState g;
             const Ray gr = path_begin(fp, x, y, tt, g);
             a0 = make_float4(gr.o.x, gr.o.y, gr.o.z, gr.d.x);
-            a1 = make_float4(gr.d.y, gr.d.z, __builtin_bit_cast(float, pg), __builtin_bit_cast(float, pack_dspec(g)));
+            a1 = make_float4(gr.d.y, gr.d.z, __builtin_bit_cast(float, pid), __builtin_bit_cast(float, pack_dspec(g)));
             c2 = make_float4(g.L.x, g.L.y, g.L.z, __builtin_bit_cast(float, g.seed));
             d3 = make_float4(g.beta.x, g.beta.y, g.beta.z, 0.0f);
             if (COUNT) { c.samples++; c.ext_queries++; }
@@ -1006,16 +1237,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_persist_bf(SceneView sc, Fra
     if (LDS) stage_scene_lds(sc, l.scene);
     Counters c = {};
     const uint32_t wv = threadIdx.x / 64, nwv = blockDim.x / 64;
-    const uint32_t npix = fp.width * fp.height;
     for (uint32_t k = wv; k < nmine; k += nwv) {  // camera rays: local batch k = global batch rg + k R
         const uint32_t p = (rg + k * R) * 64 + lane;
         if (p < P) {
             uint32_t x, y, f;
-            path_pixel(p, npix, fp.width, x, y, f);
+            const uint32_t pid = slot_path(p, fp, x, y, f);
             const uint32_t t = raw_salt ? frame0 : (uint32_t)(float)(frame0 + (fbase + f) * stride);
             PathState ps;
             const Ray r = path_begin(fp, x, y, t, ps);
-            store_entry(wb.ext, (uint32_t)(rbase + k * 64 + lane), r, p, ps);
+            store_entry(wb.ext, (uint32_t)(rbase + k * 64 + lane), r, pid, ps);
             if (COUNT) { c.samples++; c.ext_queries++; }
         }
     }
@@ -1444,6 +1674,24 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     const uint32_t F = np * std::max<uint32_t>(1, std::min<uint32_t>((nframes + np - 1) / np, (uint32_t)(wb.capacity / np / npix)));
     const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc);
     int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
+    // k_wf_trace_pk (option packet): its LDS (per-lane replay stacks, per-wave packet stack and hit
+    // slots, the scene when it fits) and an occupancy-derived grid
+    const size_t pk_lds = (size_t)sc.max_stack * kPkBlock * 4 + (kPkBlock / 64) * kPkLdsPerWave + (LDS ? sc.span_bytes : 0);
+    const bool pk_ok = pk_lds <= 64 * 1024;  // a workgroup's LDS limit; else the traversal kernel runs
+    auto pk_blocks = [&](size_t bytes) {
+        static int cached = 0;
+        static size_t cached_bytes = 0;
+        if (!cached || cached_bytes != bytes) {
+            int per_cu = 0, dev = 0, cus = 0;
+            hipGetDevice(&dev);
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_wf_trace_pk<LDS, ((TRAV / 10) & 1) != 0>,
+                                                         kPkBlock, bytes);
+            cached = std::max(1, per_cu) * std::max(1, cus);
+            cached_bytes = bytes;
+        }
+        return ws.trace_blocks > 0 ? std::min(cached, ws.trace_blocks) : cached;
+    };
     if (ws.trace_blocks > 0) tblocks = std::min(tblocks, ws.trace_blocks);  // option wf_trace_blocks (tests)
     const int iters = 2 * (fp.max_depth + 1);
     // option trace_watchdog: tests of the failure report
@@ -1540,6 +1788,9 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 } else if constexpr (TRAV >= 300)
                     PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
                               dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
+                else if (!COUNT && pk_ok && pk_launch(ws.packet, it))  // packet walk + replay (option packet)
+                    PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_pk<LDS, ((TRAV / 10) & 1) != 0>), dim3(pk_blocks(pk_lds)),
+                              dim3(kPkBlock), pk_lds, st, sc, w, in_q, ws.packet_nodes > 0 ? ws.packet_nodes : kPkMaxNodes);
                 else
                     PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc,
                               w, in_q, cnt, watchdog, trace_dyn);
@@ -1552,6 +1803,9 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                               fp, w, cnt, ws.sort_bins);
             }
             in_q ^= 1;
+            // a launch that cannot run (e.g. a configuration error) fails here, after the first
+            // iteration, instead of leaving the later launches to read counts it never wrote
+            if (it == 0) HIP_RETURN_IF(hipGetLastError());
         }
         if (np > 1) {
             for (int h = 0; h < nh; ++h) {
@@ -1585,6 +1839,8 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.trace_dyn = lo.trace_dyn;
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
+    ws.packet = lo.packet > 0 ? lo.packet : 0;
+    ws.packet_nodes = lo.packet_nodes;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     // turn policy of the lean16 traversal: 4 since the queues are grouped by coherence keys (in

@@ -93,7 +93,9 @@ function merge_groups(groups) {
     for (const g of groups) {
         const base = out.vertices.length / 3;
         const nv = g.vertices.length / 3;
-        out.vertices.push(...g.vertices);
+        // an index loop, not push(...g.vertices): spreading a large mesh as call arguments exceeds
+        // V8's argument limit (RangeError)
+        for (let i = 0; i < g.vertices.length; i++) out.vertices.push(g.vertices[i]);
         for (let i = 0; i < 3 * nv; i++) out.vertex_normals.push(i < g.vertex_normals.length ? g.vertex_normals[i] : 0);
         for (const o of g.objects) out.objects.push(Object.assign({}, o, { indices: o.indices.map((v) => v + base) }));
     }

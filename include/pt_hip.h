@@ -148,8 +148,9 @@ int pt_set_hw_queues(int n);
  *   "kernel"        auto | mega | wavefront | literal    pipeline (auto = PT_MODE_* and the scene)
  *   "trav"          nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32   traversal flavour
  *   "lds" "fastrcp" "pipe" "ifif" "dual" "stagger" "fuse" "fuse_gen" "bf" "mailbox" "persist"
- *   "regen" "regen_bf" "bf_stackless" "trace_dyn" "packet"                  0 | 1 switches
- *   "parts" "cull" "sort" "node_bias" "big_leaf" "bf_slots" "wf_paths" "wf_trace_blocks"
+ *   "regen" "regen_bf" "bf_stackless" "trace_dyn" "tiles"                   0 | 1 switches
+ *   "parts" "cull" "sort" "node_bias" "big_leaf" "bf_slots" "wf_paths" "wf_trace_blocks" "packet"
+ *   "packet_nodes"
  *   "regen_target" "trace_watchdog"                                         integers
  *   "mb_uid_order"  forward | reverse   (read by pt_scene_create: uid numbering of mailbox scenes)
  *   "reduce"        rccl | ordered      (pt_render_multi's reduction)

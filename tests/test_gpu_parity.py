@@ -89,6 +89,18 @@ KERNELS = {
     "mega_bf_stack_replay": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1", "PT_BF_STACKLESS": "0"},
     # traversal pipeline: survivors grouped by 8 / 64 / 512 coherence keys per shade block (queue order only; 512 is the default)
     "wavefront_sort8": {"PT_KERNEL": "wavefront", "PT_SORT": "8"},
+    # camera paths generated in 8x8 pixel tiles (slot_path): every generator, both pipelines
+    "wavefront_tiles": {"PT_KERNEL": "wavefront", "PT_TILES": "1"},
+    "wavefront_tiles_nogen": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_FUSE_GEN": "0"},
+    "wavefront_tiles_persist": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_PERSIST": "1"},
+    "wavefront_tiles_trav": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_MAILBOX": "0"},
+    # packet walk + replay (k_wf_trace_pk): camera launches, camera + shadow, every launch; with a
+    # node budget so small that every packet gives up (the real-test replay), and on one block
+    "wavefront_packet1": {"PT_KERNEL": "wavefront", "PT_PACKET": "1", "PT_MAILBOX": "0"},
+    "wavefront_packet2": {"PT_KERNEL": "wavefront", "PT_PACKET": "2", "PT_MAILBOX": "0"},
+    "wavefront_packet3_div": {"PT_KERNEL": "wavefront", "PT_PACKET": "3", "PT_MAILBOX": "0", "PT_FASTRCP": "0"},
+    "wavefront_packet3_1block": {"PT_KERNEL": "wavefront", "PT_PACKET": "3", "PT_MAILBOX": "0", "PT_WF_TRACE_BLOCKS": "1"},
+    "wavefront_packet3_giveup": {"PT_KERNEL": "wavefront", "PT_PACKET": "3", "PT_MAILBOX": "0", "PT_PACKET_NODES": "1"},
     # traversal kernel with windows from group counters (PT_TRACE_DYN=1), also on a 1-block grid
     "wavefront_trace_dyn": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_MAILBOX": "0"},
     "wavefront_trace_dyn_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_WF_TRACE_BLOCKS": "1"},

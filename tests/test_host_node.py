@@ -227,3 +227,15 @@ def test_multi_mesh_buffers_match_oracle(tmp_path):
     # the merged scene holds both meshes: 72 + 15222 vertices, 36 + 12573 triangles
     tri = multi.triangle_data
     assert int(tri[0]) == 72 + 15222 and (int(tri[4]) - int(tri[3])) // 4 == 36 + 12573
+
+
+def test_merge_groups_large_mesh():
+    """--all-meshes merge of a mesh far above V8's call-argument limit (no RangeError from a spread)."""
+    r = node_eval('''
+const scene = require(require('path').join(''' + json.dumps(NODE_DIR) + ''', 'lib', 'scene'));
+const n = 600000;
+const big = { vertices: new Array(3 * n).fill(0.5), vertex_normals: [], objects: [{ indices: [1, 2, 3] }] };
+const small = { vertices: [0, 0, 0, 1, 0, 0, 0, 1, 0], vertex_normals: [], objects: [{ indices: [1, 2, 3] }] };
+const m = scene.merge_groups([big, small]);
+console.log(JSON.stringify({ nv: m.vertices.length, last: m.objects[1].indices }));''')
+    assert r["nv"] == 3 * 600000 + 9 and r["last"] == [600001, 600002, 600003]
