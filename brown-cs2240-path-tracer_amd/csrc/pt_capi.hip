@@ -322,7 +322,7 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                 L.cull[3 * (size_t)u + 1] = make_float4(upf(hi[0]), upf(hi[1]), upf(hi[2]), 4e-3f);
                 L.cull[3 * (size_t)u + 2] = make_float4((float)n[0], (float)n[1], (float)n[2], upf(2.0 * lv + l1 + l2));
             }
-            L.bfpair.assign(20 * (size_t)((U + 1) / 2), 0.0f);
+            L.bfpair.assign(40 * (size_t)((U + 3) / 4), 0.0f);  // whole quads of entries (bf_quads); zero entries never hit
             for (int32_t u = 0; u < U; ++u) {
                 const Tri& t = L.tris[(size_t)(L.mb_base + u)];
                 const float c[9] = {t.q0[0], t.q0[1], t.q0[2], t.q0[3], t.q1[0], t.q1[1], t.q1[2], t.q1[3], t.e2z};

@@ -386,7 +386,7 @@ constexpr int kBfSlots = 8;
 #define PT_BF_PACKED 0
 #endif
 constexpr bool kBfPacked = PT_BF_PACKED != 0;  // (k_regen_bf, itself opt-in, uses bf_pairs: tests cover it)
-constexpr bool kBfPackedShadow = PT_BF_PACKED >= 2;  // the shadow instances too
+constexpr bool kBfPackedShadow = PT_BF_PACKED == 2 || PT_BF_PACKED >= 4;  // the shadow instances too (3: bf_quads, extension only; 4: both)
 // Diagnostic build only (EXTRA=-DPT_PHASE_TIMING=1, scripts/phase_timing.py): shader-clock
 // cycles per phase of bf_step_batch, summed per wave slot (8 phases x {extension, shadow}).
 #ifndef PT_PHASE_TIMING
@@ -544,6 +544,69 @@ __device__ __forceinline__ void bf_pairs(const SceneView& sc, const Ray& r, bool
     }
 }
 
+// bf_pairs two pairs at a time (PT_BF_PACKED=3 builds): the two pairs' det/u parts are
+// independent, so their packed instructions interleave and hide each other's latency (one pair's
+// chain alone stalls: PMC of PT_BF_PACKED=1, WAIT_INST_ANY +27 %).  Hits are recorded in entry order.
+template <bool FAST_RCP>
+__device__ __forceinline__ void bf_quads(const SceneView& sc, const Ray& r, bool valid, float* slot, int nslots,
+                                         uint64_t& hits, int& nh, float& tmin) {
+    const int NQ = (sc.n_tris - sc.mb_base + 3) >> 2;  // bfpair holds a whole number of quads (host)
+    const uint64_t vmask = __builtin_amdgcn_ballot_w64(valid);
+    const fv2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
+    for (int j = 0; j < NQ; ++j) {
+        fv2 bu[2], det[2], inv[2], sx[2], sy[2], sz[2];
+        const __attribute__((address_space(4))) float* f0 = (const __attribute__((address_space(4))) float*)(sc.bfpair + 40 * j);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const __attribute__((address_space(4))) float* f = f0 + 20 * h;
+            const fv2 v0x = {f[0], f[1]}, v0y = {f[2], f[3]}, v0z = {f[4], f[5]};
+            const fv2 e1x = {f[6], f[7]}, e1y = {f[8], f[9]}, e1z = {f[10], f[11]};
+            const fv2 e2x = {f[12], f[13]}, e2y = {f[14], f[15]}, e2z = {f[16], f[17]};
+            const fv2 rx = fma2(dy, e2z, -(dz * e2y)), ry = fma2(dz, e2x, -(dx * e2z)), rz = fma2(dx, e2y, -(dy * e2x));
+            det[h] = fma2(e1z, rz, fma2(e1y, ry, e1x * rx));
+            if (FAST_RCP) {
+                const fv2 y = {__builtin_amdgcn_rcpf(det[h].x), __builtin_amdgcn_rcpf(det[h].y)};
+                inv[h] = fma2(fma2(-det[h], y, sp2(1.0f)), y, y);
+            } else {
+                inv[h] = fv2{1.0f / det[h].x, 1.0f / det[h].y};
+            }
+            sx[h] = sp2(r.o.x) - v0x; sy[h] = sp2(r.o.y) - v0y; sz[h] = sp2(r.o.z) - v0z;
+            bu[h] = inv[h] * fma2(sz[h], rz, fma2(sy[h], ry, sx[h] * rx));
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const bool d0 = !(det[h].x > -1e-8f && det[h].x < 1e-8f), l0 = !(bu[h].x < 0.0f), g0 = !(bu[h].x > 1.0f);
+            const bool d1 = !(det[h].y > -1e-8f && det[h].y < 1e-8f), l1 = !(bu[h].y < 0.0f), g1 = !(bu[h].y > 1.0f);
+            const uint64_t any0 = __builtin_amdgcn_ballot_w64(d0) & __builtin_amdgcn_ballot_w64(l0) & __builtin_amdgcn_ballot_w64(g0);
+            const uint64_t any1 = __builtin_amdgcn_ballot_w64(d1) & __builtin_amdgcn_ballot_w64(l1) & __builtin_amdgcn_ballot_w64(g1);
+            if ((vmask & (any0 | any1)) == 0) continue;  // wave-uniform
+            const bool ok0 = valid & d0 & l0 & g0, ok1 = valid & d1 & l1 & g1;
+            const __attribute__((address_space(4))) float* f = f0 + 20 * h;
+            const fv2 e1x = {f[6], f[7]}, e1y = {f[8], f[9]}, e1z = {f[10], f[11]};
+            const fv2 e2x = {f[12], f[13]}, e2y = {f[14], f[15]}, e2z = {f[16], f[17]};
+            const fv2 cx = fma2(sy[h], e1z, -(sz[h] * e1y)), cy = fma2(sz[h], e1x, -(sx[h] * e1z)),
+                      cz = fma2(sx[h], e1y, -(sy[h] * e1x));
+            const fv2 bv = inv[h] * fma2(dz, cz, fma2(dy, cy, dx * cx));
+            const fv2 t = inv[h] * fma2(e2z, cz, fma2(e2y, cy, e2x * cx));
+            const bool h0 = ok0 & !(bv.x < 0.0f) & !(bu[h].x + bv.x > 1.0f) & (t.x > 1e-8f);
+            const bool h1 = ok1 & !(bv.y < 0.0f) & !(bu[h].y + bv.y > 1.0f) & (t.y > 1e-8f);
+            const int u = 4 * j + 2 * h;
+            if (h0) {
+                if (nh < nslots) slot[64 * nh] = t.x;
+                ++nh;
+                hits |= 1ull << u;
+                tmin = t.x < tmin ? t.x : tmin;
+            }
+            if (h1) {
+                if (nh < nslots) slot[64 * nh] = t.y;
+                ++nh;
+                hits |= 1ull << (u + 1);
+                tmin = t.y < tmin ? t.y : tmin;
+            }
+        }
+    }
+}
+
 // Phase 2 without a stack (SceneView::bfnode; scenes of <= 64 internal nodes, <= 63 entries).
 // The reference's traversal visits nodes depth first, right child before left (a node with both
 // children to visit keeps the left one on its stack), and a child's visit is decided when its
@@ -629,8 +692,9 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     int nh = 0;
     const uint64_t vmask = __builtin_amdgcn_ballot_w64(valid);  // loop-invariant part of phase 1's vote
     float tmin = 3.0e38f;  // smallest t of any entry this ray hits
-    if (PK && todo == ~0ull) {  // every entry: in pairs, packed f32 (bf_pairs)
-        bf_pairs<FAST_RCP>(sc, r, valid, slot, nslots, hits, nh, tmin);
+    if (PK && todo == ~0ull) {  // every entry: in pairs, packed f32 (bf_pairs; two pairs at a time: bf_quads)
+        if (PT_BF_PACKED >= 3) bf_quads<FAST_RCP>(sc, r, valid, slot, nslots, hits, nh, tmin);
+        else bf_pairs<FAST_RCP>(sc, r, valid, slot, nslots, hits, nh, tmin);
         todo = 0;
     }
     // one entry of phase 1 against the wave's 64 rays
