@@ -201,7 +201,74 @@ __global__ __launch_bounds__(256) void k_selftest_valu_pk(int iters, float seed,
     if (s == -1.0f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// mixed: 4 packed chains and 8 plain chains interleaved (the issue rate of a mix of the two kinds;
+// per loop iteration 16 v_pk_fma_f32 + 32 v_fma_f32 = 48 wave-instructions)
+__global__ __launch_bounds__(256) void k_selftest_valu_mix(int iters, float seed, float m, float c, float* out) {
+    fv2s a[4];
+    float b[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = fv2s{seed + (float)(threadIdx.x + k), seed - (float)(threadIdx.x + k)};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = seed * (float)(threadIdx.x + k);
+    const fv2s mm = {m, m}, cc = {c, c};
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a[k] = __builtin_elementwise_fma(a[k], mm, cc);
+                b[2 * k] = fmaf(b[2 * k], m, c);
+                b[2 * k + 1] = fmaf(b[2 * k + 1], m, c);
+            }
+        }
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += a[k].x + a[k].y;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += b[k];
+    if (s == -1.0f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// dependent chains: 2 packed (mode 3) or 2 plain (mode 4) chains per thread, 32 instructions per
+// iteration — the issue rate when each wave's next instruction depends on its last but one
+__global__ __launch_bounds__(256) void k_selftest_valu_dep(int iters, int pk, float seed, float m, float c, float* out) {
+    float s = 0.0f;
+    if (pk) {
+        fv2s a0 = {seed + threadIdx.x, seed - threadIdx.x}, a1 = {seed * 2.0f, seed * 3.0f};
+        const fv2s mm = {m, m}, cc = {c, c};
+        for (int i = 0; i < iters; ++i) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                a0 = __builtin_elementwise_fma(a0, mm, cc);
+                a1 = __builtin_elementwise_fma(a1, mm, cc);
+            }
+        }
+        s = a0.x + a0.y + a1.x + a1.y;
+    } else {
+        float a0 = seed + threadIdx.x, a1 = seed * 2.0f;
+        for (int i = 0; i < iters; ++i) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                a0 = fmaf(a0, m, c);
+                a1 = fmaf(a1, m, c);
+            }
+        }
+        s = a0 + a1;
+    }
+    if (s == -1.0f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, hipStream_t stream) {
+    if (packed == 3 || packed == 4) {
+        hipLaunchKernelGGL(k_selftest_valu_dep, dim3(blocks), dim3(256), 0, stream, iters, packed == 3 ? 1 : 0, 1.0f,
+                           0.99999994f, 1.0e-7f, out);
+        return hipGetLastError();
+    }
+    if (packed == 2) {  // 48 instructions per iteration: scale iters so the count below holds (x 32 per iteration)
+        hipLaunchKernelGGL(k_selftest_valu_mix, dim3(blocks), dim3(256), 0, stream, iters * 2 / 3, 1.0f, 0.99999994f, 1.0e-7f, out);
+        return hipGetLastError();
+    }
     // m, c as arguments: the FMAs read them from SGPRs (no literal-constant encodings in the loop)
     if (packed)
         hipLaunchKernelGGL(k_selftest_valu_pk, dim3(blocks), dim3(256), 0, stream, iters, 1.0f, 0.99999994f, 1.0e-7f, out);

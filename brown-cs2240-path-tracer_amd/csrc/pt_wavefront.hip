@@ -382,6 +382,9 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
 constexpr int kBfSlots = 8;
 // phase 1 in entry pairs with packed f32 (bf_pairs): bit-exact, measured no faster (fused kernel,
 // extension rays only: 2598 vs 2607 Msamples/s; both queues: 2446, VGPR spills in the shadow instance)
+#ifndef PT_BF_LDSREC
+#define PT_BF_LDSREC 0
+#endif
 #ifndef PT_BF_PACKED
 #define PT_BF_PACKED 0
 #endif
@@ -737,7 +740,10 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
                 entry(u, tr);
             }
         } else {
-            for (int u = 0; u < U; ++u) entry(u, load_tri_scalar(gtris, sc.mb_base + u));
+            // PT_BF_LDSREC builds (A/B): the record read from the scene's copy (LDS when staged) by
+            // every lane at one address (a broadcast ds_read) instead of through the scalar cache
+            if (PT_BF_LDSREC) for (int u = 0; u < U; ++u) entry(u, load_tri(sc.tris, sc.mb_base + u));
+            else for (int u = 0; u < U; ++u) entry(u, load_tri_scalar(gtris, sc.mb_base + u));
         }
     } else {
         todo &= U >= 64 ? ~0ull : (1ull << U) - 1;  // wave-uniform

@@ -375,11 +375,12 @@ def selftest_rcp(steps: int = -1, lo_bits: int = 0x00800000, hi_bits: int = 0x7E
     return int(m.value), int(b.value)
 
 
-def selftest_valu(iters: int = 20000, reps: int = 5, packed: bool = False, device: int = 0):
-    """pt_selftest_valu: (ms of the timed launches, FMA wave-instructions they issued; packed: v_pk_fma_f32)."""
+def selftest_valu(iters: int = 20000, reps: int = 5, packed: int = 0, device: int = 0):
+    """pt_selftest_valu: (ms of the timed launches, FMA wave-instructions they issued; packed 1:
+    v_pk_fma_f32, 2: packed and plain chains interleaved)."""
     ms = ctypes.c_double(0.0)
     n = ctypes.c_uint64(0)
-    _check(load_library().pt_selftest_valu(device, iters, reps, 1 if packed else 0, ctypes.byref(ms), ctypes.byref(n)))
+    _check(load_library().pt_selftest_valu(device, iters, reps, int(packed), ctypes.byref(ms), ctypes.byref(n)))
     return float(ms.value), int(n.value)
 
 

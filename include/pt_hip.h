@@ -248,7 +248,8 @@ int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, u
                     uint32_t* failing_bits);
 
 /* VALU issue calibration: `reps` timed launches (after one untimed) of a kernel whose threads run 8
- * independent v_fma_f32 chains (packed != 0: v_pk_fma_f32, two FMAs per lane each; 32 instructions
+ * independent v_fma_f32 chains (packed 1: v_pk_fma_f32, two FMAs per lane each; 2: packed and plain
+ * chains interleaved 1 : 2; 32 instructions
  * per iteration, `iters` iterations, no memory operation) at 8 waves per SIMD — the SIMDs issue VALU
  * at their peak rate.  *ms_out = the timed launches' event time; *fma_wave_instr_out (nullable) =
  * their FMA wave-instructions.  Profiled with rocprofv3 PMC it pins the counter formula for the

@@ -31,13 +31,18 @@ def run(argv):
     ap.add_argument("--iters", type=int, default=20000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--packed", action="store_true", help="v_pk_fma_f32 chains (two FMAs per lane each)")
+    ap.add_argument("--mixed", action="store_true", help="packed and plain chains interleaved (1 : 2)")
+    ap.add_argument("--dep", choices=["packed", "plain"], help="two dependent chains per thread")
     a = ap.parse_args(argv)
     import pt_amd
-    ms, n = pt_amd.selftest_valu(a.iters, a.reps, a.packed)
+    mode = 2 if a.mixed else (3 if a.dep == "packed" else 4) if a.dep else int(a.packed)
+    ms, n = pt_amd.selftest_valu(a.iters, a.reps, mode)
     cus = 256
     # achieved rate: 2 flops per lane per FMA (x2 packed), 64 lanes per wave-instruction
-    tflops = n * 64 * 2 * (2 if a.packed else 1) / (ms * 1e-3) / 1e12
-    print(json.dumps({"kernel": "k_selftest_valu" + ("_pk" if a.packed else ""), "iters": a.iters, "reps": a.reps, "ms": ms,
+    flops_per_instr = 4 / 3 if a.mixed else 2 if (a.packed or a.dep == "packed") else 1
+    tflops = n * 64 * 2 * flops_per_instr / (ms * 1e-3) / 1e12
+    name = "k_selftest_valu" + ("_mix" if a.mixed else ("_dep_" + a.dep) if a.dep else "_pk" if a.packed else "")
+    print(json.dumps({"kernel": name, "iters": a.iters, "reps": a.reps, "ms": ms,
                       "fma_wave_instr": n, "fma_wave_instr_per_launch": n // a.reps, "tflops_f32": round(tflops, 2),
                       "wave_instr_per_simd_per_ns": n / (cus * 4) / (ms * 1e6)}), flush=True)
 

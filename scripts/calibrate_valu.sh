@@ -9,6 +9,9 @@ OUT=gpurun_out/valucal
 rm -rf $OUT; mkdir -p $OUT gpurun_out/profiles
 timeout -k 10 120 python3 scripts/calibrate_valu.py run --iters 20000 --reps 3 > $OUT/plain.log 2>&1 || exit $?
 timeout -k 10 120 python3 scripts/calibrate_valu.py run --iters 20000 --reps 3 --packed >> $OUT/plain.log 2>&1 || exit $?
+timeout -k 10 120 python3 scripts/calibrate_valu.py run --iters 20000 --reps 3 --mixed >> $OUT/plain.log 2>&1 || exit $?
+timeout -k 10 120 python3 scripts/calibrate_valu.py run --iters 20000 --reps 3 --dep packed >> $OUT/plain.log 2>&1 || exit $?
+timeout -k 10 120 python3 scripts/calibrate_valu.py run --iters 20000 --reps 3 --dep plain >> $OUT/plain.log 2>&1 || exit $?
 cat $OUT/plain.log | grep '^{'
 timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
   --output-format csv -d $OUT/pmc -o run -- python3 scripts/calibrate_valu.py run --iters 20000 --reps 3 > $OUT/pmc.log 2>&1 || exit $?
