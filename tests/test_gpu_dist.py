@@ -42,6 +42,7 @@ def _worker(rank, world, port, tri, bvh, meta, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.timeout(240, method="thread")
 def test_two_ranks_hip_render_gloo_reduce(packed, tmp_path):
     import torch.multiprocessing as mp
 

@@ -83,6 +83,7 @@ def test_rccl_mode_rejects_repeated_devices(packed, env):
             s.close()
 
 
+@pytest.mark.timeout(240, method="thread")  # a stuck collective ends the run with its stacks, not a hang
 @pytest.mark.parametrize("ndev", [2, 8])
 def test_rccl_reduce_distinct_devices_vs_oracle(packed, env, ndev):
     """The RCCL branch of pt_render_multi (ncclCommInitAll + ONE ncclReduce): the same partials as
