@@ -17,6 +17,7 @@
 
 #include "../../include/pt_hip.h"
 #include "pt_kernels.h"
+#include "pt_leafbvh.h"
 
 using namespace pt;
 
@@ -73,11 +74,14 @@ constexpr OptSpec kOptSpecs[] = {
     {"fuse", OPT_BOOL, nullptr},         {"fuse_gen", OPT_BOOL, nullptr},    {"bf", OPT_BOOL, nullptr},
     {"mailbox", OPT_BOOL, nullptr},      {"persist", OPT_BOOL, nullptr},     {"regen", OPT_BOOL, nullptr},
     {"regen_bf", OPT_BOOL, nullptr},     {"bf_stackless", OPT_BOOL, nullptr}, {"trace_dyn", OPT_BOOL, nullptr},
-    {"tiles", OPT_BOOL, nullptr},        {"packet", OPT_INT, nullptr},       {"packet_nodes", OPT_INT, nullptr},
+    {"trace_sparse", OPT_INT, nullptr},
+    {"tiles", OPT_BOOL, nullptr},        {"batch_pipe", OPT_BOOL, nullptr},
+    {"packet", OPT_INT, nullptr},       {"packet_nodes", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"cull", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr},
     {"regen_target", OPT_INT, nullptr},  {"trace_watchdog", OPT_INT, nullptr},
+    {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
     {"reduce", OPT_ENUM, "rccl|ordered"},
 };
@@ -130,6 +134,12 @@ Opts opts_snapshot() {
     return o;
 }
 
+// leaves of at least this many entries get a leaf BVH (option leaf_bvh, read by pt_scene_create).
+// Off by default: exact (tests/test_gpu_leafbvh.py), but on the boat the walk is 5.5x slower than
+// the cooperative big-leaf turn (the skip rule needs a bound on |cos(ray, normal)|
+// over a node, and the boat's low-poly geometry leaves ~1200 wide-cone nodes open per ray)
+constexpr long kLeafBvhDefault = 0;
+
 struct HostLayout {
     std::vector<Node> nodes;
     std::vector<Tri> tris;
@@ -141,6 +151,10 @@ struct HostLayout {
     std::vector<float> bfpair;    // mailbox scenes: 20 per pair of distinct entries (SceneView::bfpair)
     std::vector<BfNode> bfnode;   // mailbox scenes with <= 64 internal nodes, <= 63 entries (SceneView::bfnode)
     std::vector<int32_t> bfmap;
+    std::vector<LNode> lnodes;    // leaf BVHs (SceneView::lnodes), and per such leaf (first record, entries, nodes)
+    std::vector<int32_t> lidx;
+    std::vector<std::array<int32_t, 3>> lleaves;
+    int32_t leaf_min = 0;         // leaves of at least this many entries have one (option leaf_bvh; 0: none)
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -358,6 +372,26 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             }
         }
     }
+    // Leaf BVHs (pt_leafbvh.cpp): every leaf of at least leaf_bvh entries (option, read here;
+    // default kLeafBvhDefault, 0 = none).  The leaf's first record holds root + 1, its second the
+    // end of its nodes (Tri::lbvh).  The lean traversal's big-leaf step walks them (mailbox scenes:
+    // only with option mailbox=0, their default kernels test every entry once per ray anyway).
+    {
+        const long lmin = opts_snapshot().num("leaf_bvh", kLeafBvhDefault);
+        if (lmin >= 2) {
+            L.leaf_min = (int32_t)std::min<long>(lmin, INT32_MAX);
+            std::sort(leaf_ranges.begin(), leaf_ranges.end());
+            for (const auto& lr : leaf_ranges) {
+                if (lr.second < L.leaf_min || L.lidx.size() + (size_t)lr.second >= (1u << 24)) continue;
+                int32_t root = 0, end = 0;
+                build_leaf_bvh(L.tris.data(), lr.first, lr.second, L.lnodes, L.lidx, root, end);
+                L.tris[(size_t)lr.first].lbvh = root + 1;
+                L.tris[(size_t)lr.first + 1].lbvh = end;
+                L.lleaves.push_back({lr.first, lr.second, end - root});
+            }
+            if (L.lleaves.empty()) L.leaf_min = 0;
+        }
+    }
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
     // a reflection/refraction of unit vectors; non-finite ones give no hit on either path)
     double emax = 0.0;
@@ -468,6 +502,8 @@ struct pt_scene {
     uint64_t rad_cap = 0;
     float* d_peer = nullptr;  // pt_render_multi (ordered reduction): another device's partial accumulator
     size_t peer_cap = 0;
+    int32_t leaf_min = 0;  // leaf BVHs: leaves of at least this many entries have one (0: none)
+    std::vector<std::array<int32_t, 3>> lleaves;  // (first record, entries, nodes) per leaf BVH
 };
 
 // Set once any call of this library has touched the HIP runtime (pt_set_hw_queues is then too late).
@@ -620,7 +656,9 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
     const size_t o_cull = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     const size_t o_pair = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
-    const size_t total = align_up(o_pair + std::max<size_t>(1, L.bfpair.size()) * sizeof(float), 256);
+    const size_t o_lnode = align_up(o_pair + std::max<size_t>(1, L.bfpair.size()) * sizeof(float), 256);
+    const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
+    const size_t total = align_up(o_lidx + std::max<size_t>(1, L.lidx.size()) * sizeof(int32_t), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -635,7 +673,9 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_bfmap, L.bfmap.data(), L.bfmap.size() * sizeof(int32_t)) != hipSuccess ||
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess ||
-        up(o_pair, L.bfpair.data(), L.bfpair.size() * sizeof(float)) != hipSuccess) {
+        up(o_pair, L.bfpair.data(), L.bfpair.size() * sizeof(float)) != hipSuccess ||
+        up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
+        up(o_lidx, L.lidx.data(), L.lidx.size() * sizeof(int32_t)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -663,6 +703,10 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.cull = reinterpret_cast<const float4*>(base + o_cull);
     s->view.cull_its = 0;  // per launch (launch_wavefront)
     s->view.bfpair = reinterpret_cast<const float*>(base + o_pair);
+    s->view.lnodes = L.lnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_lnode);
+    s->view.lidx = L.lnodes.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_lidx);
+    s->leaf_min = L.leaf_min;
+    s->lleaves = L.lleaves;
     s->view.mb_base = L.mb_base;
     s->view.bfnode = L.bfnode.empty() ? nullptr : reinterpret_cast<const BfNode*>(base + o_bfnode);
     s->view.bfmap = L.bfmap.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_bfmap);
@@ -686,8 +730,10 @@ void pt_scene_destroy(pt_scene* s) {
         if (s->ws.aux[h]) { hipStreamSynchronize(s->ws.aux[h]); hipStreamDestroy(s->ws.aux[h]); }
         if (s->ws.join[h]) hipEventDestroy(s->ws.join[h]);
         if (h < 2 && s->ws.traced[h]) hipEventDestroy(s->ws.traced[h]);
+        if (h < 2 && s->ws.acc_done[h]) hipEventDestroy(s->ws.acc_done[h]);
     }
     if (s->ws.fork) hipEventDestroy(s->ws.fork);
+    if (s->ws.mid) hipEventDestroy(s->ws.mid);
     for (int h = 0; h < kMaxParts; ++h)
         for (int k = 0; k < 2; ++k)
             if (s->ws.poll_ev[h][k]) hipEventDestroy(s->ws.poll_ev[h][k]);
@@ -751,6 +797,12 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 constexpr uint64_t kWfAutoMinPaths = 1ull << 19;
 constexpr int kTilesDefault = 0;
 
+// two parts run their batches half a batch apart (option batch_pipe; wf_render_t)
+constexpr int kBatchPipeDefault = 0;
+// k_wf_trace narrows its windows when 32-entry ones would keep < 1/4 of the waves busy (option
+// trace_sparse=n; in-process A/B: MedievalBoat +16 %, Glossy and the synthetic scenes +-0.5 %)
+constexpr int kTraceSparseDefault = 4;
+
 LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView& view) {
     LaunchOpts lo;
     const uint64_t auto_min = (view.mailbox || view.big_leaf > 0) ? 1 : kWfAutoMinPaths;
@@ -769,6 +821,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.fuse_gen = o.flag("fuse_gen", lo.fuse_gen);
     lo.dual = o.flag("dual", lo.dual);
     lo.stagger = o.flag("stagger", lo.stagger);
+    lo.pipeline = o.flag("batch_pipe", kBatchPipeDefault);
     lo.regen_bf = o.flag("regen_bf", lo.regen_bf);
     lo.persist = o.flag("persist", lo.persist);
     lo.fuse = o.flag("fuse", lo.fuse);
@@ -780,6 +833,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.packet = (int)o.num("packet", lo.packet);
     lo.packet_nodes = (int)o.num("packet_nodes", 0);
     lo.trace_dyn = o.flag("trace_dyn", lo.trace_dyn);
+    lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);
@@ -857,7 +911,10 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
         for (int h = 0; h < kMaxParts && ok; ++h)
             ok = hipStreamCreateWithFlags(&s->ws.aux[h], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&s->ws.join[h], hipEventDisableTiming) == hipSuccess;
-        for (int h = 0; h < 2 && ok; ++h) ok = hipEventCreateWithFlags(&s->ws.traced[h], hipEventDisableTiming) == hipSuccess;
+        for (int h = 0; h < 2 && ok; ++h)
+            ok = hipEventCreateWithFlags(&s->ws.traced[h], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&s->ws.acc_done[h], hipEventDisableTiming) == hipSuccess;
+        if (ok) ok = hipEventCreateWithFlags(&s->ws.mid, hipEventDisableTiming) == hipSuccess;
         for (int h = 0; h < kMaxParts && ok; ++h)
             for (int k = 0; k < 2 && ok; ++k)
                 ok = hipEventCreateWithFlags(&s->ws.poll_ev[h][k], hipEventDisableTiming) == hipSuccess;
@@ -932,6 +989,12 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     {
         const long big = o.num("big_leaf", kBigLeafDefault);
         view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? (int32_t)big : 0;
+        // leaf BVHs (built at pt_scene_create, option leaf_bvh): lanes park at every leaf that has
+        // one and walk it (leaf_turn); option leaf_walk=0 keeps them out (A/B: cooperative turns)
+        if (s->leaf_min > 0 && o.flag("leaf_walk", 1) != 0)
+            view.big_leaf = view.big_leaf > 0 ? std::min<int32_t>(view.big_leaf, s->leaf_min) : s->leaf_min;
+        else
+            view.lnodes = nullptr;
     }
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
@@ -954,8 +1017,10 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         // radiance: the batch's paths; with streaming regeneration (opt-in, when it can run) the
         // call's frames up to kRadMaxPaths, whole frames
         const bool regen = lo.regen > 0 && s->ws.h_poll != nullptr;
+        // batch pipelining (more than one batch): two batches' radiance, one per buffer
         const uint64_t rad_want = regen ? std::max<uint64_t>(s->wf.capacity, std::min<uint64_t>(all, std::max<uint64_t>(npix, kRadMaxPaths / npix * npix)))
-                                        : s->wf.capacity;
+                                  : lo.pipeline > 0 && all > s->wf.capacity ? 2ull * s->wf.capacity
+                                                                           : s->wf.capacity;
         rc2 = ensure_rad(s, rad_want);
         if (rc2 == PT_ERR_NOMEM && rad_want > s->wf.capacity) rc2 = ensure_rad(s, s->wf.capacity);
         if (rc2 != PT_OK) return rc2;
@@ -1156,6 +1221,31 @@ int pt_selftest_valu(int device, int iters, int reps, int packed, double* ms_out
     *ms_out = ms;
     // v_fma_f32 / v_pk_fma_f32 wave-instructions of the timed launches: 32 per iteration per wave
     if (fma_wave_instr_out) *fma_wave_instr_out = (uint64_t)reps * blocks * 4 * (uint64_t)iters * 32;
+    return PT_OK;
+}
+
+int pt_scene_leaf_bvh(const pt_scene* s, int leaf, int32_t* first_record, int32_t* entries, int32_t* nodes) {
+    if (!s) return fail(PT_ERR_INVALID, "null scene");
+    if (leaf < 0 || (size_t)leaf >= s->lleaves.size()) return fail(PT_ERR_INVALID, "no such leaf BVH");
+    const auto& l = s->lleaves[(size_t)leaf];
+    if (first_record) *first_record = l[0];
+    if (entries) *entries = l[1];
+    if (nodes) *nodes = l[2];
+    return PT_OK;
+}
+
+int pt_selftest_leaf(pt_scene* s, int leaf, int mode, uint32_t seed, uint32_t nrays, int32_t* out) {
+    if (!s || !out) return fail(PT_ERR_INVALID, "null argument");
+    if (leaf < 0 || (size_t)leaf >= s->lleaves.size()) return fail(PT_ERR_INVALID, "no such leaf BVH");
+    if (mode < 0 || mode > 3 || nrays == 0 || nrays > (1u << 24)) return fail(PT_ERR_INVALID, "bad mode or ray count");
+    HIP_TRY(hipSetDevice(s->device));
+    const auto& l = s->lleaves[(size_t)leaf];
+    int32_t* d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)nrays * 6 * sizeof(int32_t)));
+    hipError_t e = launch_selftest_leaf(s->view, l[0], l[1], mode, seed, nrays, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)nrays * 6 * sizeof(int32_t), hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
     return PT_OK;
 }
 

@@ -470,6 +470,91 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
     }
 }
 
+// Leaf BVH walk (SceneView::lnodes; pt_leafbvh.cpp builds the trees, pt_layout.h LNode states the
+// skip rule): the entries of the leaf whose records start at rec0 that can report a hit at t <=
+// min(prior, the leaf's best so far) — every entry that the reference's sequential strict-< loop
+// over the leaf could take — so (bt, bk) ends as the smallest (t, position) among the leaf's
+// hits below `prior`, which is what that loop ends with when it takes one.  A lane walks its own
+// ray, stackless: a node that is not skipped continues at its first child (i + 1), a skipped one
+// or a leaf node at `skip`.  tests / nodes: work counters (selftest only).
+template <bool FAST_RCP, bool STATS = false>
+__device__ __forceinline__ void leaf_walk(const SceneView& sc, const Ray& r, int rec0, float prior, float& bt, int& bk,
+                                          int* tests = nullptr, int* nodes = nullptr) {
+    int i = sc.tris[rec0].lbvh - 1;
+    const int end = sc.tris[rec0 + 1].lbvh;
+    const float idl = 1.0f / sqrtf(dot(r.d, r.d));
+    const float on = sqrtf(dot(r.o, r.o));
+    const float4* q = reinterpret_cast<const float4*>(sc.lnodes);
+    bt = __builtin_inff();
+    bk = 0x7fffffff;
+    while (i < end) {
+        const float4 a = q[4 * i], b = q[4 * i + 1], c = q[4 * i + 2];
+        const int4 e = reinterpret_cast<const int4*>(q)[4 * i + 3];
+        if (STATS) ++*nodes;
+        // |cos(d, n)| >= cos(angle(d, axis) + half-angle) over the node's normals, less a slack
+        // for this arithmetic's rounding
+        const float cb = fabsf(r.d.x * a.w + r.d.y * b.w + r.d.z * c.x) * idl;
+        const float sb = sqrtf(fmaxf(0.0f, 1.0f - cb * cb));
+        const float cf = cb * c.y - sb * c.z - 1e-5f;
+        bool skip = false;
+        if (cf > 1e-4f) {
+            const float dl = (__builtin_bit_cast(float, e.x) + c.w * on) / cf + 1e-5f * on + __builtin_bit_cast(float, e.y);
+            if (dl < 1e30f) {
+                float tn = -3.0e38f, tf = 3.0e38f;
+                float t1 = (a.x - dl - r.o.x) * r.inv.x, t2 = (b.x + dl - r.o.x) * r.inv.x;
+                tn = fmaxf(tn, fminf(t1, t2));
+                tf = fminf(tf, fmaxf(t1, t2));
+                t1 = (a.y - dl - r.o.y) * r.inv.y; t2 = (b.y + dl - r.o.y) * r.inv.y;
+                tn = fmaxf(tn, fminf(t1, t2));
+                tf = fminf(tf, fmaxf(t1, t2));
+                t1 = (a.z - dl - r.o.z) * r.inv.z; t2 = (b.z + dl - r.o.z) * r.inv.z;
+                tn = fmaxf(tn, fminf(t1, t2));
+                tf = fminf(tf, fmaxf(t1, t2));
+                skip = (tf < tn) | (tf < 0.0f) | (tn > fminf(prior, bt));
+            }
+        }
+        if (!skip && e.w >= 0) {
+            const int first = e.w & 0xffffff, cnt = e.w >> 24;
+            for (int j = 0; j < cnt; ++j) {
+                const int k = sc.lidx[first + j];
+                float t;
+                const bool hit = tri_hit<FAST_RCP>(sc.tris, rec0 + k, r, t);
+                if (STATS) ++*tests;
+                if (hit & ((t < bt) | ((t == bt) & (k < bk)))) { bt = t; bk = k; }
+            }
+        }
+        i = (!skip && e.w < 0) ? i + 1 : e.z;
+    }
+}
+__device__ __forceinline__ bool leaf_bvh_at(const SceneView& sc, const TravLean& s) {
+    int rec0 = 0, n = 0;
+    big_seg(s, rec0, n);
+    return sc.tris[rec0].lbvh > 0;
+}
+// A parked lane whose big leaf has a leaf BVH: the walk instead of the cooperative turn, then
+// the same bookkeeping as big_turn's (the leaf counts as n reference tests).
+template <bool COUNT, bool FAST_RCP>
+__device__ __forceinline__ void leaf_turn(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack, int stride,
+                                          Counters& cnt) {
+    int rec0 = 0, n = 0;
+    big_seg(s, rec0, n);
+    float bt;
+    int bk;
+    leaf_walk<FAST_RCP>(sc, r, rec0, s.best_t < 0.0f ? __builtin_inff() : s.best_t, bt, bk);
+    const bool take = (bk != 0x7fffffff) & ((s.best_t < 0.0f) | (bt < s.best_t));
+    s.best_t = take ? bt : s.best_t;
+    s.best = take ? rec0 + bk : s.best;
+    if (COUNT) cnt.tri_tests += n;
+    s.k += n;
+    s.fl &= ~TF_PARK;
+    if (s.k == s.nt) {
+        s.fl &= ~TF_LEAF;
+        lean_decide(s, stack, stride);
+    } else if (big_at(sc, s)) {
+        s.fl |= TF_PARK;  // its right leaf is big too
+    }
+}
+
 // IFIF = false: each iteration runs ONE unit type for the whole wave — a leaf turn (up to K
 // triangle tests) when leaf lanes >= node_bias * node lanes, else a node turn.  IFIF = true:
 // each iteration runs a node step for every lane that wants one and then the leaf loop for
@@ -482,6 +567,13 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     if constexpr (BIG) {  // a parked lane's big leaf goes first: the wave tests it for that ray
         const uint64_t parked = __ballot((state & TF_PARK) != 0);
         if (parked) {  // wave-uniform
+            if (sc.lnodes) {  // lanes parked at a leaf with a leaf BVH walk it, each its own ray
+                const bool walk = (state & TF_PARK) && leaf_bvh_at(sc, s);
+                if (__ballot(walk)) {
+                    if (walk) leaf_turn<COUNT, FAST_RCP>(sc, r, s, stack, stride, cnt);
+                    return true;
+                }
+            }
             big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);
             return true;
         }

@@ -77,9 +77,11 @@ struct LaunchOpts {
     int bf_slots = -1;     // brute-force kernels: hit slots per lane (< kBfSlots: tests of the recompute path): -1 default
     int trace_blocks = 0;  // traversal / step kernels: cap on the grid (tests): 0 = occupancy-derived
     int trace_dyn = 0;     // k_wf_trace takes its windows from group counters (1) or the static split (0)
+    int trace_sparse = -1; // k_wf_trace: narrower windows when 32-entry ones keep < 1/n of the waves busy (n; 0 off): -1 default
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
     int packet = -1;       // traversal scenes: packet walk + replay (k_wf_trace_pk) on 1 camera / 2 + shadow / 3 all launches: -1 default (off)
     int packet_nodes = 0;  // k_wf_trace_pk's node budget per packet (0: kPkMaxNodes)
+    int pipeline = -1;     // two parts run their batches half a batch apart on two radiance buffers: -1 default
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -143,6 +145,10 @@ struct WfStreams {
     hipStream_t aux[kMaxParts] = {};
     hipEvent_t fork = nullptr, join[kMaxParts] = {};
     hipEvent_t traced[2] = {nullptr, nullptr};  // "part h finished its trace i" (staggering, two parts)
+    // batch pipelining (LaunchOpts::pipeline): "part 0 is half-way through the first batch" and
+    // "the accumulation of the batches of radiance buffer k has been issued behind them"
+    hipEvent_t mid = nullptr, acc_done[2] = {nullptr, nullptr};
+    bool pipeline = false;
     bool stagger = false;
     bool fuse_gen = true;  // LaunchOpts::fuse_gen
     int nparts = 2;
@@ -155,6 +161,7 @@ struct WfStreams {
     // per-call launch shape (LaunchOpts, filled by launch_wavefront)
     int trace_blocks = 0;  // cap on the trace / step grid (0: occupancy-derived)
     int trace_dyn = 0;     // k_wf_trace window hand-out from group counters
+    int trace_sparse = 0;  // k_wf_trace windows below 32 entries for short queues (LaunchOpts::trace_sparse)
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
     int packet = 0;        // traversal scenes: packet walk + replay (k_wf_trace_pk; pk_launch)
@@ -183,5 +190,7 @@ hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t 
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);
 hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, hipStream_t stream);
+hipError_t launch_selftest_leaf(const SceneView& sc, int rec0, int n, int mode, uint32_t seed, uint32_t nrays, int32_t* out,
+                                hipStream_t stream);
 
 }  // namespace pt

@@ -55,7 +55,7 @@ struct alignas(16) Tri {
     float e2z;
     int32_t mat;
     int32_t uid;   // id of this (i0, i1, i2, material) entry (distinct entries numbered by first appearance; < 64 on mailbox scenes)
-    int32_t pad;
+    int32_t lbvh;  // a leaf with a leaf BVH (LNode): its first record holds root + 1, its second the end node (else 0)
 };
 inline void tri_set(Tri& t, const float v0[3], const float e1[3], const float e2[3]) {
     t.q0[0] = v0[0]; t.q0[1] = v0[1]; t.q0[2] = v0[2]; t.q0[3] = e1[0];
@@ -63,6 +63,23 @@ inline void tri_set(Tri& t, const float v0[3], const float e1[3], const float e2
     t.e2z = e2[2];
 }
 static_assert(sizeof(Tri) == 48, "tri record is 3 x 16 B");
+
+// Leaf BVH node (pt_leafbvh.cpp): the entries of one big leaf of the reference tree in a
+// tree of their own, walked without a stack in depth-first order (internal node i: its first
+// child is i + 1; `skip` is the node after its subtree).  A node is skipped only when no entry
+// below it can report a hit at t <= the closest t so far: the ray misses, or enters late, the
+// node's box grown by delta = (A + B |o|) / cf + 1e-5 |o| + C, where cf > 0 bounds
+// |cos(ray, normal)| from below over the node's cone of triangle normals (axis a, half-angle
+// with cosine ca and sine sa) — the test's rounding bound.
+struct alignas(16) LNode {
+    float lo[3], ax;
+    float hi[3], ay;
+    float az, ca, sa, B;
+    float A, C;
+    int32_t skip;
+    int32_t info;  // leaf: first lidx slot | count << 24; internal: -1
+};
+static_assert(sizeof(LNode) == 64, "leaf BVH node is 4 x 16 B");
 
 struct alignas(16) Material {
     float Ns, Ni, illum, phong;  // phong = (Ns + 2) / (2 pi), f32, as program-raymarch.wgsl:271
@@ -131,6 +148,10 @@ struct SceneView {
     // entries 2j, 2j+1 as 20 floats {v0.x of 2j, v0.x of 2j+1, v0.y, v0.y, ..., e2.z, e2.z, 0, 0};
     // an odd count ends with an all-zero entry (det = 0: never a hit)
     const float* bfpair;
+    // leaf BVHs (pt_leafbvh.cpp; nullptr when the scene has none or option leaf_walk=0): nodes and
+    // the entry (position in its leaf) of each leaf slot
+    const LNode* lnodes;
+    const int32_t* lidx;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

@@ -1,0 +1,255 @@
+// pt_leafbvh.cpp — leaf BVHs: the entries of each big leaf of the reference tree in a tree of
+// their own (pt_layout.h LNode), so that a query tests the few entries near its ray instead of
+// all of them (MedievalBoat: one leaf of 7327 entries, half the scene's box).
+//
+// The reference tests a leaf's entries in order with a strict-< update (intersection-logic.wgsl
+// :47-176, ray-triangle-intersection.wgsl:1-42), so a leaf leaves the query with the smallest
+// (t, position) over its entries that report a hit, if that t beats the closest t so far.  Any
+// walk that visits every entry able to report a hit at t <= the current bound gives exactly
+// that.  An entry below a node cannot, when the ray misses (or enters after the bound) the
+// node's box grown by the test's rounding bound: a reported hit (u, v, t) puts o + t d within
+//     delta_i = eps (216 |o - v0| + 98 (|e1| + |e2|)) / (s_i |cos(d, n_i)|)
+// of the triangle (eps = 2^-24; s_i = |e1 x e2| / (|e1| |e2|); first-order error of the
+// reference's single-precision test with FMAs where it writes them, times 2 — DESIGN.md §5.3),
+// and |cos(d, n_i)| is bounded from below over the node by its normal cone.  Nodes store
+// A = max eps (216 |v0| + 98 (|e1| + |e2|)) / s_i and B = max 216 eps / s_i, so delta <=
+// (A + B |o|) / cf; the device adds 1e-5 (|o| + max |box coordinate|) for its own slab-test
+// rounding.  Degenerate entries (s_i = 0) get an unbounded delta: their nodes are never skipped.
+#include <hip/hip_runtime.h>  // pt_layout.h's vector types
+
+#include "pt_leafbvh.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+namespace pt {
+namespace {
+
+constexpr double kEps = 5.9604644775390625e-8;  // 2^-24
+constexpr double kK1 = 216.0, kK2 = 98.0;       // the rounding bound's coefficients (with the factor 2)
+constexpr double kThin = 0.05;                  // s_i below this: the thin group
+constexpr int kLeafMax = 4;                     // entries per leaf node
+constexpr int kBins = 16;
+
+struct Item {
+    double lo[3], hi[3], c[3], n[3];  // box, centroid, unit normal (zero when degenerate)
+    double na[3];                      // the normal's line, aligned to its group's axis
+    double A, B;                       // this entry's terms of the node constants
+    int32_t k;                         // position in the reference leaf
+    int cls;                           // group: normal axis (0..2) + 3 * thin
+};
+
+float down(double x) { return std::nextafter((float)x, -FLT_MAX); }
+float up(double x) { return x >= (double)FLT_MAX ? FLT_MAX : std::nextafter((float)x, FLT_MAX); }
+
+double area(const double lo[3], const double hi[3]) {
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+// node constants over items [b, e): box, cone, A, B, C
+LNode make_node(const std::vector<Item>& it, size_t b, size_t e, int axis_cls) {
+    LNode nd{};
+    double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    double A = 0.0, B = 0.0, sum[3] = {0.0, 0.0, 0.0};
+    bool degenerate = false;
+    for (size_t i = b; i < e; ++i) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], it[i].lo[a]); hi[a] = std::max(hi[a], it[i].hi[a]); }
+        A = std::max(A, it[i].A);
+        B = std::max(B, it[i].B);
+        const double* n = it[i].n;
+        if (n[0] == 0.0 && n[1] == 0.0 && n[2] == 0.0) degenerate = true;
+        const double sg = n[axis_cls] < 0.0 ? -1.0 : 1.0;  // lines, not vectors: align to the group's axis
+        for (int a = 0; a < 3; ++a) sum[a] += sg * n[a];
+    }
+    double bmax = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        nd.lo[a] = down(lo[a]);
+        nd.hi[a] = up(hi[a]);
+        bmax = std::max({bmax, std::fabs((double)nd.lo[a]), std::fabs((double)nd.hi[a])});
+    }
+    // cone: axis = the stored (float) direction, half-angle over the entries' normal lines
+    const double ls = std::sqrt(sum[0] * sum[0] + sum[1] * sum[1] + sum[2] * sum[2]);
+    double ca = 0.0, sa = 1.0;
+    float af[3] = {1.0f, 0.0f, 0.0f};
+    if (!degenerate && ls > 0.0) {
+        for (int a = 0; a < 3; ++a) af[a] = (float)(sum[a] / ls);
+        const double la = std::sqrt((double)af[0] * af[0] + (double)af[1] * af[1] + (double)af[2] * af[2]);
+        double cmin = 1.0;
+        for (size_t i = b; i < e; ++i) {
+            const double* n = it[i].n;
+            const double c = std::fabs(n[0] * af[0] + n[1] * af[1] + n[2] * af[2]) / la;
+            cmin = std::min(cmin, c);
+        }
+        const double alpha = std::acos(std::min(1.0, cmin)) + 1e-5;
+        if (alpha < 0.5 * M_PI) { ca = std::cos(alpha); sa = std::sin(alpha); }
+    }
+    nd.ax = af[0]; nd.ay = af[1]; nd.az = af[2];
+    nd.ca = ca > 0.0 ? down(ca) : 0.0f;
+    nd.sa = sa < 1.0 ? up(sa) : 1.0f;
+    nd.A = degenerate ? FLT_MAX : up(A);
+    nd.B = degenerate ? FLT_MAX : up(B);
+    nd.C = up(1e-5 * bmax);
+    nd.skip = 0;
+    nd.info = -1;
+    return nd;
+}
+
+// Splits: binned over centroids (space) or over the aligned normals' components (direction), 3
+// axes each, chosen by the expected number of entries below a child that a ray opens: a child
+// is opened when its cone admits no bound (probability ~ sin(half-angle) for uniform directions)
+// or else when the ray meets its box (~ area ratio, as SAH).  Curved and closed surfaces put
+// every direction into a spatially small node, so the upper levels split by direction.
+void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<LNode>& nodes, std::vector<int32_t>& lidx) {
+    const size_t me = nodes.size();
+    nodes.push_back(make_node(it, b, e, axis_cls));
+    const size_t n = e - b;
+    if (n <= (size_t)kLeafMax) {
+        nodes[me].info = (int32_t)lidx.size() | (int32_t)(n << 24);
+        for (size_t i = b; i < e; ++i) lidx.push_back(it[i].k);
+        nodes[me].skip = (int32_t)nodes.size();
+        return;
+    }
+    double plo[3], phi[3];
+    for (int a = 0; a < 3; ++a) { plo[a] = nodes[me].lo[a]; phi[a] = nodes[me].hi[a]; }
+    const double AN = std::max(area(plo, phi), 1e-300);
+    struct Bin { double lo[3], hi[3], sum[3]; size_t cnt; };
+    double best = DBL_MAX;
+    int bkind = -1, bax = 0, bsplit = 0;
+    double bkmin = 0.0, bkext = 1.0;
+    std::vector<uint8_t> side(n);
+    for (int kind = 0; kind < 2; ++kind)
+        for (int ax = 0; ax < 3; ++ax) {
+            auto key = [&](const Item& x) { return kind ? x.na[ax] : x.c[ax]; };
+            double kmin = DBL_MAX, kmax = -DBL_MAX;
+            for (size_t i = b; i < e; ++i) { kmin = std::min(kmin, key(it[i])); kmax = std::max(kmax, key(it[i])); }
+            const double kext = kmax - kmin;
+            if (!(kext > 0.0)) continue;
+            auto bin_of = [&](const Item& x) { return std::min(kBins - 1, (int)((key(x) - kmin) / kext * kBins)); };
+            Bin bins[kBins];
+            for (auto& bn : bins) {
+                for (int a = 0; a < 3; ++a) { bn.lo[a] = DBL_MAX; bn.hi[a] = -DBL_MAX; bn.sum[a] = 0.0; }
+                bn.cnt = 0;
+            }
+            for (size_t i = b; i < e; ++i) {
+                Bin& bn = bins[bin_of(it[i])];
+                for (int a = 0; a < 3; ++a) {
+                    bn.lo[a] = std::min(bn.lo[a], it[i].lo[a]);
+                    bn.hi[a] = std::max(bn.hi[a], it[i].hi[a]);
+                    bn.sum[a] += it[i].na[a];
+                }
+                bn.cnt++;
+            }
+            for (int s = 1; s < kBins; ++s) {
+                double lo2[2][3], hi2[2][3], sm[2][3] = {{0, 0, 0}, {0, 0, 0}};
+                size_t cnt[2] = {0, 0};
+                for (int h = 0; h < 2; ++h)
+                    for (int a = 0; a < 3; ++a) { lo2[h][a] = DBL_MAX; hi2[h][a] = -DBL_MAX; }
+                for (int j = 0; j < kBins; ++j) {
+                    const Bin& bn = bins[j];
+                    if (!bn.cnt) continue;
+                    const int h = j < s ? 0 : 1;
+                    for (int a = 0; a < 3; ++a) {
+                        lo2[h][a] = std::min(lo2[h][a], bn.lo[a]);
+                        hi2[h][a] = std::max(hi2[h][a], bn.hi[a]);
+                        sm[h][a] += bn.sum[a];
+                    }
+                    cnt[h] += bn.cnt;
+                }
+                if (!cnt[0] || !cnt[1]) continue;
+                double axis[2][3], cmin[2] = {1.0, 1.0};
+                for (int h = 0; h < 2; ++h) {
+                    const double l = std::sqrt(sm[h][0] * sm[h][0] + sm[h][1] * sm[h][1] + sm[h][2] * sm[h][2]);
+                    for (int a = 0; a < 3; ++a) axis[h][a] = l > 0.0 ? sm[h][a] / l : 0.0;
+                    if (!(l > 0.0)) cmin[h] = 0.0;
+                }
+                for (size_t i = b; i < e; ++i) {
+                    const int h = bin_of(it[i]) < s ? 0 : 1;
+                    const double* v = it[i].na;
+                    cmin[h] = std::min(cmin[h], v[0] * axis[h][0] + v[1] * axis[h][1] + v[2] * axis[h][2]);
+                }
+                double cost = 0.0;
+                for (int h = 0; h < 2; ++h) {
+                    const double sn = cmin[h] > 0.0 ? std::sqrt(std::max(0.0, 1.0 - cmin[h] * cmin[h])) : 1.0;
+                    cost += (double)cnt[h] * (sn + (1.0 - sn) * std::min(1.0, area(lo2[h], hi2[h]) / AN));
+                }
+                if (cost < best) { best = cost; bkind = kind; bax = ax; bsplit = s; bkmin = kmin; bkext = kext; }
+            }
+        }
+    size_t mid = b;
+    if (bkind >= 0) {
+        auto p = std::partition(it.begin() + (std::ptrdiff_t)b, it.begin() + (std::ptrdiff_t)e, [&](const Item& x) {
+            const double k = bkind ? x.na[bax] : x.c[bax];
+            return std::min(kBins - 1, (int)((k - bkmin) / bkext * kBins)) < bsplit;
+        });
+        mid = (size_t)(p - it.begin());
+    }
+    if (mid == b || mid == e) {  // no usable split: halve by centroid order on the widest axis
+        double cl[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, ch[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+        for (size_t i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) { cl[a] = std::min(cl[a], it[i].c[a]); ch[a] = std::max(ch[a], it[i].c[a]); }
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+            if (ch[a] - cl[a] > ch[ax] - cl[ax]) ax = a;
+        mid = b + n / 2;
+        std::nth_element(it.begin() + (std::ptrdiff_t)b, it.begin() + (std::ptrdiff_t)mid, it.begin() + (std::ptrdiff_t)e,
+                         [&](const Item& x, const Item& y) { return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.k < y.k); });
+    }
+    build(it, b, mid, axis_cls, nodes, lidx);
+    build(it, mid, e, axis_cls, nodes, lidx);
+    nodes[me].skip = (int32_t)nodes.size();
+}
+
+}  // namespace
+
+void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
+                    int32_t& root, int32_t& end) {
+    std::vector<Item> it((size_t)n);
+    for (int32_t k = 0; k < n; ++k) {
+        const Tri& t = tris[rec0 + k];
+        const double v0[3] = {t.q0[0], t.q0[1], t.q0[2]}, e1[3] = {t.q0[3], t.q1[0], t.q1[1]},
+                     e2[3] = {t.q1[2], t.q1[3], t.e2z};
+        Item& x = it[(size_t)k];
+        x.k = k;
+        for (int a = 0; a < 3; ++a) {
+            // the triangle the test sees: v0, v0 + e1, v0 + e2 (float edges)
+            const double p1 = v0[a] + e1[a], p2 = v0[a] + e2[a];
+            x.lo[a] = std::min({v0[a], p1, p2});
+            x.hi[a] = std::max({v0[a], p1, p2});
+            x.c[a] = (v0[a] + p1 + p2) / 3.0;
+        }
+        const double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        const double ln = std::sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+        const double l1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+        const double l2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+        const double s = (ln > 0.0 && l1 > 0.0 && l2 > 0.0 && std::isfinite(ln)) ? ln / (l1 * l2) : 0.0;
+        const double lv = std::sqrt(v0[0] * v0[0] + v0[1] * v0[1] + v0[2] * v0[2]);
+        int cls = 0;
+        if (s > 0.0) {
+            for (int a = 0; a < 3; ++a) x.n[a] = nv[a] / ln;
+            for (int a = 1; a < 3; ++a)
+                if (std::fabs(x.n[a]) > std::fabs(x.n[cls])) cls = a;
+            x.A = kEps * (kK1 * lv + kK2 * (l1 + l2)) / s;
+            x.B = kEps * kK1 / s;
+        } else {
+            x.n[0] = x.n[1] = x.n[2] = 0.0;
+            x.A = x.B = DBL_MAX;
+        }
+        x.cls = cls + (s < kThin ? 3 : 0);
+        const double sg = x.n[cls] < 0.0 ? -1.0 : 1.0;
+        for (int a = 0; a < 3; ++a) x.na[a] = sg * x.n[a];
+    }
+    // groups in a fixed order; within a group the entries keep their leaf order until split
+    std::stable_sort(it.begin(), it.end(), [](const Item& a, const Item& b) { return a.cls < b.cls; });
+    root = (int32_t)nodes.size();
+    for (size_t b = 0; b < it.size();) {
+        size_t e = b;
+        while (e < it.size() && it[e].cls == it[b].cls) ++e;
+        build(it, b, e, it[b].cls % 3, nodes, lidx);
+        b = e;
+    }
+    end = (int32_t)nodes.size();
+}
+
+}  // namespace pt

@@ -231,7 +231,15 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
     // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-    const uint32_t nwin = (count + kWinRays - 1) / kWinRays;
+    // sparse windows (dyn >> 1 = n > 0, option trace_sparse=n): when windows of wr entries would
+    // keep fewer than 1/n of the waves busy (the last depths), windows of wr / 2 .. 1 entries
+    // spread the queue over more waves, so each wave's traversal is the slowest of fewer rays.  A
+    // window still takes kWinRays sequence numbers (ring and flush bookkeeping unchanged); only
+    // its queue span is wr.
+    uint32_t wr = kWinRays;
+    if (const uint32_t n = (uint32_t)dyn >> 1)
+        while (wr > 1 && (uint64_t)count * n < (uint64_t)nwaves * wr) wr >>= 1;
+    const uint32_t nwin = (count + wr - 1) / wr;
     if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * kStageBytes);
     // windows: group g owns windows g, g + G, g + 2G, ... (interleaved over the whole queue, whose
     // order is spatially coherent, so every group's share costs about the same), handed out one
@@ -250,10 +258,10 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
     uint32_t ticket = 0;  // lane 0: the group counter's value for the next fetch
     uint32_t nstatic = 0;
     auto issue = [&]() {
-        if (dyn && lane == 0) ticket = atomicAdd(ctr, 1u);
+        if ((dyn & 1) && lane == 0) ticket = atomicAdd(ctr, 1u);
     };
     auto fetch = [&]() {  // the group's next window (wave-uniform), or kNone; issues the one after
-        if (!dyn) {
+        if (!(dyn & 1)) {
             const uint64_t wid = (uint64_t)(nstatic++) * nwaves + w;
             return wid < nwin ? (uint32_t)wid : kNone;
         }
@@ -262,8 +270,8 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
         const uint64_t wid = ((uint64_t)(i / kChunk) * G + g) * kChunk + i % kChunk;  // chunk (i / 8) of group g
         return wid < nwin ? (uint32_t)wid : kNone;
     };
-    auto wcount = [&](uint32_t wid) { return min(kWinRays, count - wid * kWinRays); };
-    if ((dyn ? g * kChunk : w) >= nwin) return;  // wave-uniform: nothing for this wave
+    auto wcount = [&](uint32_t wid) { return min(wr, count - wid * wr); };
+    if (((dyn & 1) ? g * kChunk : w) >= nwin) return;  // wave-uniform: nothing for this wave
     issue();
     const uint32_t w0 = fetch();
     if (w0 == kNone) return;  // wave-uniform
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
     // local window jl (id wtab[jl % kWinTab]) sits in LDS; window jl + 1 is in flight in registers
     uint32_t jl = 0, wv = wcount(w0);
     if (lane == 0) wtab[0] = w0;
-    if (wl < wv) wray[2 * wl + half] = q[2 * (size_t)(w0 * kWinRays + wl) + half];
+    if (wl < wv) wray[2 * wl + half] = q[2 * (size_t)(w0 * wr + wl) + half];
     uint32_t nv = 0;
     float4 na = make_float4(0, 0, 0, 0);
     {
@@ -282,7 +290,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
         if (w1 != kNone) {
             nv = wcount(w1);
             if (lane == 0) wtab[1] = w1;
-            if (wl < nv) na = q[2 * (size_t)(w1 * kWinRays + wl) + half];
+            if (wl < nv) na = q[2 * (size_t)(w1 * wr + wl) + half];
         }
     }
     uint32_t cur = 0;      // sequence number of the next entry to hand out (in window jl)
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
             if (!handed || wave_any(has && sq < flushed + kWinRays)) break;
             const uint32_t wf = wtab[jf % kWinTab];
             const uint32_t fv = wcount(wf);
-            if (lane < fv) wb.hitq[wf * kWinRays + lane] = ring[(flushed + lane) & (kHitRing - 1)];
+            if (lane < fv) wb.hitq[wf * wr + lane] = ring[(flushed + lane) & (kHitRing - 1)];
             flushed += kWinRays;
         }
         // hand the next entries to idle lanes (wave-uniform control)
@@ -334,7 +342,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
                 if (wn != kNone) {
                     nv = wcount(wn);
                     if (lane == 0) wtab[(jl + 1) % kWinTab] = wn;
-                    if (wl < nv) na = q[2 * (size_t)(wn * kWinRays + wl) + half];
+                    if (wl < nv) na = q[2 * (size_t)(wn * wr + wl) + half];
                 }
             }
             const uint32_t wend = jl * kWinRays + wv;
@@ -1768,7 +1776,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     const uint32_t watchdog = ws.watchdog > 0 ? ws.watchdog : kTraceWatchdog;
     // option trace_dyn=1: k_wf_trace takes its windows from group counters (opt-in: with two parts the
     // static split is 4 % faster on Glossy and the 100k synthetic scene, the counters 2 % on the boat)
-    const int trace_dyn = ws.trace_dyn;
+    const int trace_dyn = (ws.trace_dyn ? 1 : 0) | (std::max(0, std::min(ws.trace_sparse, 1 << 20)) << 1);
     // option bf_slots < kBfSlots: tests of the recompute path
     const int bf_slots = ws.bf_slots >= 0 ? std::min(kBfSlots, ws.bf_slots) : kBfSlots;
     if constexpr (TRAV >= 500) {  // one workgroup-local launch per batch (k_wf_persist_bf), one stream
@@ -1791,8 +1799,21 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
             return wf_render_regen<LDS, TRAV, COUNT>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream, ws,
                                                      tblocks, lds, bf_slots);
     }
-    for (uint32_t fb = 0; fb < nframes; fb += F) {
+    // Batch pipelining (option batch_pipe, two parts, more than one batch): without it both parts
+    // start every batch together behind a fork and the accumulation joins them, so their launch
+    // tails (the last depths, few paths each) coincide and leave the machine idle.  With it part 1
+    // starts the call half a batch behind part 0 and neither waits for the other again: batches
+    // alternate between two radiance buffers, the accumulation of batch b (on the caller's stream)
+    // joins the parts' batch b, and a part reuses a buffer only behind the accumulation that read
+    // it.  Every path computes the same bits and the accumulation order is unchanged.
+    const uint32_t nbatches = (nframes + F - 1) / F;
+    const bool pipe = np == 2 && ws.pipeline && !ws.stagger && nbatches > 1 && ws.mid && ws.acc_done[0] &&
+                      wb.rad_cap >= 2ull * wb.capacity;
+    uint32_t b = 0;
+    for (uint32_t fb = 0; fb < nframes; fb += F, ++b) {
         const uint32_t Fb = std::min(F, nframes - fb);
+        WfBuffers wbb = wb;
+        if (pipe) wbb.rad += (size_t)(b & 1) * wb.capacity * 3;
         // frames of the batch dealt to the parts in contiguous runs (part h: frames fb + f0[h] ..)
         struct Part { WfBuffers w; uint32_t fbase, P; hipStream_t st; };
         Part pv[kMaxParts];
@@ -1800,7 +1821,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
         uint32_t f0 = 0;
         for (int h = 0; h < np && f0 < Fb; ++h) {
             const uint32_t fh = std::min<uint32_t>((Fb + np - 1) / np, Fb - f0);
-            pv[nh].w = np > 1 ? wb_part(wb, h, np, (size_t)f0 * npix * 3) : wb;
+            pv[nh].w = np > 1 ? wb_part(wbb, h, np, (size_t)f0 * npix * 3) : wbb;
             pv[nh].fbase = fb + f0;
             pv[nh].P = fh * npix;
             pv[nh].st = np > 1 ? ws.aux[h] : stream;
@@ -1814,9 +1835,11 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 pv[h].w.rstride = pv[h].w.qcap / R / 64 * 64;  // R * rstride >= paths of the part (qcap slack)
             }
         }
-        if (np > 1) {
+        if (np > 1 && (!pipe || b == 0)) {
             HIP_RETURN_IF(hipEventRecord(ws.fork, stream));
             for (int h = 0; h < nh; ++h) HIP_RETURN_IF(hipStreamWaitEvent(pv[h].st, ws.fork, 0));
+        } else if (pipe && b >= 2) {  // the radiance buffer of batch b - 2 has been accumulated
+            for (int h = 0; h < nh; ++h) HIP_RETURN_IF(hipStreamWaitEvent(pv[h].st, ws.acc_done[b & 1], 0));
         }
         // the fused kernel's first launch makes the camera paths itself (GEN); it appends into
         // count slot 1, zeroed here (k_wf_generate zeroes it otherwise)
@@ -1833,49 +1856,61 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
         // part 1's trace i waits for part 0's trace i and part 0's trace i+1 for part 1's trace i,
         // so the persistent trace kernels never share the machine.  Default: parts overlap freely.
         const bool stagger = nh == 2 && ws.stagger;
-        int in_q = 0;
-        for (int it = 0; it < iters; ++it) {
-            for (int h = 0; h < nh; ++h) {
-                const hipStream_t st = pv[h].st;
-                const WfBuffers& w = pv[h].w;
-                const int sblocks = (int)((pv[h].P + kShadeBlock - 1) / kShadeBlock);
-                if (stagger && (h == 1 || it > 0)) HIP_RETURN_IF(hipStreamWaitEvent(st, ws.traced[1 - h], 0));
-                if constexpr (TRAV >= 400) {  // trace + shade in one launch
-                    constexpr bool rcp = ((TRAV / 10) & 1) != 0;
-                    const bool cull = it < sc.cull_its;
-                    const bool g0 = fgen && it == 0;
+        // launch `it` of part h (in_q: the queue the trace kernels read, it & 1)
+        auto step = [&](int h, int it) -> hipError_t {
+            const int in_q = it & 1;
+            const hipStream_t st = pv[h].st;
+            const WfBuffers& w = pv[h].w;
+            const int sblocks = (int)((pv[h].P + kShadeBlock - 1) / kShadeBlock);
+            if (stagger && (h == 1 || it > 0)) HIP_RETURN_IF(hipStreamWaitEvent(st, ws.traced[1 - h], 0));
+            if constexpr (TRAV >= 400) {  // trace + shade in one launch
+                constexpr bool rcp = ((TRAV / 10) & 1) != 0;
+                const bool cull = it < sc.cull_its;
+                const bool g0 = fgen && it == 0;
 #define PT_STEP(E, C, G) PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<E, LDS, rcp, COUNT, C, G>), dim3(tblocks), \
                                    dim3(kTraceBlock), lds, st, sc, fp, w, it, cnt, bf_slots, frame0, stride,   \
                                    pv[h].fbase, pv[h].P, !accum)
-                    if (g0 && cull) PT_STEP(true, true, true);
-                    else if (g0) PT_STEP(true, false, true);
-                    else if ((it & 1) == 0 && cull) PT_STEP(true, true, false);
-                    else if ((it & 1) == 0) PT_STEP(true, false, false);
-                    else if (cull) PT_STEP(false, true, false);
-                    else PT_STEP(false, false, false);
+                if (g0 && cull) PT_STEP(true, true, true);
+                else if (g0) PT_STEP(true, false, true);
+                else if ((it & 1) == 0 && cull) PT_STEP(true, true, false);
+                else if ((it & 1) == 0) PT_STEP(true, false, false);
+                else if (cull) PT_STEP(false, true, false);
+                else PT_STEP(false, false, false);
 #undef PT_STEP
-                    continue;
-                } else if constexpr (TRAV >= 300)
-                    PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
-                              dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
-                else if (!COUNT && pk_ok && pk_launch(ws.packet, it))  // packet walk + replay (option packet)
-                    PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_pk<LDS, ((TRAV / 10) & 1) != 0>), dim3(pk_blocks(pk_lds)),
-                              dim3(kPkBlock), pk_lds, st, sc, w, in_q, ws.packet_nodes > 0 ? ws.packet_nodes : kPkMaxNodes);
-                else
-                    PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc,
-                              w, in_q, cnt, watchdog, trace_dyn);
-                if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
-                if ((it & 1) == 0)
-                    PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
-                              w, cnt, ws.sort_bins);
-                else
-                    PT_LAUNCH(KID_WF_SHADE_SHADOW, st, (k_wf_shade<false, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc,
-                              fp, w, cnt, ws.sort_bins);
+                return hipSuccess;
+            } else if constexpr (TRAV >= 300)
+                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
+                          dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
+            else if (!COUNT && pk_ok && pk_launch(ws.packet, it))  // packet walk + replay (option packet)
+                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_pk<LDS, ((TRAV / 10) & 1) != 0>), dim3(pk_blocks(pk_lds)),
+                          dim3(kPkBlock), pk_lds, st, sc, w, in_q, ws.packet_nodes > 0 ? ws.packet_nodes : kPkMaxNodes);
+            else
+                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc,
+                          w, in_q, cnt, watchdog, trace_dyn);
+            if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
+            if ((it & 1) == 0)
+                PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
+                          w, cnt, ws.sort_bins);
+            else
+                PT_LAUNCH(KID_WF_SHADE_SHADOW, st, (k_wf_shade<false, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc,
+                          fp, w, cnt, ws.sort_bins);
+            return hipSuccess;
+        };
+        if (pipe) {  // part 0's launches, then part 1's (its first batch starts at part 0's midpoint)
+            for (int h = 0; h < nh; ++h)
+                for (int it = 0; it < iters; ++it) {
+                    if (b == 0 && h == 1 && it == 0) HIP_RETURN_IF(hipStreamWaitEvent(pv[1].st, ws.mid, 0));
+                    HIP_RETURN_IF(step(h, it));
+                    if (b == 0 && h == 0 && it == iters / 2 - 1) HIP_RETURN_IF(hipEventRecord(ws.mid, pv[0].st));
+                    if (it == 0) HIP_RETURN_IF(hipGetLastError());
+                }
+        } else {
+            for (int it = 0; it < iters; ++it) {
+                for (int h = 0; h < nh; ++h) HIP_RETURN_IF(step(h, it));
+                // a launch that cannot run (e.g. a configuration error) fails here, after the first
+                // iteration, instead of leaving the later launches to read counts it never wrote
+                if (it == 0) HIP_RETURN_IF(hipGetLastError());
             }
-            in_q ^= 1;
-            // a launch that cannot run (e.g. a configuration error) fails here, after the first
-            // iteration, instead of leaving the later launches to read counts it never wrote
-            if (it == 0) HIP_RETURN_IF(hipGetLastError());
         }
         if (np > 1) {
             for (int h = 0; h < nh; ++h) {
@@ -1883,8 +1918,9 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 HIP_RETURN_IF(hipStreamWaitEvent(stream, ws.join[h], 0));
             }
         }
-        PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix, Fb,
+        PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wbb.rad, out, npix, Fb,
                   accum);
+        if (pipe) HIP_RETURN_IF(hipEventRecord(ws.acc_done[b & 1], stream));
     }
     return hipGetLastError();
 }
@@ -1897,6 +1933,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     for (int h = 0; h < kMaxParts; ++h) for (int k = 0; k < 2; ++k) ws.poll_ev[h][k] = ws_in.poll_ev[h][k];
     ws.nparts = std::max(1, std::min(kMaxParts, lo.parts > 0 ? lo.parts : 2));
     ws.stagger = lo.stagger > 0;
+    ws.pipeline = lo.pipeline > 0;
     ws.fuse_gen = lo.fuse_gen != 0;
     ws.regen = lo.regen > 0 && ws.h_poll != nullptr;  // option regen=1 (measured slower so far)
     ws.regen_target = lo.regen_target > 0 ? (uint32_t)std::min<long>(lo.regen_target, 0x7fffffffL) : 0u;
@@ -1907,6 +1944,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.sort_bins = sort > 0 ? (sort >= 512 ? 512 : sort >= 64 ? 64 : 8) : 0;
     ws.trace_blocks = lo.trace_blocks;
     ws.trace_dyn = lo.trace_dyn;
+    ws.trace_sparse = std::max(0, lo.trace_sparse);
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
     ws.packet = lo.packet > 0 ? lo.packet : 0;

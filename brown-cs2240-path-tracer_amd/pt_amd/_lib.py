@@ -13,7 +13,8 @@ ABI_VERSION = 3  # include/pt_hip.h PT_ABI_VERSION
 _CSRC = os.path.join(_PKG_ROOT, "csrc")
 # csrc/Makefile BUILD_SRCS: the sources whose SHA-256 the library carries as pt_build_id()
 _BUILD_SRCS = ["pt_kernels.hip", "pt_wavefront.hip", "pt_image.hip", "pt_capi.hip", "pt_math.h", "pt_layout.h",
-               "pt_device.h", "pt_path.h", "pt_kernels.h", "../../include/pt_hip.h", "pt_bvh.cpp", "Makefile"]
+               "pt_device.h", "pt_path.h", "pt_kernels.h", "../../include/pt_hip.h", "pt_bvh.cpp", "pt_leafbvh.h",
+               "pt_leafbvh.cpp", "Makefile"]
 MODE_AUTO, MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1, 2
 MATH_FNS = ["sin", "cos", "tan", "acos", "log2", "exp2", "pow", "sqrt", "div", "hash1u", "hash1", "hash2x",
             "hash2y", "min", "max"]
@@ -130,7 +131,10 @@ def load_library():
     L.pt_get_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
     L.pt_reset_options.argtypes = []
     L.pt_reset_options.restype = None
-    for fn in ("pt_selftest_valu", "pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    L.pt_scene_leaf_bvh.argtypes = [p, i, i32p, i32p, i32p]
+    L.pt_selftest_leaf.argtypes = [p, i, i, u32, u32, p]
+    for fn in ("pt_scene_leaf_bvh", "pt_selftest_leaf", "pt_selftest_valu", "pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
                "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
@@ -257,6 +261,23 @@ class Scene:
         inf = SceneInfo()
         _check(self._lib.pt_scene_get_info(self._h, ctypes.byref(inf)))
         return inf.as_dict()
+
+    def leaf_bvhs(self) -> list:
+        """pt_scene_leaf_bvh: (first record, entries, nodes) of every leaf BVH of the scene."""
+        out, k = [], 0
+        while True:
+            a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+            if self._lib.pt_scene_leaf_bvh(self._h, k, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) != 0:
+                return out
+            out.append((a.value, b.value, c.value))
+            k += 1
+
+    def selftest_leaf(self, leaf: int, mode: int, seed: int, nrays: int) -> np.ndarray:
+        """pt_selftest_leaf: [nrays, 6] int32 — the sequential loop's (position or -1, t bits), the
+        walk's, the walk's entry tests and nodes."""
+        out = np.zeros((nrays, 6), np.int32)
+        _check(self._lib.pt_selftest_leaf(self._h, leaf, mode, seed, nrays, _ptr(out)))
+        return out
 
     def render(self, meta, frame0: int, nframes: int, stride: int = 1, max_depth: int = -1, mode: int = MODE_AUTO,
                accum: np.ndarray | None = None, counters: bool = False):

@@ -148,11 +148,12 @@ int pt_set_hw_queues(int n);
  *   "kernel"        auto | mega | wavefront | literal    pipeline (auto = PT_MODE_* and the scene)
  *   "trav"          nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32   traversal flavour
  *   "lds" "fastrcp" "pipe" "ifif" "dual" "stagger" "fuse" "fuse_gen" "bf" "mailbox" "persist"
- *   "regen" "regen_bf" "bf_stackless" "trace_dyn" "tiles"                   0 | 1 switches
+ *   "regen" "regen_bf" "bf_stackless" "trace_dyn" "tiles" "batch_pipe" "leaf_walk"   0 | 1 switches
  *   "parts" "cull" "sort" "node_bias" "big_leaf" "bf_slots" "wf_paths" "wf_trace_blocks" "packet"
- *   "packet_nodes"
+ *   "packet_nodes" "trace_sparse"
  *   "regen_target" "trace_watchdog"                                         integers
  *   "mb_uid_order"  forward | reverse   (read by pt_scene_create: uid numbering of mailbox scenes)
+ *   "leaf_bvh"      integer             (read by pt_scene_create: leaves with a leaf BVH, >= this many entries)
  *   "reduce"        rccl | ordered      (pt_render_multi's reduction)
  * DESIGN.md §6 describes each.  pt_get_option writes the current value ("" = default) into buf. */
 int pt_set_option(const char* name, const char* value);
@@ -255,6 +256,18 @@ int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, u
  * their FMA wave-instructions.  Profiled with rocprofv3 PMC it pins the counter formula for the
  * fraction of VALU issue (scripts/calibrate_valu.sh). */
 int pt_selftest_valu(int device, int iters, int reps, int packed, double* ms_out, uint64_t* fma_wave_instr_out);
+
+/* Leaf BVHs (option leaf_bvh, read by pt_scene_create: leaves of at least that many entries,
+ * default 64, 0 = none): leaf BVH `leaf`'s first record, entries and nodes.
+ * PT_ERR_INVALID past the last one. */
+int pt_scene_leaf_bvh(const pt_scene* scene, int leaf, int32_t* first_record, int32_t* entries, int32_t* nodes);
+
+/* Leaf BVH stress test: nrays rays of family `mode` (0 near the leaf's entries, uniform
+ * directions; 1 aimed at them; 2 grazing their planes; 3 leaving their surfaces), each tested
+ * against leaf BVH `leaf` by the reference's sequential loop over all entries and by the walk,
+ * with the same closest-t-so-far.  out (host, nrays x 6): loop (position taken or -1, t bits),
+ * walk (position or -1, t bits), the walk's entry tests and nodes.  Blocking. */
+int pt_selftest_leaf(pt_scene* scene, int leaf, int mode, uint32_t seed, uint32_t nrays, int32_t* out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,67 @@
+"""Leaf BVHs (csrc/pt_leafbvh.cpp, pt_device.h leaf_walk): the walk over a big leaf's own tree
+must end exactly where the reference's sequential strict-< loop over all the leaf's entries
+ends — same entry, same t bits — for every ray and closest-t-so-far.  pt_selftest_leaf runs both
+on the device for four ray families, including rays grazing the entries' planes (where the
+triangle test's rounding, which the skip rule bounds, is largest) and rays leaving the surfaces
+as the path tracer's bounces do.  Renders through the walk are checked against the oracle by
+test_gpu_parity.py (the leaf variants, the boat frames) and test_gpu_config_bands.py (the boat
+band at 1920x1080)."""
+import numpy as np
+import pytest
+
+import pt_amd
+
+pytestmark = pytest.mark.gpu
+
+NRAYS = 1 << 15
+
+
+def _check(s, label, nrays=NRAYS):
+    leaves = s.leaf_bvhs()
+    assert leaves, f"{label}: no leaf BVH"
+    stats = []
+    for li, (rec0, n, nodes) in enumerate(leaves):
+        for mode in range(4):
+            out = s.selftest_leaf(li, mode, 1234 + 17 * li, nrays)
+            bad = np.flatnonzero(np.any(out[:, :2] != out[:, 2:4], axis=1))
+            assert bad.size == 0, (f"{label} leaf {li} ({n} entries) mode {mode}: {bad.size} rays differ, first "
+                                   f"{out[bad[:4]].tolist()}")
+            hits = int((out[:, 0] >= 0).sum())
+            stats.append((li, n, nodes, mode, hits, float(out[:, 4].mean()), float(out[:, 5].mean())))
+    for li, n, nodes, mode, hits, tests, nvis in stats:
+        print(f"{label} leaf {li}: {n} entries {nodes} nodes mode {mode}: {hits}/{nrays} taken, "
+              f"{tests:.1f} tests + {nvis:.1f} nodes per ray (loop: {n} tests)")
+    return stats
+
+
+def test_leaf_walk_equals_loop_boat(packed, ptopts):
+    ptopts.set("leaf_bvh", "64")
+    p = packed["MedievalBoat"]
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        stats = _check(s, "boat")
+    # the 7327-entry leaf: ~19 % of its entries tested per ray (DESIGN.md §5.3 — too many to beat
+    # the cooperative turn, hence off by default); a regression guard on the tree
+    big = [st for st in stats if st[1] > 7000]
+    assert big and all(st[5] < 0.3 * st[1] for st in big), big
+
+
+@pytest.mark.parametrize("scene", ["CornellBox", "CornellBox-Glossy", "CornellBox-Sphere"])
+def test_leaf_walk_equals_loop_small_leaves(packed, ptopts, scene):
+    """Every leaf of >= 2 entries with a leaf BVH: the Cornell boxes' axis-aligned walls give
+    rays exactly parallel to an entry's plane and to a node's box faces."""
+    ptopts.set("leaf_bvh", "2")
+    p = packed[scene]
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        _check(s, scene, nrays=1 << 13)
+
+
+def test_leaf_bvh_option(packed, ptopts):
+    p = packed["MedievalBoat"]
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        assert s.leaf_bvhs() == []  # default off
+    ptopts.set("leaf_bvh", "0")
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        assert s.leaf_bvhs() == []
+    ptopts.set("leaf_bvh", "1000")
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        assert [n for _, n, _ in s.leaf_bvhs()] == [7327]

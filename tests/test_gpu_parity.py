@@ -104,6 +104,25 @@ KERNELS = {
     # traversal kernel with windows from group counters (PT_TRACE_DYN=1), also on a 1-block grid
     "wavefront_trace_dyn": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_MAILBOX": "0"},
     "wavefront_trace_dyn_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_WF_TRACE_BLOCKS": "1"},
+    # short queues in windows below 32 entries (option trace_sparse=n; default 4): n = 1 on the full
+    # grid (windows of 1..4 entries), on 3 blocks (the last depths only), with the group counters;
+    # n = 8 on one block; off
+    "wavefront_trace_sparse_off": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "0", "PT_MAILBOX": "0"},
+    "wavefront_trace_sparse": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "1", "PT_MAILBOX": "0"},
+    "wavefront_trace_sparse_3blocks": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "1", "PT_MAILBOX": "0",
+                                       "PT_WF_TRACE_BLOCKS": "3"},
+    "wavefront_trace_sparse_dyn": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "1", "PT_TRACE_DYN": "1",
+                                   "PT_MAILBOX": "0"},
+    "wavefront_trace_sparse8_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "8", "PT_MAILBOX": "0",
+                                       "PT_WF_TRACE_BLOCKS": "1"},
+    # leaf BVHs (option leaf_bvh, read at scene creation; default off): on every leaf of >= 4 / >= 2
+    # entries (every scene, Cornell boxes with mailbox=0; the boat's 7327-entry leaf too), and on the
+    # megakernel's big-leaf path
+    "wavefront_leaf4": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0"},
+    "wavefront_leaf2_div_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0", "PT_FASTRCP": "0",
+                                   "PT_WF_TRACE_BLOCKS": "1"},
+    "mega_leaf4_lean4": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_FASTRCP": "1", "PT_LEAF_BVH": "4",
+                         "PT_MAILBOX": "0"},
     "wavefront_nosort_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "0", "PT_MAILBOX": "0"},
     "wavefront_sort64": {"PT_KERNEL": "wavefront", "PT_SORT": "64"},
     "wavefront_sort512_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "512", "PT_MAILBOX": "0"},
@@ -115,7 +134,9 @@ KERNELS = {
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
             "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
-            "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN")
+            "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN",
+            "PT_TRACE_SPARSE", "PT_BATCH_PIPE", "PT_TILES", "PT_PACKET", "PT_PACKET_NODES", "PT_LEAF_BVH",
+            "PT_LEAF_WALK")
 
 
 @pytest.fixture(params=list(KERNELS))
