@@ -153,6 +153,7 @@ struct HostLayout {
     std::vector<int32_t> bfmap;
     std::vector<LNode> lnodes;    // leaf BVHs (SceneView::lnodes), and per such leaf (first record, entries, nodes)
     std::vector<int32_t> lidx;
+    std::vector<Tri> ltris;       // per chunk slot: its entry's record, lbvh = the entry's position in its leaf
     std::vector<std::array<int32_t, 3>> lleaves;
     int32_t leaf_min = 0;         // leaves of at least this many entries have one (option leaf_bvh; 0: none)
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
@@ -384,7 +385,13 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             for (const auto& lr : leaf_ranges) {
                 if (lr.second < L.leaf_min || L.lidx.size() + (size_t)lr.second >= (1u << 24)) continue;
                 int32_t root = 0, end = 0;
+                const size_t slot0 = L.lidx.size();
                 build_leaf_bvh(L.tris.data(), lr.first, lr.second, L.lnodes, L.lidx, root, end);
+                for (size_t j = slot0; j < L.lidx.size(); ++j) {
+                    Tri t = L.tris[(size_t)(lr.first + L.lidx[j])];
+                    t.lbvh = L.lidx[j];
+                    L.ltris.push_back(t);
+                }
                 L.tris[(size_t)lr.first].lbvh = root + 1;
                 L.tris[(size_t)lr.first + 1].lbvh = end;
                 L.lleaves.push_back({lr.first, lr.second, end - root});
@@ -658,7 +665,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_pair = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
     const size_t o_lnode = align_up(o_pair + std::max<size_t>(1, L.bfpair.size()) * sizeof(float), 256);
     const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
-    const size_t total = align_up(o_lidx + std::max<size_t>(1, L.lidx.size()) * sizeof(int32_t), 256);
+    const size_t total = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -675,7 +682,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess ||
         up(o_pair, L.bfpair.data(), L.bfpair.size() * sizeof(float)) != hipSuccess ||
         up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
-        up(o_lidx, L.lidx.data(), L.lidx.size() * sizeof(int32_t)) != hipSuccess) {
+        up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -704,7 +711,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.cull_its = 0;  // per launch (launch_wavefront)
     s->view.bfpair = reinterpret_cast<const float*>(base + o_pair);
     s->view.lnodes = L.lnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_lnode);
-    s->view.lidx = L.lnodes.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_lidx);
+    s->view.ltris = L.lnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_lidx);
     s->leaf_min = L.leaf_min;
     s->lleaves = L.lleaves;
     s->view.mb_base = L.mb_base;
@@ -990,7 +997,7 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         const long big = o.num("big_leaf", kBigLeafDefault);
         view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? (int32_t)big : 0;
         // leaf BVHs (built at pt_scene_create, option leaf_bvh): lanes park at every leaf that has
-        // one and walk it (leaf_turn); option leaf_walk=0 keeps them out (A/B: cooperative turns)
+        // chunks and test them chunk by chunk (chunk_turn); option leaf_walk=0 keeps them out (A/B)
         if (s->leaf_min > 0 && o.flag("leaf_walk", 1) != 0)
             view.big_leaf = view.big_leaf > 0 ? std::min<int32_t>(view.big_leaf, s->leaf_min) : s->leaf_min;
         else

@@ -422,6 +422,12 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
     float bt = 0.0f;
     int bk = 0x7fffffff;  // none
+#ifndef PT_DIAG_BIG_REPS
+#define PT_DIAG_BIG_REPS 1
+#endif
+    // diagnostic build only (PT_DIAG_BIG_REPS=2: every turn tests its leaf twice, same result —
+    // the render's extra time is one pass's cost; scripts/gpu_ab_bigleaf.sh)
+    for (int rep = 0; rep < PT_DIAG_BIG_REPS; ++rep)
     for (int c = me; c < n; c += na) {
         float t;
         const bool take = tri_hit<FAST_RCP>(sc.tris, rec0 + c, q, t) & ((bk == 0x7fffffff) | (t < bt));
@@ -470,88 +476,139 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
     }
 }
 
-// Leaf BVH walk (SceneView::lnodes; pt_leafbvh.cpp builds the trees, pt_layout.h LNode states the
-// skip rule): the entries of the leaf whose records start at rec0 that can report a hit at t <=
-// min(prior, the leaf's best so far) — every entry that the reference's sequential strict-< loop
-// over the leaf could take — so (bt, bk) ends as the smallest (t, position) among the leaf's
-// hits below `prior`, which is what that loop ends with when it takes one.  A lane walks its own
-// ray, stackless: a node that is not skipped continues at its first child (i + 1), a skipped one
-// or a leaf node at `skip`.  tests / nodes: work counters (selftest only).
+// Leaf chunks (SceneView::lnodes; pt_leafbvh.cpp groups a big leaf's entries into chunks of at
+// most 8, pt_layout.h LNode states the skip rule).  chunk_skip: no entry of the chunk (its LNode as
+// a, b, c, e) can report a
+// hit at t <= bound for ray r (idl = 1 / |d|, on = |o|).
+__device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const float4 c, const float4 e, const Ray& r,
+                                           float idl, float on, float bound) {
+    // |cos(d, n)| >= cos(angle(d, axis) + half-angle) over the chunk's normals, less a slack for
+    // this arithmetic's rounding (the reciprocals here are within 1 ulp; the slack is 1e-5)
+    const float cb = fabsf(r.d.x * a.w + r.d.y * b.w + r.d.z * c.x) * idl;
+    const float sb = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cb * cb));
+    const float cf = cb * c.y - sb * c.z - 1e-5f;
+    if (!(cf > 1e-4f)) return false;
+    // delta, rounded up by 1e-5 relative against the approximate reciprocal
+    const float dl = (e.x + c.w * on) * __builtin_amdgcn_rcpf(cf) * 1.00001f + 1e-5f * on + e.y;
+    if (!(dl < 1e30f)) return false;
+    float tn = -3.0e38f, tf = 3.0e38f;
+    float t1 = (a.x - dl - r.o.x) * r.inv.x, t2 = (b.x + dl - r.o.x) * r.inv.x;
+    tn = fmaxf(tn, fminf(t1, t2));
+    tf = fminf(tf, fmaxf(t1, t2));
+    t1 = (a.y - dl - r.o.y) * r.inv.y; t2 = (b.y + dl - r.o.y) * r.inv.y;
+    tn = fmaxf(tn, fminf(t1, t2));
+    tf = fminf(tf, fmaxf(t1, t2));
+    t1 = (a.z - dl - r.o.z) * r.inv.z; t2 = (b.z + dl - r.o.z) * r.inv.z;
+    tn = fmaxf(tn, fminf(t1, t2));
+    tf = fminf(tf, fmaxf(t1, t2));
+    return (tf < tn) | (tf < 0.0f) | (tn > bound);
+}
+
+// The leaf whose records start at rec0, for ONE ray q (wave-uniform: every lane holds it), by
+// the whole wave: lane l checks chunk l of each block of 64 (chunk_skip against the closest t so
+// far — `prior` or the best found in earlier flushes); the open chunks are gathered one per lane
+// (ds_permute: the open lanes' chunks go to lanes filled, filled + 1, ... in rank order, the rest
+// of the permutation lands above them and is ignored), and once 64 are gathered — or the leaf is
+// done — every lane tests its chunk's up to 8 records, contiguous copies in chunk order (ltris),
+// so the loads of a lane's tests are independent of each other and of the tests.  Every entry
+// that could report a hit at t <= the bound is tested, so the wave's smallest (t, position) —
+// returned in every lane — is the sequential strict-< loop's outcome whenever the loop would take
+// one (t < prior).  tests / chunks: work counters (selftest only).
 template <bool FAST_RCP, bool STATS = false>
-__device__ __forceinline__ void leaf_walk(const SceneView& sc, const Ray& r, int rec0, float prior, float& bt, int& bk,
-                                          int* tests = nullptr, int* nodes = nullptr) {
-    int i = sc.tris[rec0].lbvh - 1;
-    const int end = sc.tris[rec0 + 1].lbvh;
-    const float idl = 1.0f / sqrtf(dot(r.d, r.d));
-    const float on = sqrtf(dot(r.o, r.o));
-    const float4* q = reinterpret_cast<const float4*>(sc.lnodes);
-    bt = __builtin_inff();
-    bk = 0x7fffffff;
-    while (i < end) {
-        const float4 a = q[4 * i], b = q[4 * i + 1], c = q[4 * i + 2];
-        const int4 e = reinterpret_cast<const int4*>(q)[4 * i + 3];
-        if (STATS) ++*nodes;
-        // |cos(d, n)| >= cos(angle(d, axis) + half-angle) over the node's normals, less a slack
-        // for this arithmetic's rounding
-        const float cb = fabsf(r.d.x * a.w + r.d.y * b.w + r.d.z * c.x) * idl;
-        const float sb = sqrtf(fmaxf(0.0f, 1.0f - cb * cb));
-        const float cf = cb * c.y - sb * c.z - 1e-5f;
-        bool skip = false;
-        if (cf > 1e-4f) {
-            const float dl = (__builtin_bit_cast(float, e.x) + c.w * on) / cf + 1e-5f * on + __builtin_bit_cast(float, e.y);
-            if (dl < 1e30f) {
-                float tn = -3.0e38f, tf = 3.0e38f;
-                float t1 = (a.x - dl - r.o.x) * r.inv.x, t2 = (b.x + dl - r.o.x) * r.inv.x;
-                tn = fmaxf(tn, fminf(t1, t2));
-                tf = fminf(tf, fmaxf(t1, t2));
-                t1 = (a.y - dl - r.o.y) * r.inv.y; t2 = (b.y + dl - r.o.y) * r.inv.y;
-                tn = fmaxf(tn, fminf(t1, t2));
-                tf = fminf(tf, fmaxf(t1, t2));
-                t1 = (a.z - dl - r.o.z) * r.inv.z; t2 = (b.z + dl - r.o.z) * r.inv.z;
-                tn = fmaxf(tn, fminf(t1, t2));
-                tf = fminf(tf, fmaxf(t1, t2));
-                skip = (tf < tn) | (tf < 0.0f) | (tn > fminf(prior, bt));
-            }
-        }
-        if (!skip && e.w >= 0) {
-            const int first = e.w & 0xffffff, cnt = e.w >> 24;
-            for (int j = 0; j < cnt; ++j) {
-                const int k = sc.lidx[first + j];
+__device__ __forceinline__ void chunk_leaf(const SceneView& sc, const Ray& q, int rec0, float prior, float& bt_out,
+                                           int& bk_out, int* tests = nullptr, int* chunks = nullptr) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const int c0 = sc.tris[rec0].lbvh - 1, c1 = sc.tris[rec0 + 1].lbvh;
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(sc.lnodes);
+    const float idl = 1.0f / sqrtf(dot(q.d, q.d));
+    const float on = sqrtf(dot(q.o, q.o));
+    float bt = __builtin_inff();
+    int bk = 0x7fffffff;  // none
+    float bound = prior;
+    int mine = 0;    // the gathered chunk of this lane (first slot | count << 24; count 0: none)
+    int filled = 0;  // lanes holding a gathered chunk (wave-uniform)
+    auto test_gathered = [&]() {
+        const int first = mine & 0xffffff, cnt = lane < filled ? (mine >> 24) : 0;
+        // two records in flight at a time: all eight would hold 96 VGPRs and cost the trace
+        // kernel its occupancy (62 -> 94 VGPRs measured)
+#pragma unroll 2
+        for (int e = 0; e < 8; ++e) {
+            if (e < cnt) {
+                const Tri* rec = sc.ltris + first + e;
+                const int k = rec->lbvh;
                 float t;
-                const bool hit = tri_hit<FAST_RCP>(sc.tris, rec0 + k, r, t);
+                const bool hit = tri_hit<FAST_RCP>(load_tri(rec, 0), q, t);
                 if (STATS) ++*tests;
                 if (hit & ((t < bt) | ((t == bt) & (k < bk)))) { bt = t; bk = k; }
             }
         }
-        i = (!skip && e.w < 0) ? i + 1 : e.z;
+        float w = bt;  // the next checks against the best so far (a lane without a hit holds +inf)
+        for (int off = 1; off < 64; off <<= 1) w = fminf(w, __shfl_xor(w, off, 64));
+        bound = fminf(prior, w);
+        filled = 0;
+    };
+    const int cl = max(c0, c1 - 1);  // a valid chunk for lanes past the end (their check is off)
+    for (int cb = c0; cb < c1; cb += 64) {
+        const int c = cb + lane, cn = min(c, cl);
+        const float4 a = nodes[4 * cn], b = nodes[4 * cn + 1], cc = nodes[4 * cn + 2], e = nodes[4 * cn + 3];
+        const int info = __builtin_bit_cast(int, e.w);
+        const bool open = c < c1 && !chunk_skip(a, b, cc, e, q, idl, on, bound);
+        const uint64_t m = __ballot(open);
+        const int cnt = (int)__popcll(m);
+        if (STATS) *chunks += cnt;
+        if (!cnt) continue;
+        if (filled + cnt > 64) test_gathered();
+        const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const int dest = open ? filled + below : (filled + cnt + (lane - below)) & 63;
+        const int got = __builtin_amdgcn_ds_permute(dest << 2, info);
+        mine = (lane >= filled && lane < filled + cnt) ? got : mine;
+        filled += cnt;
     }
+    if (filled) test_gathered();
+    // every lane ends with the wave's smallest (t, position)
+    for (int off = 1; off < 64; off <<= 1) {
+        const float ot = __shfl_xor(bt, off, 64);
+        const int ok = __shfl_xor(bk, off, 64);
+        const bool b = (ok != 0x7fffffff) & ((bk == 0x7fffffff) | (ot < bt) | ((ot == bt) & (ok < bk)));
+        bt = b ? ot : bt;
+        bk = b ? ok : bk;
+    }
+    bt_out = bt;
+    bk_out = bk;
 }
-__device__ __forceinline__ bool leaf_bvh_at(const SceneView& sc, const TravLean& s) {
-    int rec0 = 0, n = 0;
-    big_seg(s, rec0, n);
-    return sc.tris[rec0].lbvh > 0;
-}
-// A parked lane whose big leaf has a leaf BVH: the walk instead of the cooperative turn, then
-// the same bookkeeping as big_turn's (the leaf counts as n reference tests).
+// The first parked lane f whose big leaf has chunks: chunk_leaf for f's ray, then big_turn's
+// bookkeeping (the leaf counts as n reference tests).  Needs every lane of the wave running (the
+// wavefront kernels; the megakernel reaches here only through the same step with all lanes on).
 template <bool COUNT, bool FAST_RCP>
-__device__ __forceinline__ void leaf_turn(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack, int stride,
-                                          Counters& cnt) {
-    int rec0 = 0, n = 0;
-    big_seg(s, rec0, n);
+__device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, int32_t* stack,
+                                           int stride, Counters& cnt) {
+    const int f = (int)__builtin_ctzll(parked);
+    int my0 = 0, myn = 0;
+    big_seg(s, my0, myn);
+    const int rec0 = __builtin_amdgcn_readlane(my0, f), n = __builtin_amdgcn_readlane(myn, f);
+    auto bc = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), f)); };
+    Ray q;
+    q.o = mk(bc(r.o.x), bc(r.o.y), bc(r.o.z));
+    q.d = mk(bc(r.d.x), bc(r.d.y), bc(r.d.z));
+    q.inv = mk(bc(r.inv.x), bc(r.inv.y), bc(r.inv.z));
+    const float pb = bc(s.best_t);
     float bt;
     int bk;
-    leaf_walk<FAST_RCP>(sc, r, rec0, s.best_t < 0.0f ? __builtin_inff() : s.best_t, bt, bk);
-    const bool take = (bk != 0x7fffffff) & ((s.best_t < 0.0f) | (bt < s.best_t));
-    s.best_t = take ? bt : s.best_t;
-    s.best = take ? rec0 + bk : s.best;
-    if (COUNT) cnt.tri_tests += n;
-    s.k += n;
-    s.fl &= ~TF_PARK;
-    if (s.k == s.nt) {
-        s.fl &= ~TF_LEAF;
-        lean_decide(s, stack, stride);
-    } else if (big_at(sc, s)) {
-        s.fl |= TF_PARK;  // its right leaf is big too
+    chunk_leaf<FAST_RCP>(sc, q, rec0, pb < 0.0f ? __builtin_inff() : pb, bt, bk);
+    const int lane = (int)(threadIdx.x & 63u);
+    if (lane == f) {
+        const bool take = (bk != 0x7fffffff) & ((s.best_t < 0.0f) | (bt < s.best_t));
+        s.best_t = take ? bt : s.best_t;
+        s.best = take ? rec0 + bk : s.best;
+        if (COUNT) cnt.tri_tests += n;
+        s.k += n;
+        s.fl &= ~TF_PARK;
+        if (s.k == s.nt) {
+            s.fl &= ~TF_LEAF;
+            lean_decide(s, stack, stride);
+        } else if (big_at(sc, s)) {
+            s.fl |= TF_PARK;  // its right leaf is big too
+        }
     }
 }
 
@@ -560,21 +617,20 @@ __device__ __forceinline__ void leaf_turn(const SceneView& sc, const Ray& r, Tra
 // each iteration runs a node step for every lane that wants one and then the leaf loop for
 // every lane in a leaf (including lanes that just entered one), then one decision — no lane
 // waits a whole leaf turn for its node step.  Both keep each lane's unit order.
-template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false, bool IFIF = false, bool BIG = false>
+template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false, bool IFIF = false, bool BIG = false, bool CHUNKS = false>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
                                                int stride, Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE | (BIG ? TF_PARK : 0));
     if constexpr (BIG) {  // a parked lane's big leaf goes first: the wave tests it for that ray
         const uint64_t parked = __ballot((state & TF_PARK) != 0);
         if (parked) {  // wave-uniform
-            if (sc.lnodes) {  // lanes parked at a leaf with a leaf BVH walk it, each its own ray
-                const bool walk = (state & TF_PARK) && leaf_bvh_at(sc, s);
-                if (__ballot(walk)) {
-                    if (walk) leaf_turn<COUNT, FAST_RCP>(sc, r, s, stack, stride, cnt);
-                    return true;
-                }
-            }
-            big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);
+            int my0 = 0, myn = 0;  // the first parked lane's leaf (the other lanes' fields may not be a leaf's)
+            big_seg(s, my0, myn);
+            if (CHUNKS && sc.lnodes && __ballot(1) == ~0ull &&
+                sc.tris[__builtin_amdgcn_readlane(my0, (int)__builtin_ctzll(parked))].lbvh > 0)
+                chunk_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);  // its leaf has chunks
+            else
+                big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);
             return true;
         }
     }
@@ -689,7 +745,9 @@ struct TravSel { using type = TravState; };
 template <int TRAV>
 struct TravSel<TRAV, true> { using type = TravLean; };
 
-template <int TRAV, bool COUNT>
+// CHUNKS: big leaves with leaf chunks take chunk_turn (the wavefront traversal kernel; the
+// megakernel keeps the cooperative turn and its registers)
+template <int TRAV, bool COUNT, bool CHUNKS = false>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
                                              int32_t* stack, int stride, Counters& cnt) {
     if constexpr (TRAV >= 100 && TRAV < 160) {  // mailboxed lean<K> (SceneView::mailbox scenes); + 10: fast reciprocal
@@ -701,7 +759,7 @@ __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, 
         constexpr int B = TRAV % 10;
         constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
         return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, ((TRAV / 20) & 1) != 0, ((TRAV / 40) & 1) != 0,
-                              TRAV >= 160>(sc, r, s, stack, stride, cnt);
+                              TRAV >= 160, CHUNKS>(sc, r, s, stack, stride, cnt);
     }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
     else return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);

@@ -277,22 +277,23 @@ hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, h
     return hipGetLastError();
 }
 
-// Leaf BVH stress (pt_selftest_leaf): rays against the leaf whose records start at rec0, tested
-// once by the reference's sequential loop over all n entries and once by leaf_walk, both against
-// the same closest t so far (prior; none for half the rays).  Ray families (mode): 0 origins
+// Leaf chunk stress (pt_selftest_leaf): rays against the leaf whose records start at rec0, tested
+// once by the reference's sequential loop over all n entries (each lane its own ray) and once by
+// chunk_leaf (the wave on each lane's ray in turn, as chunk_turn runs it), both against the same
+// closest t so far (prior; none for half the rays).  Ray families (mode): 0 origins
 // within 5 units of a random point of an entry, directions uniform; 1 aimed at such a point
 // from 10^-3 .. 20 units away; 2 grazing: along the entry's plane, tilted by 10^-7 .. 10^-1 rad,
 // so the test's rounding is at its largest; 3 leaving a surface as the path tracer's bounces do
 // (the point offset by 1e-4 along the normal, directions uniform).  Row i of out: the loop's
-// result (position taken or -1, t bits), the walk's, the walk's entry tests and nodes.
+// result (position taken or -1, t bits), chunk_leaf's, its entry tests and open chunks.
 __device__ __forceinline__ uint32_t st_hash(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
     return x;
 }
 __global__ __launch_bounds__(256) void k_selftest_leaf(SceneView sc, int rec0, int n, int mode, uint32_t seed,
                                                        uint32_t nrays, int32_t* __restrict__ out) {
+    // every lane runs (chunk_leaf needs the whole wave); lanes past nrays store nothing
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nrays) return;
     uint32_t st = st_hash(seed * 0x9e3779b9u + i * 0x85ebca6bu + (uint32_t)mode);
     auto u01 = [&]() { st = st_hash(st + 0x6a09e667u); return (float)(st >> 8) * (1.0f / 16777216.0f); };
     auto unit = [&]() {
@@ -337,9 +338,22 @@ __global__ __launch_bounds__(256) void k_selftest_leaf(SceneView sc, int rec0, i
         float t;
         if (tri_hit<false>(sc.tris, rec0 + k, r, t) && t < lt) { lt = t; lk = k; }
     }
-    float wt;
-    int wk, tests = 0, nodes = 0;
-    leaf_walk<false, true>(sc, r, rec0, pb, wt, wk, &tests, &nodes);
+    float wt = 0.0f;
+    int wk = 0x7fffffff, tests = 0, chunks = 0;
+    const int lane = (int)(threadIdx.x & 63u);
+    for (int f = 0; f < 64; ++f) {
+        auto bc = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), f)); };
+        Ray q;
+        q.o = mk(bc(r.o.x), bc(r.o.y), bc(r.o.z));
+        q.d = mk(bc(r.d.x), bc(r.d.y), bc(r.d.z));
+        q.inv = mk(bc(r.inv.x), bc(r.inv.y), bc(r.inv.z));
+        float bt;
+        int bk, t_lane = 0, c_wave = 0;
+        chunk_leaf<false, true>(sc, q, rec0, bc(pb), bt, bk, &t_lane, &c_wave);
+        for (int off = 1; off < 64; off <<= 1) t_lane += __shfl_xor(t_lane, off, 64);
+        if (lane == f) { wt = bt; wk = bk; tests = t_lane; chunks = c_wave; }
+    }
+    if (i >= nrays) return;
     const bool ltake = lk != 0x7fffffff && lt < pb, wtake = wk != 0x7fffffff && wt < pb;
     int32_t* o = out + 6 * (size_t)i;
     o[0] = ltake ? lk : -1;
@@ -347,7 +361,7 @@ __global__ __launch_bounds__(256) void k_selftest_leaf(SceneView sc, int rec0, i
     o[2] = wtake ? wk : -1;
     o[3] = wtake ? __builtin_bit_cast(int32_t, wt) : 0;
     o[4] = tests;
-    o[5] = nodes;
+    o[5] = chunks;
 }
 
 hipError_t launch_selftest_leaf(const SceneView& sc, int rec0, int n, int mode, uint32_t seed, uint32_t nrays, int32_t* out,

@@ -64,20 +64,19 @@ inline void tri_set(Tri& t, const float v0[3], const float e1[3], const float e2
 }
 static_assert(sizeof(Tri) == 48, "tri record is 3 x 16 B");
 
-// Leaf BVH node (pt_leafbvh.cpp): the entries of one big leaf of the reference tree in a
-// tree of their own, walked without a stack in depth-first order (internal node i: its first
-// child is i + 1; `skip` is the node after its subtree).  A node is skipped only when no entry
-// below it can report a hit at t <= the closest t so far: the ray misses, or enters late, the
-// node's box grown by delta = (A + B |o|) / cf + 1e-5 |o| + C, where cf > 0 bounds
-// |cos(ray, normal)| from below over the node's cone of triangle normals (axis a, half-angle
-// with cosine ca and sine sa) — the test's rounding bound.
+// Leaf chunk (pt_leafbvh.cpp): up to 8 entries of one big leaf of the reference tree, grouped by
+// position and normal direction.  A chunk is skipped only when none of its entries can report a
+// hit at t <= the closest t so far: the ray misses, or enters late, the chunk's box grown by
+// delta = (A + B |o|) / cf + 1e-5 |o| + C, where cf > 0 bounds |cos(ray, normal)| from below over
+// the chunk's cone of triangle normals (axis a, half-angle with cosine ca and sine sa) — the
+// test's rounding bound.
 struct alignas(16) LNode {
     float lo[3], ax;
     float hi[3], ay;
     float az, ca, sa, B;
     float A, C;
-    int32_t skip;
-    int32_t info;  // leaf: first lidx slot | count << 24; internal: -1
+    int32_t skip;  // builder only
+    int32_t info;  // first lidx slot | count << 24
 };
 static_assert(sizeof(LNode) == 64, "leaf BVH node is 4 x 16 B");
 
@@ -148,10 +147,11 @@ struct SceneView {
     // entries 2j, 2j+1 as 20 floats {v0.x of 2j, v0.x of 2j+1, v0.y, v0.y, ..., e2.z, e2.z, 0, 0};
     // an odd count ends with an all-zero entry (det = 0: never a hit)
     const float* bfpair;
-    // leaf BVHs (pt_leafbvh.cpp; nullptr when the scene has none or option leaf_walk=0): nodes and
-    // the entry (position in its leaf) of each leaf slot
+    // leaf chunks (pt_leafbvh.cpp; nullptr when the scene has none or option leaf_walk=0): chunks,
+    // and per chunk slot a copy of its entry's record whose lbvh field holds the entry's position
+    // in its leaf (ltris: one load per test, no index indirection)
     const LNode* lnodes;
-    const int32_t* lidx;
+    const Tri* ltris;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

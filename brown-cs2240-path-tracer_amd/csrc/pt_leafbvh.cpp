@@ -1,20 +1,21 @@
-// pt_leafbvh.cpp — leaf BVHs: the entries of each big leaf of the reference tree in a tree of
-// their own (pt_layout.h LNode), so that a query tests the few entries near its ray instead of
-// all of them (MedievalBoat: one leaf of 7327 entries, half the scene's box).
+// pt_leafbvh.cpp — leaf chunks: the entries of each big leaf of the reference tree in chunks of up
+// to 8 with a conservative skip test each (pt_layout.h LNode), so that a query tests the chunks
+// near its ray instead of every entry (MedievalBoat: one leaf of 7327 entries, half the scene's
+// box; pt_device.h chunk_leaf checks 64 chunks per wave step and tests 8 open ones per step).
 //
 // The reference tests a leaf's entries in order with a strict-< update (intersection-logic.wgsl
 // :47-176, ray-triangle-intersection.wgsl:1-42), so a leaf leaves the query with the smallest
 // (t, position) over its entries that report a hit, if that t beats the closest t so far.  Any
 // walk that visits every entry able to report a hit at t <= the current bound gives exactly
-// that.  An entry below a node cannot, when the ray misses (or enters after the bound) the
-// node's box grown by the test's rounding bound: a reported hit (u, v, t) puts o + t d within
+// that.  An entry of a chunk cannot, when the ray misses (or enters after the bound) the
+// chunk's box grown by the test's rounding bound: a reported hit (u, v, t) puts o + t d within
 //     delta_i = eps (216 |o - v0| + 98 (|e1| + |e2|)) / (s_i |cos(d, n_i)|)
 // of the triangle (eps = 2^-24; s_i = |e1 x e2| / (|e1| |e2|); first-order error of the
 // reference's single-precision test with FMAs where it writes them, times 2 — DESIGN.md §5.3),
-// and |cos(d, n_i)| is bounded from below over the node by its normal cone.  Nodes store
+// and |cos(d, n_i)| is bounded from below over the chunk by its normal cone.  Chunks store
 // A = max eps (216 |v0| + 98 (|e1| + |e2|)) / s_i and B = max 216 eps / s_i, so delta <=
 // (A + B |o|) / cf; the device adds 1e-5 (|o| + max |box coordinate|) for its own slab-test
-// rounding.  Degenerate entries (s_i = 0) get an unbounded delta: their nodes are never skipped.
+// rounding.  Degenerate entries (s_i = 0) get an unbounded delta: their chunks are never skipped.
 #include <hip/hip_runtime.h>  // pt_layout.h's vector types
 
 #include "pt_leafbvh.h"
@@ -29,7 +30,7 @@ namespace {
 constexpr double kEps = 5.9604644775390625e-8;  // 2^-24
 constexpr double kK1 = 216.0, kK2 = 98.0;       // the rounding bound's coefficients (with the factor 2)
 constexpr double kThin = 0.05;                  // s_i below this: the thin group
-constexpr int kLeafMax = 4;                     // entries per leaf node
+constexpr int kLeafMax = 8;                     // entries per chunk (leaf node of the build tree)
 constexpr int kBins = 16;
 
 struct Item {
@@ -172,7 +173,10 @@ void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<
                 double cost = 0.0;
                 for (int h = 0; h < 2; ++h) {
                     const double sn = cmin[h] > 0.0 ? std::sqrt(std::max(0.0, 1.0 - cmin[h] * cmin[h])) : 1.0;
-                    cost += (double)cnt[h] * (sn + (1.0 - sn) * std::min(1.0, area(lo2[h], hi2[h]) / AN));
+                    // a cone without a bound opens the child for every ray that meets the leaf's
+                    // box, not just those meeting the child's: weighted 2 (scripts/leafbvh_harness.cpp:
+                    // open chunks per ray 264 -> 174 on the boat; 4 and 8 weigh worse)
+                    cost += (double)cnt[h] * std::min(1.0, 2.0 * sn + (1.0 - sn) * std::min(1.0, area(lo2[h], hi2[h]) / AN));
                 }
                 if (cost < best) { best = cost; bkind = kind; bax = ax; bsplit = s; bkmin = kmin; bkext = kext; }
             }
@@ -242,13 +246,17 @@ void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>
     }
     // groups in a fixed order; within a group the entries keep their leaf order until split
     std::stable_sort(it.begin(), it.end(), [](const Item& a, const Item& b) { return a.cls < b.cls; });
-    root = (int32_t)nodes.size();
+    std::vector<LNode> tree;
     for (size_t b = 0; b < it.size();) {
         size_t e = b;
         while (e < it.size() && it[e].cls == it[b].cls) ++e;
-        build(it, b, e, it[b].cls % 3, nodes, lidx);
+        build(it, b, e, it[b].cls % 3, tree, lidx);
         b = e;
     }
+    // the device checks chunks, not the tree: keep its leaf nodes, in depth-first order
+    root = (int32_t)nodes.size();
+    for (const LNode& nd : tree)
+        if (nd.info >= 0) nodes.push_back(nd);
     end = (int32_t)nodes.size();
 }
 

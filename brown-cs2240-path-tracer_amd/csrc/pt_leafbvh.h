@@ -8,11 +8,11 @@
 
 namespace pt {
 
-// Leaf BVH over the n entries of the leaf whose records are tris[rec0 .. rec0 + n): nodes are
-// appended to `nodes` (depth-first, LNode), the entries' positions in the leaf to `lidx`; the
-// walk covers nodes [root, end).  Entries are grouped by the axis their normal is closest to
-// and by shape (thin triangles apart, whose larger rounding bound would widen their neighbours'
-// boxes), one tree per group.
+// Chunks of the n entries of the leaf whose records are tris[rec0 .. rec0 + n): a build tree
+// groups them (by the axis their normal is closest to, by shape — thin triangles apart, whose
+// larger rounding bound would widen their neighbours' boxes — then by splits between position and
+// direction); its leaf nodes, up to 8 entries each, are appended to `nodes` as chunks [root, end)
+// (LNode), the entries' positions in the leaf to `lidx`.
 void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
                     int32_t& root, int32_t& end);
 

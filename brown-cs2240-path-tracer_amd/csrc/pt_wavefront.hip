@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
             if (nv == 0 && cur == jl * kWinRays + wv && flushed >= (jl + 1) * kWinRays) break;  // all done
             continue;  // ring full with nothing in flight: the flush above frees it
         }
-        trav_advance<TRAV, COUNT>(sc, r, s, stack, blockDim.x, c);
+        trav_advance<TRAV, COUNT, true>(sc, r, s, stack, blockDim.x, c);
         if (has && trav_finished(s)) {
             ring[sq & (kHitRing - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--synthetic", type=int, default=0, help="bench.py's N-triangle synthetic scene instead of --scene")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--profile", action="store_true", help="one more render per variant with per-launch events")
+    ap.add_argument("--scene-opt", action="append", default=[],
+                    help="NAME=VALUE set while the scene is created (options pt_scene_create reads, e.g. leaf_bvh=128)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -36,7 +38,10 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         tri, bvh, meta = bench.pack_scene(a.scene, td, a.width, a.height, a.spp, a.synthetic)
     W, H = int(meta[0]), int(meta[1])
+    for kv in a.scene_opt:
+        pt_amd.set_option(*kv.split("=", 1))
     scene = pt_amd.Scene(tri, bvh)
+    pt_amd.reset_options()
     st = torch.cuda.Stream()
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
     variants = [dict(kv.split("=", 1) for kv in v.split(",") if kv) for v in a.variants]
