@@ -134,11 +134,10 @@ Opts opts_snapshot() {
     return o;
 }
 
-// leaves of at least this many entries get a leaf BVH (option leaf_bvh, read by pt_scene_create).
-// Off by default: exact (tests/test_gpu_leafbvh.py), but on the boat the walk is 5.5x slower than
-// the cooperative big-leaf turn (the skip rule needs a bound on |cos(ray, normal)|
-// over a node, and the boat's low-poly geometry leaves ~1200 wide-cone nodes open per ray)
-constexpr long kLeafBvhDefault = 0;
+// leaves of at least this many entries get leaf chunks (option leaf_bvh, read by pt_scene_create;
+// the big-leaf threshold): exact (tests/test_gpu_leafbvh.py), MedievalBoat +10 % in process
+// (DESIGN.md §5.3); 0 = none
+constexpr long kLeafBvhDefault = 128;
 
 struct HostLayout {
     std::vector<Node> nodes;

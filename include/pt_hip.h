@@ -257,16 +257,17 @@ int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, u
  * fraction of VALU issue (scripts/calibrate_valu.sh). */
 int pt_selftest_valu(int device, int iters, int reps, int packed, double* ms_out, uint64_t* fma_wave_instr_out);
 
-/* Leaf BVHs (option leaf_bvh, read by pt_scene_create: leaves of at least that many entries,
- * default 64, 0 = none): leaf BVH `leaf`'s first record, entries and nodes.
+/* Leaf chunks (option leaf_bvh, read by pt_scene_create: leaves of at least that many entries,
+ * default 128, 0 = none): leaf `leaf`'s first record, entries and chunks.
  * PT_ERR_INVALID past the last one. */
 int pt_scene_leaf_bvh(const pt_scene* scene, int leaf, int32_t* first_record, int32_t* entries, int32_t* nodes);
 
-/* Leaf BVH stress test: nrays rays of family `mode` (0 near the leaf's entries, uniform
+/* Leaf chunk stress test: nrays rays of family `mode` (0 near the leaf's entries, uniform
  * directions; 1 aimed at them; 2 grazing their planes; 3 leaving their surfaces), each tested
- * against leaf BVH `leaf` by the reference's sequential loop over all entries and by the walk,
- * with the same closest-t-so-far.  out (host, nrays x 6): loop (position taken or -1, t bits),
- * walk (position or -1, t bits), the walk's entry tests and nodes.  Blocking. */
+ * against chunked leaf `leaf` by the reference's sequential loop over all entries and by the
+ * chunk scheme the traversal uses, with the same closest-t-so-far.  out (host, nrays x 6): loop
+ * (position taken or -1, t bits), chunks (position or -1, t bits), entries tested and chunks
+ * opened.  Blocking. */
 int pt_selftest_leaf(pt_scene* scene, int leaf, int mode, uint32_t seed, uint32_t nrays, int32_t* out);
 
 #ifdef __cplusplus

@@ -3,7 +3,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+TAG=${1:-r03}
 mkdir -p gpurun_out/profiles
-bash scripts/gpu_configs.sh r03 || exit $?
-SPP=16 bash scripts/gpu_sweep.sh r03 || exit $?
-cp gpurun_out/r03_sweep.jsonl gpurun_out/profiles/r03_sweep.jsonl
+bash scripts/gpu_configs.sh $TAG || exit $?
+SPP=16 bash scripts/gpu_sweep.sh $TAG || exit $?
+cp gpurun_out/${TAG}_sweep.jsonl gpurun_out/profiles/${TAG}_sweep.jsonl

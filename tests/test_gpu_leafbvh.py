@@ -28,11 +28,13 @@ def _check(s, label, nrays=NRAYS):
                                    f"{out[bad[:4]].tolist()}")
             hits = int((out[:, 0] >= 0).sum())
             stats.append((li, n, nodes, mode, hits, float(out[:, 4].mean()), float(out[:, 5].mean())))
-    for li, n, nchunks, mode, hits, tests, opened in stats:
+    for li, n, nchunks, mode, hits, tests, opened in stats if len(stats) <= 64 else []:
         steps = -(-nchunks // 64) + 8 * -(-opened // 64)
         print(f"{label} leaf {li}: {n} entries {nchunks} chunks mode {mode}: {hits}/{nrays} taken, "
               f"{tests:.1f} tests, {opened:.1f} open chunks per ray: ~{steps:.0f} wave-steps "
               f"(cooperative turn: {-(-n // 64)})")
+    if len(stats) > 64:
+        print(f"{label}: {len(leaves)} leaves x 4 ray families, {nrays} rays each: identical")
     return stats
 
 
@@ -59,8 +61,8 @@ def test_leaf_walk_equals_loop_small_leaves(packed, ptopts, scene):
 
 def test_leaf_bvh_option(packed, ptopts):
     p = packed["MedievalBoat"]
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        assert s.leaf_bvhs() == []  # default off
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:  # default: leaves of >= 128 entries
+        assert sorted(n for _, n, _ in s.leaf_bvhs()) == [132, 206, 219, 238, 275, 520, 7327]
     ptopts.set("leaf_bvh", "0")
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         assert s.leaf_bvhs() == []
