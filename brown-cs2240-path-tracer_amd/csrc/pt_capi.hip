@@ -851,9 +851,12 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     return lo;
 }
 
-// paths in flight per wavefront batch (kWfBytesPerPath = 188 B of queue state per path: 8 M
-// paths ~ 1.6 GB, plus the queue slack of the region layout)
-constexpr uint64_t kWfTargetPaths = 8ull << 20;
+// paths in flight per wavefront batch (kWfBytesPerPath = 188 B of queue state per path: 64 M
+// paths ~ 12 GB of the 288 GB, plus the queue slack of the region layout).  Every batch ends in
+// launch tails that carry few paths at low occupancy (the last depths); a larger batch pays them
+// for more samples: CornellBox 1024^2 x 256 +6 % at 64 M over 8 M, CornellBox-Glossy +28 %
+// (probe of option wf_paths)
+constexpr uint64_t kWfTargetPaths = 64ull << 20;
 constexpr int kBigLeafDefault = 128;
 
 // radiance of finished paths: the batch's (capacity), or with streaming regeneration a whole
@@ -1014,11 +1017,16 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         // 4096^2): the batch's parts run on their own streams and overlap (+29 % at 4096^2)
         const uint64_t all = npix * (accum ? nframes : 1);
         const uint64_t two = 2 * npix <= 0x7fffffffull ? 2 * npix : npix;
-        const uint64_t want = std::max<uint64_t>(std::min<uint64_t>(all, two), std::min<uint64_t>(all, target));
+        // a call that fits the target runs as one batch: its two parts take whole frames each, so
+        // an odd frame count gets one frame of room more (5 frames: 3 + 2, not batches of 4 and 1)
+        const uint64_t all_even = accum && nframes > 1 && (nframes & 1) ? all + npix : all;
+        const uint64_t want = std::max<uint64_t>(std::min<uint64_t>(all, two), std::min<uint64_t>(all_even, target));
         int rc2 = ensure_wavefront(s, want);
-        // the two-frame minimum doubles the state of images above the batch target (~188 B/path):
-        // fall back to one frame per batch when that does not fit
-        if (rc2 == PT_ERR_NOMEM && want > std::min<uint64_t>(all, npix)) rc2 = ensure_wavefront(s, std::min<uint64_t>(all, npix));
+        // the batch's state (~188 B/path: 12 GB at the 64 M-path target) may not fit beside other
+        // allocations: halve it down to one frame per batch before giving up
+        const uint64_t floor_paths = std::min<uint64_t>(all, npix);
+        for (uint64_t w = want; rc2 == PT_ERR_NOMEM && w > floor_paths;)
+            rc2 = ensure_wavefront(s, w = std::max<uint64_t>(w / 2, floor_paths));
         if (rc2 != PT_OK) return rc2;
         // radiance: the batch's paths; with streaming regeneration (opt-in, when it can run) the
         // call's frames up to kRadMaxPaths, whole frames

@@ -5,13 +5,15 @@ pins which BVH the reference builds.
   AUTO (so the large-grid paths run: two-part batches on their own streams, several batches per
   call with a ragged last one, coherence-sorted traversal queues, cooperative big-leaf turns on
   the boat's 7,327-entry leaf), and bands of rows of that accumulator are compared with the C
-  oracle (oracle/pt_oracle.c) rendering the same rows (po_render's y0/y1):
+  oracle (oracle/pt_oracle.c) rendering the same rows (po_render's y0/y1).  Each image is
+  rendered twice: at the default batch target (64 M paths: one batch for most of these calls)
+  and at 8 M paths (option wf_paths: several batches), and the two must be identical:
     - CornellBox-Mirror and CornellBox-Glossy 1024^2, depth 16 (the reference default), 16 frames
-      (configs[2]; 16 M paths = two 8 M-path batches of two parts each);
-    - MedievalBoat 1920x1080, depth 16, 5 frames (configs[3]; a 4-frame batch of two parts and a
-      ragged 1-frame batch), a band through the hull and one through the lit deck;
+      (configs[2]; 16 M paths = one batch, or two 8 M-path batches of two parts each);
+    - MedievalBoat 1920x1080, depth 16, 5 frames (configs[3]; at 8 M paths a 4-frame batch of two
+      parts and a ragged 1-frame batch), a band through the hull and one through the lit deck;
     - CornellBox 4096^2, depth 8, 4 frames (configs[4]'s image on one GPU; a frame is 16.8 M
-      paths, so the batch holds two frames as two parts).
+      paths, so a batch holds two frames as two parts: two batches at either target).
 * Negative control for the tree: js-geometry's `Bounds` strides are read as fixed
   at construction (`bvh.ts:46-52` with the child boxes cloned from the parent at `:72-73,
   113-114`).  The other reading — live strides — builds a different tree, and with it the
@@ -35,38 +37,54 @@ from test_gpu_bench_config import K_SETS, L2_TOL, ORACLE_THREADS, assert_same_bi
 pytestmark = pytest.mark.gpu
 
 
+SMALL_BATCH = 8 << 20  # option wf_paths: round 2's batch target, several batches per call
+
+
 def _render_bands(p, W, H, frames, depth, bands):
+    """The image at the default batch target and at SMALL_BATCH (identical bits), bands vs the
+    oracle.  Returns the accumulator and the kernel profiles of both renders."""
     meta = p.meta_for(W, H)
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        s.profile_enable(True)
-        gpu = s.render(meta, 0, frames, 1, depth, pt_amd.MODE_AUTO)
-        prof = s.profile_read()
-        s.profile_enable(False)
+    out, profs = [], []
+    for wf_paths in (None, SMALL_BATCH):
+        pt_amd.set_option("wf_paths", wf_paths)
+        try:
+            with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+                s.profile_enable(True)
+                out.append(s.render(meta, 0, frames, 1, depth, pt_amd.MODE_AUTO))
+                profs.append(s.profile_read())
+                s.profile_enable(False)
+        finally:
+            pt_amd.set_option("wf_paths", None)
+    gpu, small = out
+    assert_same_bits(small, gpu, f"{W}x{H} batch target {SMALL_BATCH} vs default")
     for y0, y1 in bands:
         ref, _ = oracle.render(p.triangle_data, p.bvh_data, meta, 0, frames, 1, depth, y0=y0, y1=y1,
                                nthreads=ORACLE_THREADS)
         assert_same_bits(gpu[y0:y1], ref, f"{W}x{H} rows {y0}..{y1}")
         assert float(ref.mean()) > 0.0, (y0, y1)  # the band sees light
-    return gpu, prof
+    return gpu, profs
 
 
 @pytest.mark.parametrize("scene", ["CornellBox-Mirror", "CornellBox-Glossy"])
 def test_config3_1024_depth16_rows_bitexact(packed, scene):
     # upper walls (Glossy's camera sees no ceiling above row ~220), the centre (mirror box / glossy
     # spheres), the floor
-    _, prof = _render_bands(packed[scene], 1024, 1024, 16, 16, [(260, 276), (500, 516), (900, 916)])
+    _, profs = _render_bands(packed[scene], 1024, 1024, 16, 16, [(260, 276), (500, 516), (900, 916)])
     want = "k_wf_step" if scene == "CornellBox-Mirror" else "k_wf_trace"  # mailbox scene / traversal scene
-    assert want in prof, prof
+    for prof in profs:
+        assert want in prof, prof
+    assert [p["k_wf_accum"]["launches"] for p in profs] == [1, 2], profs
 
 
 def test_config4_boat_1080p_depth16_rows_bitexact(packed):
-    _, prof = _render_bands(packed["MedievalBoat"], 1920, 1080, 5, 16, [(680, 696), (560, 568)])
-    assert "k_wf_trace" in prof and prof["k_wf_accum"]["launches"] == 2, prof  # two batches
+    _, profs = _render_bands(packed["MedievalBoat"], 1920, 1080, 5, 16, [(680, 696), (560, 568)])
+    assert all("k_wf_trace" in p for p in profs), profs
+    assert [p["k_wf_accum"]["launches"] for p in profs] == [1, 2], profs  # one batch / two batches
 
 
 def test_config5_image_4096_depth8_rows_bitexact(packed):
-    _, prof = _render_bands(packed["CornellBox"], 4096, 4096, 4, 8, [(400, 416), (2040, 2056), (3700, 3708)])
-    assert "k_wf_step" in prof, prof
+    _, profs = _render_bands(packed["CornellBox"], 4096, 4096, 4, 8, [(400, 416), (2040, 2056), (3700, 3708)])
+    assert all("k_wf_step" in p for p in profs), profs
 
 
 def _l2_ratios(tri, bvh, meta, spp, ref):
