@@ -81,7 +81,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr},
     {"regen_target", OPT_INT, nullptr},  {"trace_watchdog", OPT_INT, nullptr},
-    {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_mask", OPT_INT, nullptr},
+    {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
     {"reduce", OPT_ENUM, "rccl|ordered"},
 };
@@ -138,10 +138,6 @@ Opts opts_snapshot() {
 // the big-leaf threshold): exact (tests/test_gpu_leafbvh.py), MedievalBoat +10 % in process
 // (DESIGN.md §5.3); 0 = none
 constexpr long kLeafBvhDefault = 128;
-// leaves of leaf_mask .. 64 entries (below leaf_bvh) get chunks that a lane checks itself before
-// testing the open ones (pt_device.h lean_leaf_masked; option leaf_mask, read by pt_scene_create;
-// 0 = none)
-constexpr long kLeafMaskDefault = 16;
 
 struct HostLayout {
     std::vector<Node> nodes;
@@ -157,10 +153,8 @@ struct HostLayout {
     std::vector<LNode> lnodes;    // leaf BVHs (SceneView::lnodes), and per such leaf (first record, entries, nodes)
     std::vector<int32_t> lidx;
     std::vector<Tri> ltris;       // per chunk slot: its entry's record, lbvh = the entry's position in its leaf
-    std::vector<uint64_t> lcmask;  // per chunk: its entries' positions (masked leaves; SceneView::lcmask)
     std::vector<std::array<int32_t, 3>> lleaves;
     int32_t leaf_min = 0;         // leaves of at least this many entries have one (option leaf_bvh; 0: none)
-    bool masked = false;          // some leaf of <= 64 entries has chunks (option leaf_mask)
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -382,19 +376,13 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
     // default kLeafBvhDefault, 0 = none).  The leaf's first record holds root + 1, its second the
     // end of its nodes (Tri::lbvh).  The lean traversal's big-leaf step walks them (mailbox scenes:
     // only with option mailbox=0, their default kernels test every entry once per ray anyway).
-    // Masked leaves (option leaf_mask, default kLeafMaskDefault): leaves of leaf_mask .. 64 entries
-    // below leaf_bvh get the same chunks, plus per chunk the set of its entries' positions (lcmask).
     {
-        const Opts o = opts_snapshot();
-        const long lmin = o.num("leaf_bvh", kLeafBvhDefault), mmin = o.num("leaf_mask", kLeafMaskDefault);
-        if (lmin >= 2 || mmin >= 2) {
-            L.leaf_min = lmin >= 2 ? (int32_t)std::min<long>(lmin, INT32_MAX) : 0;
-            bool coop = false;
+        const long lmin = opts_snapshot().num("leaf_bvh", kLeafBvhDefault);
+        if (lmin >= 2) {
+            L.leaf_min = (int32_t)std::min<long>(lmin, INT32_MAX);
             std::sort(leaf_ranges.begin(), leaf_ranges.end());
             for (const auto& lr : leaf_ranges) {
-                const bool big = L.leaf_min > 0 && lr.second >= L.leaf_min;
-                const bool mask = !big && mmin >= 2 && lr.second >= mmin && lr.second <= 64;
-                if ((!big && !mask) || L.lidx.size() + (size_t)lr.second >= (1u << 24)) continue;
+                if (lr.second < L.leaf_min || L.lidx.size() + (size_t)lr.second >= (1u << 24)) continue;
                 int32_t root = 0, end = 0;
                 const size_t slot0 = L.lidx.size();
                 build_leaf_bvh(L.tris.data(), lr.first, lr.second, L.lnodes, L.lidx, root, end);
@@ -403,20 +391,11 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                     t.lbvh = L.lidx[j];
                     L.ltris.push_back(t);
                 }
-                L.lcmask.resize(L.lnodes.size(), 0ull);
-                if (mask)
-                    for (int32_t c = root; c < end; ++c) {
-                        const LNode& nd = L.lnodes[(size_t)c];
-                        const int32_t first = nd.info & 0xffffff, cnt = (int32_t)((uint32_t)nd.info >> 24);
-                        for (int32_t e = 0; e < cnt; ++e) L.lcmask[(size_t)c] |= 1ull << L.lidx[(size_t)(first + e)];
-                    }
                 L.tris[(size_t)lr.first].lbvh = root + 1;
                 L.tris[(size_t)lr.first + 1].lbvh = end;
                 L.lleaves.push_back({lr.first, lr.second, end - root});
-                coop |= big;
-                L.masked |= mask;
             }
-            if (!coop) L.leaf_min = 0;
+            if (L.lleaves.empty()) L.leaf_min = 0;
         }
     }
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
@@ -685,8 +664,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_pair = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
     const size_t o_lnode = align_up(o_pair + std::max<size_t>(1, L.bfpair.size()) * sizeof(float), 256);
     const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
-    const size_t o_lcm = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
-    const size_t total = align_up(o_lcm + std::max<size_t>(1, L.lcmask.size()) * sizeof(uint64_t), 256);
+    const size_t total = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -703,8 +681,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess ||
         up(o_pair, L.bfpair.data(), L.bfpair.size() * sizeof(float)) != hipSuccess ||
         up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
-        up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess ||
-        up(o_lcm, L.lcmask.data(), L.lcmask.size() * sizeof(uint64_t)) != hipSuccess) {
+        up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -734,7 +711,6 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.bfpair = reinterpret_cast<const float*>(base + o_pair);
     s->view.lnodes = L.lnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_lnode);
     s->view.ltris = L.lnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_lidx);
-    s->view.lcmask = L.masked ? reinterpret_cast<const uint64_t*>(base + o_lcm) : nullptr;
     s->leaf_min = L.leaf_min;
     s->lleaves = L.lleaves;
     s->view.mb_base = L.mb_base;
@@ -1024,12 +1000,10 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? (int32_t)big : 0;
         // leaf BVHs (built at pt_scene_create, option leaf_bvh): lanes park at every leaf that has
         // chunks and test them chunk by chunk (chunk_turn); option leaf_walk=0 keeps them out (A/B)
-        // masked leaves (lean_leaf_masked) need the chunks too; leaf_walk=0 turns both off
-        const bool walk = o.flag("leaf_walk", 1) != 0;
-        if (s->leaf_min > 0 && walk)
+        if (s->leaf_min > 0 && o.flag("leaf_walk", 1) != 0)
             view.big_leaf = view.big_leaf > 0 ? std::min<int32_t>(view.big_leaf, s->leaf_min) : s->leaf_min;
-        if (!walk) view.lcmask = nullptr;
-        if (!walk || (s->leaf_min == 0 && !view.lcmask)) view.lnodes = nullptr;
+        else
+            view.lnodes = nullptr;
     }
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;

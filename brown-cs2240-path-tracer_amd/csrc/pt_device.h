@@ -279,7 +279,7 @@ __device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r
 // lanes reject at the same step, which practically never happens), each unit is one exec
 // region and the push/pop decision is straight-line (stack[sp] is the free slot above the
 // top: max_stack = max depth + 1, pt_capi.hip).  Same units, same order, same arithmetic.
-enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8, TF_BCUR = 16, TF_PARK = 32, TF_MASK = 64 };
+enum : int { TF_LINT = 1, TF_RINT = 2, TF_LEAF = 4, TF_DONE = 8, TF_BCUR = 16, TF_PARK = 32 };
 struct TravLean {
     int node, sp, k, na, nt, la, lb, fl, best;
     float ld, rd, best_t;
@@ -612,85 +612,6 @@ __device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, Tr
     }
 }
 
-// Masked leaves (SceneView::lcmask; leaves of 2..64 entries with chunks, option leaf_mask): a lane
-// that reaches such a leaf checks the leaf's chunks ITSELF, once, against its closest t so far
-// (chunk_skip), and tests only the entries of the open chunks — in leaf order (ascending positions
-// of the 64-bit set s.rem, each chunk's positions in lcmask), with the reference's strict-< update.
-// Exact: an entry of a skipped chunk cannot report a hit at t <= the closest t at the leaf's start,
-// so the sequential loop would not take it either (strict <, and the closest t only decreases
-// within the leaf), and every other entry is tested in the reference's order.  Lanes on other
-// leaves run the plain turn (the sequential one stops at a masked right leaf, which then starts
-// masked).  The counting build books the leaf's n reference tests when the lane starts it.
-template <int K, bool COUNT, bool FAST_RCP, bool BIG>
-__device__ __forceinline__ bool lean_leaf_masked(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
-    if constexpr (BIG) {  // park at a big leaf: now, or where this turn would enter it
-        if (big_at(sc, s)) { s.fl |= TF_PARK; return false; }
-    }
-    const bool left = s.k < s.na;
-    const int rec0 = left ? s.la : s.lb;  // the current leaf: first record, positions [kb, ke) of the pair
-    const int kb = left ? 0 : s.na, ke = left ? s.na : s.nt;
-    if (!(s.fl & TF_MASK) && s.k == kb && ke - kb <= 64 && ke - kb >= 2) {  // at a leaf's start: masked?
-        const int c0 = sc.tris[rec0].lbvh - 1;
-        if (c0 >= 0) {
-            const int c1 = sc.tris[rec0 + 1].lbvh;
-            const float4* __restrict__ nodes = reinterpret_cast<const float4*>(sc.lnodes);
-            const float idl = 1.0f / sqrtf(dot(r.d, r.d));
-            const float on = sqrtf(dot(r.o, r.o));
-            const float bound = s.best_t < 0.0f ? __builtin_inff() : s.best_t;
-            uint64_t m = 0;
-            for (int c = c0; c < c1; ++c) {
-                const float4 a = nodes[4 * c], b = nodes[4 * c + 1], cc = nodes[4 * c + 2], e = nodes[4 * c + 3];
-                if (!chunk_skip(a, b, cc, e, r, idl, on, bound)) m |= sc.lcmask[c];
-            }
-            s.rem = m;
-            s.fl |= TF_MASK;
-            if (COUNT) cnt.tri_tests += ke - kb;
-        }
-    }
-    const bool msk = (s.fl & TF_MASK) != 0;
-    // a sequential lane in its left leaf stops where a masked right leaf starts
-    int lim = s.nt;
-    if (!msk && left && s.nt > s.na) {
-        const int nr = s.nt - s.na;
-        if ((BIG && nr >= sc.big_leaf) || (nr <= 64 && nr >= 2 && sc.tris[s.lb].lbvh > 0)) lim = s.na;
-    }
-    const int k0 = s.k;
-    const int bl = s.la + k0, br = s.lb - s.na + k0;
-    uint64_t rem = s.rem;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        bool live;
-        int idx;
-        if (msk) {
-            live = rem != 0;
-            idx = rec0 + (live ? (int)__builtin_ctzll(rem) : 0);
-            rem &= rem - 1;
-        } else {
-            live = j == 0 || k0 + j < lim;
-            idx = live ? (k0 + j < s.na ? bl : br) + j : rec0;
-        }
-        if (j > 0 && !wave_any(live)) break;
-        float t;
-        const bool take = tri_hit<FAST_RCP>(sc.tris, idx, r, t) & live & ((s.best_t < 0.0f) | (t < s.best_t));
-        s.best_t = take ? t : s.best_t;
-        s.best = take ? idx : s.best;
-        if (COUNT && !msk) cnt.tri_tests += live ? 1 : 0;
-    }
-    if (msk) {
-        s.rem = rem;
-        if (rem == 0) {
-            s.k = ke;
-            s.fl &= ~TF_MASK;
-        }
-    } else {
-        s.k = max(k0 + 1, min(k0 + K, lim));
-    }
-    const bool decide = s.k == s.nt;
-    s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
-    if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
-    return decide;
-}
-
 // IFIF = false: each iteration runs ONE unit type for the whole wave — a leaf turn (up to K
 // triangle tests) when leaf lanes >= node_bias * node lanes, else a node turn.  IFIF = true:
 // each iteration runs a node step for every lane that wants one and then the leaf loop for
@@ -723,12 +644,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
         if (wave_any(in_leaf) && in_leaf) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE>(sc, r, s, cnt);
     } else {
         if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
-            if (state == TF_LEAF) {
-                if (CHUNKS && !PIPE && sc.lcmask)  // scenes with masked leaves (wave-uniform)
-                    decide = lean_leaf_masked<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);
-                else
-                    decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE, BIG>(sc, r, s, cnt);
-            }
+            if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE, BIG>(sc, r, s, cnt);
         } else if (state == 0) {
             decide = lean_node_unit<COUNT>(sc, r, s, cnt);
         }

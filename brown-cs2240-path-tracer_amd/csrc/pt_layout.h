@@ -152,10 +152,6 @@ struct SceneView {
     // in its leaf (ltris: one load per test, no index indirection)
     const LNode* lnodes;
     const Tri* ltris;
-    // masked leaves (option leaf_mask; nullptr when the scene has none, or option leaf_walk=0): per
-    // chunk, the set of its entries' positions in their leaf (leaves of <= 64 entries; 0 for the
-    // chunks of bigger leaves) — pt_device.h lean_leaf_masked
-    const uint64_t* lcmask;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

@@ -61,13 +61,7 @@ def test_leaf_walk_equals_loop_small_leaves(packed, ptopts, scene):
 
 def test_leaf_bvh_option(packed, ptopts):
     p = packed["MedievalBoat"]
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        # default: cooperative chunks on leaves of >= 128 entries, masked leaves of 16..64 entries
-        ns = sorted(n for _, n, _ in s.leaf_bvhs())
-        assert [n for n in ns if n > 64] == [132, 206, 219, 238, 275, 520, 7327]
-        assert all(16 <= n <= 64 for n in ns if n <= 64) and any(n <= 64 for n in ns), ns
-    ptopts.set("leaf_mask", "0")
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:  # default: leaves of >= 128 entries
         assert sorted(n for _, n, _ in s.leaf_bvhs()) == [132, 206, 219, 238, 275, 520, 7327]
     ptopts.set("leaf_bvh", "0")
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
@@ -75,15 +69,3 @@ def test_leaf_bvh_option(packed, ptopts):
     ptopts.set("leaf_bvh", "1000")
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         assert [n for _, n, _ in s.leaf_bvhs()] == [7327]
-
-
-@pytest.mark.parametrize("scene", ["CornellBox-Glossy", "MedievalBoat"])
-def test_masked_leaf_chunks_equal_loop(packed, ptopts, scene):
-    """The chunks of masked leaves (option leaf_mask, leaves of 2..64 entries) under the same
-    device check as the cooperative walk: the skip rule is the one lean_leaf_masked applies."""
-    ptopts.set("leaf_bvh", "0")
-    ptopts.set("leaf_mask", "2")
-    p = packed[scene]
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        assert all(2 <= n <= 64 for _, n, _ in s.leaf_bvhs())
-        _check(s, scene, nrays=1 << 12)

@@ -123,12 +123,6 @@ KERNELS = {
                                    "PT_WF_TRACE_BLOCKS": "1"},
     "mega_leaf4_lean4": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_FASTRCP": "1", "PT_LEAF_BVH": "4",
                          "PT_MAILBOX": "0"},
-    # masked leaves (option leaf_mask, default 16): every leaf of 2..64 entries, with and without the
-    # cooperative chunks of bigger ones, off; the megakernel never masks (same bits by construction)
-    "wavefront_mask2": {"PT_KERNEL": "wavefront", "PT_LEAF_MASK": "2", "PT_MAILBOX": "0"},
-    "wavefront_mask2_leaf64_div_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_MASK": "2", "PT_LEAF_BVH": "65",
-                                          "PT_MAILBOX": "0", "PT_FASTRCP": "0", "PT_WF_TRACE_BLOCKS": "1"},
-    "wavefront_mask_off": {"PT_KERNEL": "wavefront", "PT_LEAF_MASK": "0", "PT_MAILBOX": "0"},
     "wavefront_nosort_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "0", "PT_MAILBOX": "0"},
     "wavefront_sort64": {"PT_KERNEL": "wavefront", "PT_SORT": "64"},
     "wavefront_sort512_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "512", "PT_MAILBOX": "0"},
@@ -142,7 +136,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
             "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN",
             "PT_TRACE_SPARSE", "PT_BATCH_PIPE", "PT_TILES", "PT_PACKET", "PT_PACKET_NODES", "PT_LEAF_BVH",
-            "PT_LEAF_WALK", "PT_LEAF_MASK")
+            "PT_LEAF_WALK")
 
 
 @pytest.fixture(params=list(KERNELS))
