@@ -415,6 +415,25 @@ __device__ __forceinline__ uint64_t phase_clock() {
     return 0;
 #endif
 }
+// Diagnostic builds only (EXTRA=-DPT_DIAG_VALU_PAD=n, scripts/gpu_ab_valupad.sh): n extra dependent
+// v_fmac_f32 per phase-1 entry, on a register nothing reads — the images are unchanged.  If the fused
+// kernel is bound by VALU issue, each added wave-instruction costs its full issue time (about 4.2
+// SIMD cycles, profiles/valu_calibration.json); if it were bound by memory or latency, the added
+// instructions would fill idle issue slots and cost little.
+#ifndef PT_DIAG_VALU_PAD
+#define PT_DIAG_VALU_PAD 0
+#endif
+// the same for the scalar ALU (PT_DIAG_SALU_PAD extra s_add_u32 per entry) and for latency
+// (PT_DIAG_SLEEP: s_sleep n per entry, the wave idles ~64 n cycles and uses no unit)
+#ifndef PT_DIAG_VALU_KIND  // the padding instruction: 0 v_fmac a,b,b; 1 v_fma_f32 (3 sources); 2 v_fmac a,b,c; 3 v_add_u32
+#define PT_DIAG_VALU_KIND 0
+#endif
+#ifndef PT_DIAG_SALU_PAD
+#define PT_DIAG_SALU_PAD 0
+#endif
+#ifndef PT_DIAG_SLEEP
+#define PT_DIAG_SLEEP 0
+#endif
 constexpr bool kBfScalarPrefetch = false;  // phase 1: next record's s_load in flight during a test (measured -2 %)
 constexpr bool kBfPrefetch = true;  // bf_step_batch loads q2/q3 before the trace
 
@@ -709,7 +728,23 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         todo = 0;
     }
     // one entry of phase 1 against the wave's 64 rays
+    float pad = r.d.x;  // PT_DIAG_VALU_PAD builds only
     auto entry = [&](int u, const TriRec& tr) __attribute__((always_inline)) {
+        if constexpr (PT_DIAG_VALU_PAD > 0) {  // diagnostic: PAD extra v_fmac_f32 per entry (results unchanged)
+#pragma unroll
+            for (int i = 0; i < PT_DIAG_VALU_PAD; ++i) {
+                if (PT_DIAG_VALU_KIND == 1) __asm__ volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(pad) : "v"(r.o.x), "v"(r.d.y));
+                else if (PT_DIAG_VALU_KIND == 2) __asm__ volatile("v_fmac_f32 %0, %1, %2" : "+v"(pad) : "v"(r.o.x), "v"(r.d.y));
+                else if (PT_DIAG_VALU_KIND == 3) __asm__ volatile("v_add_u32 %0, %1, %0" : "+v"(pad) : "v"(r.o.x));
+                else __asm__ volatile("v_fmac_f32 %0, %1, %1" : "+v"(pad) : "v"(r.o.x));
+            }
+        }
+        if constexpr (PT_DIAG_SALU_PAD > 0) {  // diagnostic: PAD extra s_add_u32 per entry
+            uint32_t sp = (uint32_t)u;
+#pragma unroll
+            for (int i = 0; i < PT_DIAG_SALU_PAD; ++i) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(sp));
+        }
+        if constexpr (PT_DIAG_SLEEP > 0) __builtin_amdgcn_s_sleep(PT_DIAG_SLEEP);  // diagnostic: ~64 x n idle cycles per entry
         const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
         const f3 rce2 = cross(r.d, e2);
         const float det = dot(e1, rce2);
