@@ -310,22 +310,21 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    render_ms = []
+    # one event pair per step, read after the loop: the host enqueues step k + 1 while the GPU still
+    # runs step k (a synchronisation per step would leave the GPU idle while ~150 launches are issued)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     scene.profile_select(dominant)
     scene.profile_enable(not args.no_kernel_timing and dominant is not None)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for ev0, ev1 in evs:
         with torch.cuda.stream(stream):
             acc.zero_()
             ev0.record(stream)
             scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
             ev1.record(stream)
             reduce_accum(acc, dist)
-        ev1.synchronize()
-        render_ms.append(ev0.elapsed_time(ev1))
     stream.synchronize()
+    render_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

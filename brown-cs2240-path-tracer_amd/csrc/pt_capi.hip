@@ -1012,7 +1012,11 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     fp.tiles = o.flag("tiles", kTilesDefault);
     if ((rc = take_watchdog(s)) != PT_OK) return rc;  // an earlier asynchronous render failed
     if (lo.wavefront) {
-        const uint64_t target = (uint64_t)std::max(1L, o.num("wf_paths", (long)kWfTargetPaths));  // A/B
+        // the target in whole pairs of frames (a batch's two parts take whole frames each): 4096^2
+        // holds 4 frames (67 M paths), not 2 of the 3.8 that 64 M would hold
+        const uint64_t target0 = (uint64_t)std::max(1L, o.num("wf_paths", (long)kWfTargetPaths));  // A/B
+        const uint64_t pairs = (target0 + 2 * npix - 1) / (2 * npix) * (2 * npix);
+        const uint64_t target = o.has("wf_paths") || pairs > 0x7fffffffull ? target0 : pairs;
         // at least two frames per batch when the call has two (images above the target, e.g.
         // 4096^2): the batch's parts run on their own streams and overlap (+29 % at 4096^2)
         const uint64_t all = npix * (accum ? nframes : 1);
