@@ -75,7 +75,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"mailbox", OPT_BOOL, nullptr},      {"persist", OPT_BOOL, nullptr},     {"regen", OPT_BOOL, nullptr},
     {"regen_bf", OPT_BOOL, nullptr},     {"bf_stackless", OPT_BOOL, nullptr}, {"trace_dyn", OPT_BOOL, nullptr},
     {"trace_sparse", OPT_INT, nullptr},
-    {"tiles", OPT_BOOL, nullptr},        {"batch_pipe", OPT_BOOL, nullptr},
+    {"tiles", OPT_BOOL, nullptr},        {"batch_pipe", OPT_BOOL, nullptr},  {"scatter", OPT_BOOL, nullptr},
     {"packet", OPT_INT, nullptr},       {"packet_nodes", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"cull", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
@@ -802,6 +802,7 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 // 7.1 / 9.1, 512^2 x 2: 13.1 / 9.6).
 constexpr uint64_t kWfAutoMinPaths = 1ull << 19;
 constexpr int kTilesDefault = 0;
+constexpr uint64_t kScatterMinPixels = 1ull << 23;
 
 // two parts run their batches half a batch apart (option batch_pipe; wf_render_t)
 constexpr int kBatchPipeDefault = 0;
@@ -974,7 +975,7 @@ int take_watchdog(pt_scene* s) {
 
 int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframes, uint32_t stride, int max_depth,
                 int mode, bool accum, float* d_out, Counters* d_cnt, hipStream_t stream) {
-    FrameParams fp;
+    FrameParams fp{};
     int rc = make_params(meta, max_depth, fp);
     if (rc != PT_OK) return rc;
     if (mode != PT_MODE_AUTO && mode != PT_MODE_MEGAKERNEL && mode != PT_MODE_WAVEFRONT)
@@ -1010,6 +1011,18 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);
     // camera paths of the wavefront batches in 8x8 pixel tiles (slot_path; every path's bits are the same)
     fp.tiles = o.flag("tiles", kTilesDefault);
+    // camera paths scattered over the image (slot_path; every path's bits are the same): by default
+    // on images of >= kScatterMinPixels (4096^2 x 32, CornellBox: 2482 -> 2669 Msamples/s; 1024^2:
+    // 2795 -> 2652, Glossy -7.5 %: row order there; a 64-pixel row batch at 4096^2 spans a quarter of
+    // what it spans at 1024^2, but spreading it by a pixel stride of 2..8 changed nothing,
+    // profiles/r03g_ab_scatter.txt)
+    if (o.flag("scatter", npix >= kScatterMinPixels ? 1 : 0) && !fp.tiles) {
+        fp.tiles = 2;
+        uint64_t m = std::max<uint64_t>(1, (uint64_t)((double)npix * 0.6180339887498949));
+        auto gcd = [](uint64_t a, uint64_t b) { while (b) { const uint64_t t = a % b; a = b; b = t; } return a; };
+        while (gcd(m, npix) != 1) ++m;
+        fp.scatter_mul = (uint32_t)(m % npix);
+    }
     if ((rc = take_watchdog(s)) != PT_OK) return rc;  // an earlier asynchronous render failed
     if (lo.wavefront) {
         // the target in whole pairs of frames (a batch's two parts take whole frames each): 4096^2
@@ -1096,7 +1109,7 @@ static int blocking_stream(pt_scene* s) {
 int pt_render(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
               int max_depth, int mode, float* accum, pt_counters* counters) {
     if (!s || !accum || !meta) return fail(PT_ERR_INVALID, "null argument");
-    FrameParams fp;
+    FrameParams fp{};
     int rc = make_params(meta, max_depth, fp);
     if (rc != PT_OK) return rc;
     const size_t n = (size_t)fp.width * fp.height * 3;
@@ -1121,7 +1134,7 @@ int pt_frame_async(pt_scene* s, const float meta[48], uint32_t t, int max_depth,
 
 int pt_frame(pt_scene* s, const float meta[48], uint32_t t, int max_depth, float* radiance) {
     if (!s || !radiance || !meta) return fail(PT_ERR_INVALID, "null argument");
-    FrameParams fp;
+    FrameParams fp{};
     int rc = make_params(meta, max_depth, fp);
     if (rc != PT_OK) return rc;
     const size_t n = (size_t)fp.width * fp.height * 3;
@@ -1150,7 +1163,7 @@ int pt_render_image(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t
                     int max_depth, int mode, uint8_t* rgba, pt_counters* counters) {
     if (!s || !rgba || !meta) return fail(PT_ERR_INVALID, "null argument");
     if (nframes == 0) return fail(PT_ERR_INVALID, "nframes == 0 (the image divides by the sample count)");
-    FrameParams fp;
+    FrameParams fp{};
     int rc = make_params(meta, max_depth, fp);
     if (rc != PT_OK) return rc;
     const size_t npix = (size_t)fp.width * fp.height;
@@ -1415,7 +1428,7 @@ extern "C" int pt_render_multi(pt_scene* const* scenes, int n, const float meta[
             if (!scenes[g] || scenes[g] == scenes[h]) return fail(PT_ERR_INVALID, "null or repeated scene");
     if (!scenes[0]) return fail(PT_ERR_INVALID, "null scene");
     if (n == 1) return pt_render(scenes[0], meta, frame0, nframes, frame_stride, max_depth, mode, accum, counters);
-    FrameParams fp;
+    FrameParams fp{};
     int rc = make_params(meta, max_depth, fp);
     if (rc != PT_OK) return rc;
     if ((uint64_t)frame0 + (uint64_t)(nframes ? nframes - 1 : 0) * frame_stride >= (1ull << 24))

@@ -168,7 +168,8 @@ struct FrameParams {
     uint32_t width, height;  // u32(meta[0]), u32(meta[1])
     int32_t direct_only;  // meta[46] > 0
     int32_t max_depth;    // literal 16 in `while(depth <= 16)`, program-raymarch.wgsl:118
-    int32_t tiles;        // wavefront camera paths generated in 8x8 pixel tiles (slot_path; results unchanged)
+    int32_t tiles;        // wavefront camera paths: 0 row order, 1 in 8x8 pixel tiles, 2 scattered (slot_path; results unchanged)
+    uint32_t scatter_mul; // tiles == 2: the multiplier of the scatter order, coprime with width * height
 };
 
 }  // namespace pt

@@ -122,12 +122,20 @@ __device__ __forceinline__ Ray unpack_shadow_ray(float4 a, float4 h, float4 n, u
 // (fp.tiles != 0): a frame's slots walk 8x8 pixel tiles, so the 64 paths of a generation batch are
 // one tile (coherent camera rays in one wave) — the W8 x H8 part of the image (W8, H8 = W, H
 // rounded down to multiples of 8) in tiles, then the pixels right of it, then those below it, row
-// by row.  Only which slot a path starts in changes: every path computes the same bits.
+// by row.  Scatter order (fp.tiles == 2, option scatter; by default on images of >= 2^23 pixels,
+// where it measured +7.5 % at 4096^2 and -5 % at 1024^2): slot q of a frame starts pixel
+// (q * fp.scatter_mul) mod npix, a bijection (the multiplier is coprime with npix, ~0.618 npix), so
+// a batch's 64 paths are spread over the image.  Only which slot a path starts in changes: every
+// path computes the same bits.
 __device__ __forceinline__ uint32_t slot_path(uint32_t s, const FrameParams& fp, uint32_t& x, uint32_t& y, uint32_t& f) {
     const uint32_t W = fp.width, npix = W * fp.height;
     f = s / npix;
     uint32_t q = s - f * npix;
-    if (!fp.tiles) {
+    if (fp.tiles == 2) {
+        q = (uint32_t)(((uint64_t)q * fp.scatter_mul) % npix);
+        y = q / W;
+        x = q - y * W;
+    } else if (!fp.tiles) {
         y = q / W;
         x = q - y * W;
     } else {

@@ -94,6 +94,10 @@ KERNELS = {
     "wavefront_tiles_nogen": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_FUSE_GEN": "0"},
     "wavefront_tiles_persist": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_PERSIST": "1"},
     "wavefront_tiles_trav": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_MAILBOX": "0"},
+    # camera paths scattered over the image (option scatter: slot q -> pixel q * m mod npix)
+    "wavefront_scatter": {"PT_KERNEL": "wavefront", "PT_SCATTER": "1"},
+    "wavefront_scatter_trav_nofusegen": {"PT_KERNEL": "wavefront", "PT_SCATTER": "1", "PT_MAILBOX": "0",
+                                         "PT_FUSE_GEN": "0"},
     # packet walk + replay (k_wf_trace_pk): camera launches, camera + shadow, every launch; with a
     # node budget so small that every packet gives up (the real-test replay), and on one block
     "wavefront_packet1": {"PT_KERNEL": "wavefront", "PT_PACKET": "1", "PT_MAILBOX": "0"},
@@ -136,7 +140,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
             "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN",
             "PT_TRACE_SPARSE", "PT_BATCH_PIPE", "PT_TILES", "PT_PACKET", "PT_PACKET_NODES", "PT_LEAF_BVH",
-            "PT_LEAF_WALK")
+            "PT_LEAF_WALK", "PT_SCATTER")
 
 
 @pytest.fixture(params=list(KERNELS))
