@@ -76,6 +76,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"regen_bf", OPT_BOOL, nullptr},     {"bf_stackless", OPT_BOOL, nullptr}, {"trace_dyn", OPT_BOOL, nullptr},
     {"trace_sparse", OPT_INT, nullptr},
     {"tiles", OPT_BOOL, nullptr},        {"batch_pipe", OPT_BOOL, nullptr},  {"scatter", OPT_BOOL, nullptr},
+    {"region_perm", OPT_BOOL, nullptr},
     {"packet", OPT_INT, nullptr},       {"packet_nodes", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"cull", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
@@ -802,13 +803,18 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 // 7.1 / 9.1, 512^2 x 2: 13.1 / 9.6).
 constexpr uint64_t kWfAutoMinPaths = 1ull << 19;
 constexpr int kTilesDefault = 0;
-constexpr uint64_t kScatterMinPixels = 1ull << 23;
+
 
 // two parts run their batches half a batch apart (option batch_pipe; wf_render_t)
 constexpr int kBatchPipeDefault = 0;
 // k_wf_trace narrows its windows when 32-entry ones would keep < 1/4 of the waves busy (option
 // trace_sparse=n; in-process A/B: MedievalBoat +16 %, Glossy and the synthetic scenes +-0.5 %)
 constexpr int kTraceSparseDefault = 4;
+// camera batches dealt to the fused kernel's regions by a permutation (option region_perm): a
+// block's 8 waves serve 8 neighbouring regions, which in row order hold neighbouring batches — at
+// 4096^2, 512 neighbouring pixels of one row (an eighth of it) on one CU; permuted, batches far
+// apart: 4096^2 2475 -> 2679 Msamples/s, 1024^2 and Mirror unchanged (profiles/r03h_ab_region_perm.txt)
+constexpr int kRegionPermDefault = 1;
 
 LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView& view) {
     LaunchOpts lo;
@@ -841,6 +847,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.packet_nodes = (int)o.num("packet_nodes", 0);
     lo.trace_dyn = o.flag("trace_dyn", lo.trace_dyn);
     lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
+    lo.region_perm = o.flag("region_perm", kRegionPermDefault);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);
@@ -940,6 +947,7 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     }
     w.capacity = (uint32_t)n;
     w.qcap = (uint32_t)qn;
+    w.rq = w.rqi = 1;
     w.rad = s->d_rad;
     w.rad_cap = s->rad_cap;
     return PT_OK;
@@ -1011,12 +1019,11 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);
     // camera paths of the wavefront batches in 8x8 pixel tiles (slot_path; every path's bits are the same)
     fp.tiles = o.flag("tiles", kTilesDefault);
-    // camera paths scattered over the image (slot_path; every path's bits are the same): by default
-    // on images of >= kScatterMinPixels (4096^2 x 32, CornellBox: 2482 -> 2669 Msamples/s; 1024^2:
-    // 2795 -> 2652, Glossy -7.5 %: row order there; a 64-pixel row batch at 4096^2 spans a quarter of
-    // what it spans at 1024^2, but spreading it by a pixel stride of 2..8 changed nothing,
-    // profiles/r03g_ab_scatter.txt)
-    if (o.flag("scatter", npix >= kScatterMinPixels ? 1 : 0) && !fp.tiles) {
+    // camera paths scattered over the image (slot_path; every path's bits are the same; opt-in:
+    // 4096^2 x 32, CornellBox: 2482 -> 2669 Msamples/s, but 1024^2: 2795 -> 2652 and Glossy -7.5 %,
+    // profiles/r03g_ab_scatter.txt; the default region permutation gives the 4096^2 gain without
+    // the 1024^2 loss, profiles/r03h_ab_region_perm.txt)
+    if (o.flag("scatter", 0) && !fp.tiles) {
         fp.tiles = 2;
         uint64_t m = std::max<uint64_t>(1, (uint64_t)((double)npix * 0.6180339887498949));
         auto gcd = [](uint64_t a, uint64_t b) { while (b) { const uint64_t t = a % b; a = b; b = t; } return a; };

@@ -78,6 +78,7 @@ struct LaunchOpts {
     int trace_blocks = 0;  // traversal / step kernels: cap on the grid (tests): 0 = occupancy-derived
     int trace_dyn = 0;     // k_wf_trace takes its windows from group counters (1) or the static split (0)
     int trace_sparse = -1; // k_wf_trace: narrower windows when 32-entry ones keep < 1/n of the waves busy (n; 0 off): -1 default
+    int region_perm = -1;  // k_wf_step_bf: camera batches dealt to regions by a permutation (WfBuffers::rq); -1 default
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
     int packet = -1;       // traversal scenes: packet walk + replay (k_wf_trace_pk) on 1 camera / 2 + shadow / 3 all launches: -1 default (off)
     int packet_nodes = 0;  // k_wf_trace_pk's node budget per packet (0: kPkMaxNodes)
@@ -118,6 +119,11 @@ struct WfBuffers {
     uint32_t* rcnt;
     uint32_t rstride;
     uint32_t nreg;
+    // camera batch j of the fused kernel's regions goes to region (j mod nreg) * rqi mod nreg, so
+    // region r holds the batches j = r * rq mod nreg (+ k nreg) (rq * rqi = 1 mod nreg; option
+    // region_perm; 1, 1: j mod nreg, neighbouring regions — one block's waves — take neighbouring
+    // batches)
+    uint32_t rq, rqi;
     // streaming path regeneration (k_wf_step_bf<..., REGEN>): every extension launch tops each
     // region up to `target` entries with new camera paths of the region's share of the render;
     // rgen[slot * kRegions + r] = camera batches of region r made so far (two slots, alternating
@@ -162,6 +168,7 @@ struct WfStreams {
     int trace_blocks = 0;  // cap on the trace / step grid (0: occupancy-derived)
     int trace_dyn = 0;     // k_wf_trace window hand-out from group counters
     int trace_sparse = 0;  // k_wf_trace windows below 32 entries for short queues (LaunchOpts::trace_sparse)
+    int region_perm = 0;   // LaunchOpts::region_perm
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
     int packet = 0;        // traversal scenes: packet walk + replay (k_wf_trace_pk; pk_launch)

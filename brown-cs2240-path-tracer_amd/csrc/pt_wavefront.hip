@@ -122,8 +122,8 @@ __device__ __forceinline__ Ray unpack_shadow_ray(float4 a, float4 h, float4 n, u
 // (fp.tiles != 0): a frame's slots walk 8x8 pixel tiles, so the 64 paths of a generation batch are
 // one tile (coherent camera rays in one wave) — the W8 x H8 part of the image (W8, H8 = W, H
 // rounded down to multiples of 8) in tiles, then the pixels right of it, then those below it, row
-// by row.  Scatter order (fp.tiles == 2, option scatter; by default on images of >= 2^23 pixels,
-// where it measured +7.5 % at 4096^2 and -5 % at 1024^2): slot q of a frame starts pixel
+// by row.  Scatter order (fp.tiles == 2, option scatter, opt-in: +7.5 % at 4096^2, -5 % at 1024^2,
+// and the default region permutation gives the 4096^2 gain alone): slot q of a frame starts pixel
 // (q * fp.scatter_mul) mod npix, a bijection (the multiplier is coprime with npix, ~0.618 npix), so
 // a batch's 64 paths are spread over the image.  Only which slot a path starts in changes: every
 // path computes the same bits.
@@ -170,10 +170,11 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
     }
     // region layout (k_wf_step_bf, wb.nreg > 0): 64-path batch j goes to region j % nreg
     const uint32_t R = wb.nreg;
-    if (R && p < R) {  // counts of region p: its batches j = p, p + R, ... < ceil(P / 64)
+    if (R && p < R) {  // counts of region p: its batches j = t, t + R, ... < ceil(P / 64), t = p rq mod R
         const uint32_t nbat = (P + 63) / 64;
-        const uint32_t n = p < nbat ? (nbat - p + R - 1) / R : 0u;
-        const uint32_t last = p + (n - 1) * R;
+        const uint32_t t = (uint32_t)((uint64_t)p * wb.rq % R);
+        const uint32_t n = t < nbat ? (nbat - t + R - 1) / R : 0u;
+        const uint32_t last = t + (n - 1) * R;
         wb.rcnt[p] = n == 0 ? 0u : n * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
         wb.rcnt[kRegions + p] = 0;
     }
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
         PathState ps;
         Ray r = path_begin(fp, x, y, t, ps);
         const uint32_t j = p / 64;
-        const uint32_t i = R ? (j % R) * wb.rstride + (j / R) * 64 + (p & 63) : p;
+        const uint32_t i = R ? (uint32_t)((uint64_t)(j % R) * wb.rqi % R) * wb.rstride + (j / R) * 64 + (p & 63) : p;
         store_entry(wb.ext, i, r, pid, ps);
         if (COUNT) { c.samples++; c.ext_queries++; }
     }
@@ -1246,10 +1247,11 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     const uint32_t rg = w % R, g = w / R, G = (nwaves - rg + R - 1) / R;
     if (g == 0 && lane_id() == 0) wb.rcnt[((it + 2) % 3) * kRegions + rg] = 0;
     const uint32_t nbat = (P + 63) / 64;
-    const uint32_t ncam = rg < nbat ? (nbat - rg + R - 1) / R : 0u;  // camera batches of region rg
+    const uint32_t tg = (uint32_t)((uint64_t)rg * wb.rq % R);  // region rg's camera batches: tg, tg + R, ...
+    const uint32_t ncam = tg < nbat ? (nbat - tg + R - 1) / R : 0u;
     uint32_t count, nqb, nnew = 0;
     if constexpr (GEN) {  // k_wf_generate's closed-form count of region rg
-        const uint32_t last = rg + (ncam - 1) * R;
+        const uint32_t last = tg + (ncam - 1) * R;
         count = ncam == 0 ? 0u : ncam * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
         if (w == 0 && lane_id() == 0) { wb.ctl[WF_COUNT0] = P; wb.ctl[WF_COUNT1] = 0; }
         nqb = 0;
@@ -1262,7 +1264,7 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     const Tri* gtris = sc.tris;  // global records for phase 1
     if (LDS) stage_scene_lds(sc, l.scene);
     const uint32_t nb = nqb + nnew;
-    const GenArgs ga{frame0, stride, fbase, R, rg, P, raw_salt};
+    const GenArgs ga{frame0, stride, fbase, R, tg, P, raw_salt};
     Counters c = {};
     for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves
         bf_step_batch<EXT, FAST_RCP, COUNT, GEN>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
@@ -1704,6 +1706,7 @@ static hipError_t wf_render_regen(const SceneView& sc, const FrameParams& fp, co
             q.P = fh * npix;
             q.st = np > 1 ? ws.aux[h] : stream;
             q.w.nreg = R;
+            q.w.rq = q.w.rqi = 1;
             q.w.rstride = q.w.qcap / R / 64 * 64;  // >= capacity / R (queue slack)
             uint64_t T = q.w.capacity;
             if (ws.regen_target) T = std::min<uint64_t>(T, ws.regen_target / (uint64_t)nh);
@@ -1873,9 +1876,21 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
         }
         if constexpr (TRAV >= 400) {  // region-partitioned queues (k_wf_step_bf)
             const uint32_t R = std::min<uint32_t>(kRegions, (uint32_t)tblocks * (kTraceBlock / 64));
+            // region_perm: region r takes camera batches r q mod R (q ~ 0.618 R, coprime with R), so
+            // the 8 waves of a block (8 neighbouring regions) work on batches far apart in the image
+            uint32_t q = 1, qi = 1;
+            if (ws.region_perm && R > 2) {
+                auto gcd = [](uint32_t a, uint32_t b) { while (b) { const uint32_t t = a % b; a = b; b = t; } return a; };
+                q = std::max<uint32_t>(1, (uint32_t)(R * 0.6180339887498949));
+                while (gcd(q, R) != 1) ++q;
+                qi = 1;
+                while ((uint64_t)q * qi % R != 1) ++qi;  // R <= 512
+            }
             for (int h = 0; h < nh; ++h) {
                 pv[h].w.nreg = R;
                 pv[h].w.rstride = pv[h].w.qcap / R / 64 * 64;  // R * rstride >= paths of the part (qcap slack)
+                pv[h].w.rq = q;
+                pv[h].w.rqi = qi;
             }
         }
         if (np > 1 && (!pipe || b == 0)) {
@@ -1988,6 +2003,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.trace_blocks = lo.trace_blocks;
     ws.trace_dyn = lo.trace_dyn;
     ws.trace_sparse = std::max(0, lo.trace_sparse);
+    ws.region_perm = lo.region_perm > 0 ? 1 : 0;
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
     ws.packet = lo.packet > 0 ? lo.packet : 0;
