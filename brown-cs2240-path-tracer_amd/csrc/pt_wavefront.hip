@@ -205,6 +205,14 @@ constexpr uint32_t kHitRing = 128;  // entries; power of two, multiple of kWinRa
 constexpr uint32_t kWinTab = 8;  // window ids of the windows between the last flushed and the prefetched one
 constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8 + kWinTab * 4;
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
+// k_wf_trace's block (the traversal scenes): its LDS is per lane (the traversal stack, max_stack
+// words) and per wave (kStageBytes), so the block size sets the LDS granularity, not the total
+#ifndef PT_TRACE_BLOCK
+#define PT_TRACE_BLOCK 512
+#endif
+constexpr uint32_t kTraceBlockTr = PT_TRACE_BLOCK;
+template <int TRAV>
+constexpr uint32_t trace_block() { return TRAV >= 300 ? kTraceBlock : kTraceBlockTr; }
 
 // Work split: the queue is cut into windows of 32 entries; wave w of N takes windows w, w+N,
 // w+2N, ... (interleaving, not contiguous chunks, because queue order is spatially coherent —
@@ -225,7 +233,7 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 #define PT_TRACE_OCC
 #endif
 template <bool LDS, int TRAV, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
+__global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
                                                           uint32_t watchdog, int dyn) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
@@ -256,7 +264,7 @@ __global__ __launch_bounds__(kTraceBlock) PT_TRACE_OCC void k_wf_trace(SceneView
     // groups are made of whole blocks (the 8 waves of a block share a counter and the windows of a
     // chunk of 8 consecutive ones: rays of one chunk are neighbours in the queue, so a CU's waves
     // keep working on similar rays — its L1 then holds what they all read)
-    constexpr uint32_t kChunk = kTraceBlock / 64;
+    constexpr uint32_t kChunk = kTraceBlockTr / 64;
     const uint32_t nblk = nwaves / kChunk, G = min(kTraceGroups, nblk), g = (w / kChunk) % G;
     uint32_t* ctr = trace_counter(wb.rfetch, in_q, g);
     const uint32_t lane = lane_id();
@@ -1639,7 +1647,8 @@ constexpr const void* trace_kernel() {
 template <bool LDS, int TRAV, bool COUNT>
 static size_t trace_lds(const SceneView& sc) {
     const size_t per_wave = TRAV >= 300 ? (size_t)kBfSlots * 64 * 4 : kStageBytes;
-    return (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * per_wave + (LDS ? sc.span_bytes : 0);
+    constexpr uint32_t B = trace_block<TRAV>();
+    return (size_t)sc.max_stack * B * 4 + (B / 64) * per_wave + (LDS ? sc.span_bytes : 0);
 }
 template <bool LDS, int TRAV, bool COUNT>
 static int trace_blocks(size_t lds_bytes) {
@@ -1650,7 +1659,7 @@ static int trace_blocks(size_t lds_bytes) {
         int per_cu = 0, dev = 0, cus = 0;
         hipGetDevice(&dev);
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<LDS, TRAV, COUNT>(), kTraceBlock, lds_bytes);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<LDS, TRAV, COUNT>(), trace_block<TRAV>(), lds_bytes);
         b = std::max(1, per_cu) * std::max(1, cus);
         cached_lds = lds_bytes;
     }
@@ -1943,7 +1952,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_pk<LDS, ((TRAV / 10) & 1) != 0>), dim3(pk_blocks(pk_lds)),
                           dim3(kPkBlock), pk_lds, st, sc, w, in_q, ws.packet_nodes > 0 ? ws.packet_nodes : kPkMaxNodes);
             else
-                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds, st, sc,
+                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlockTr), lds, st, sc,
                           w, in_q, cnt, watchdog, trace_dyn);
             if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
             if ((it & 1) == 0)
