@@ -89,6 +89,25 @@ def test_options_set_get_reset_and_validate():
     assert pt_amd.get_option("trav") == "" and pt_amd.get_option("parts") == ""
 
 
+def test_round3_layout_options():
+    """The queue-layout switches of round 3 are options like the others: flags
+    that take 0/1 and reject anything else; the batch target is an integer."""
+    pt_amd.reset_options()
+    try:
+        for name in ("region_perm", "scatter"):
+            pt_amd.set_option(name, 0)
+            assert pt_amd.get_option(name) == "0"
+            pt_amd.set_option(name, 1)
+            with pytest.raises(pt_amd.PtError):
+                pt_amd.set_option(name, "2")
+        pt_amd.set_option("wf_paths", 8 << 20)
+        assert pt_amd.get_option("wf_paths") == str(8 << 20)
+        with pytest.raises(pt_amd.PtError):
+            pt_amd.set_option("wf_paths", "lots")
+    finally:
+        pt_amd.reset_options()
+
+
 def test_kernel_time_struct_matches_header():
     # pt_kernel_time: name[32], launches, total/min/max/busy ms
     assert ctypes.sizeof(pt_amd._lib.KernelTime) == 32 + 8 + 4 * 8
