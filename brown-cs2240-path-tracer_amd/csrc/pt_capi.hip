@@ -76,7 +76,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"regen_bf", OPT_BOOL, nullptr},     {"bf_stackless", OPT_BOOL, nullptr}, {"trace_dyn", OPT_BOOL, nullptr},
     {"trace_sparse", OPT_INT, nullptr},
     {"tiles", OPT_BOOL, nullptr},        {"batch_pipe", OPT_BOOL, nullptr},  {"scatter", OPT_BOOL, nullptr},
-    {"region_perm", OPT_BOOL, nullptr},
+    {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
     {"packet", OPT_INT, nullptr},       {"packet_nodes", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"cull", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
@@ -848,6 +848,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.trace_dyn = o.flag("trace_dyn", lo.trace_dyn);
     lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
     lo.region_perm = o.flag("region_perm", kRegionPermDefault);
+    lo.trace_ring = (int)o.num("trace_ring", 0);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);

@@ -79,6 +79,7 @@ struct LaunchOpts {
     int trace_dyn = 0;     // k_wf_trace takes its windows from group counters (1) or the static split (0)
     int trace_sparse = -1; // k_wf_trace: narrower windows when 32-entry ones keep < 1/n of the waves busy (n; 0 off): -1 default
     int region_perm = -1;  // k_wf_step_bf: camera batches dealt to regions by a permutation (WfBuffers::rq); -1 default
+    int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
     int packet = -1;       // traversal scenes: packet walk + replay (k_wf_trace_pk) on 1 camera / 2 + shadow / 3 all launches: -1 default (off)
     int packet_nodes = 0;  // k_wf_trace_pk's node budget per packet (0: kPkMaxNodes)
@@ -169,6 +170,7 @@ struct WfStreams {
     int trace_dyn = 0;     // k_wf_trace window hand-out from group counters
     int trace_sparse = 0;  // k_wf_trace windows below 32 entries for short queues (LaunchOpts::trace_sparse)
     int region_perm = 0;   // LaunchOpts::region_perm
+    int trace_ring = 0;    // LaunchOpts::trace_ring
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
     int packet = 0;        // traversal scenes: packet walk + replay (k_wf_trace_pk; pk_launch)

@@ -201,9 +201,17 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
 // loop: on gfx9 loads and stores share the wave's in-order vmcnt, so a per-lane global store
 // (or prefetch) in the loop makes the next use of any loaded register wait for it.
 constexpr uint32_t kWinRays = 32;
-constexpr uint32_t kHitRing = 128;  // entries; power of two, multiple of kWinRays
-constexpr uint32_t kWinTab = 8;  // window ids of the windows between the last flushed and the prefetched one
-constexpr uint32_t kStageBytes = kWinRays * 32 + kHitRing * 8 + kWinTab * 4;
+// the hit ring: 128 or 256 entries (a power of two, a multiple of kWinRays, >= 2 windows), chosen
+// per launch (trace_ring): a larger ring lets a wave take new windows while more of its earlier
+// windows' stragglers still trace (Glossy: 64 entries -15 %, 256 +4.3 % in process,
+// profiles/r03k_ab_ring*.log), but its LDS can cost a block per CU (the boat: 3 -> 2 blocks, -2.4 %)
+constexpr uint32_t kHitRing = 128;
+constexpr uint32_t kHitRingMax = 256;
+// window ids of the windows between the last flushed and the prefetched one: the ring holds
+// kHitRing / kWinRays windows, plus the one in registers
+constexpr uint32_t kWinTab = 2 * kHitRingMax / kWinRays;
+static_assert(kWinTab >= kHitRingMax / kWinRays + 2, "wtab must name every window the ring can hold");
+__host__ __device__ constexpr uint32_t stage_bytes(uint32_t ring) { return kWinRays * 32 + ring * 8 + kWinTab * 4; }
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 // k_wf_trace's block (the traversal scenes): its LDS is per lane (the traversal stack, max_stack
 // words) and per wave (kStageBytes), so the block size sets the LDS granularity, not the total
@@ -234,14 +242,14 @@ constexpr uint32_t trace_block() { return TRAV >= 300 ? kTraceBlock : kTraceBloc
 #endif
 template <bool LDS, int TRAV, bool COUNT>
 __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
-                                                          uint32_t watchdog, int dyn) {
+                                                          uint32_t watchdog, int dyn, uint32_t nring) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
-    char* stage = stage_base + (threadIdx.x / 64u) * kStageBytes;
+    char* stage = stage_base + (threadIdx.x / 64u) * stage_bytes(nring);
     float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
-    int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [kHitRing]
-    uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32 + kHitRing * 8);  // [kWinTab] window ids
+    int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [nring]
+    uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32 + nring * 8);  // [kWinTab] window ids
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     if (blockIdx.x == 0 && threadIdx.x < kTraceGroups) *trace_counter(wb.rfetch, in_q ^ 1, threadIdx.x) = 0;  // next trace's
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip
@@ -257,7 +265,7 @@ __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneVi
     if (const uint32_t n = (uint32_t)dyn >> 1)
         while (wr > 1 && (uint64_t)count * n < (uint64_t)nwaves * wr) wr >>= 1;
     const uint32_t nwin = (count + wr - 1) / wr;
-    if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * kStageBytes);
+    if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * stage_bytes(nring));
     // windows: group g owns windows g, g + G, g + 2G, ... (interleaved over the whole queue, whose
     // order is spatially coherent, so every group's share costs about the same), handed out one
     // at a time from the group's counter to the group's waves
@@ -343,13 +351,13 @@ __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneVi
             if (!handed || wave_any(has && sq < flushed + kWinRays)) break;
             const uint32_t wf = wtab[jf % kWinTab];
             const uint32_t fv = wcount(wf);
-            if (lane < fv) wb.hitq[wf * wr + lane] = ring[(flushed + lane) & (kHitRing - 1)];
+            if (lane < fv) wb.hitq[wf * wr + lane] = ring[(flushed + lane) & (nring - 1)];
             flushed += kWinRays;
         }
         // hand the next entries to idle lanes (wave-uniform control)
         const uint64_t need = __ballot(!has);
         if (need) {
-            if (cur == jl * kWinRays + wv && nv > 0 && (jl + 2) * kWinRays - flushed <= kHitRing) {
+            if (cur == jl * kWinRays + wv && nv > 0 && (jl + 2) * kWinRays - flushed <= nring) {
                 if (wl < nv) wray[2 * wl + half] = na;  // next window, if the hit ring has room
                 ++jl;
                 wv = nv;
@@ -381,7 +389,7 @@ __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneVi
         }
         trav_advance<TRAV, COUNT, true>(sc, r, s, stack, blockDim.x, c);
         if (has && trav_finished(s)) {
-            ring[sq & (kHitRing - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
+            ring[sq & (nring - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;
         }
     }
@@ -1645,8 +1653,8 @@ constexpr const void* trace_kernel() {
     else return (const void*)k_wf_trace<LDS, TRAV, COUNT>;
 }
 template <bool LDS, int TRAV, bool COUNT>
-static size_t trace_lds(const SceneView& sc) {
-    const size_t per_wave = TRAV >= 300 ? (size_t)kBfSlots * 64 * 4 : kStageBytes;
+static size_t trace_lds(const SceneView& sc, uint32_t ring = kHitRing) {
+    const size_t per_wave = TRAV >= 300 ? (size_t)kBfSlots * 64 * 4 : stage_bytes(ring);
     constexpr uint32_t B = trace_block<TRAV>();
     return (size_t)sc.max_stack * B * 4 + (B / 64) * per_wave + (LDS ? sc.span_bytes : 0);
 }
@@ -1805,8 +1813,27 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     int np = ws.aux[0] != nullptr ? ws.nparts : 1;
     while (np > 1 && (nframes < (uint32_t)np || wb.capacity / np < npix)) np /= 2;
     const uint32_t F = np * std::max<uint32_t>(1, std::min<uint32_t>((nframes + np - 1) / np, (uint32_t)(wb.capacity / np / npix)));
-    const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc);
+    size_t lds = trace_lds<LDS, TRAV, COUNT>(sc);
     int tblocks = trace_blocks<LDS, TRAV, COUNT>(lds);
+    // k_wf_trace's hit ring: 256 entries when the extra 8 KB per block cost no block per CU (option
+    // trace_ring: 128 / 256 forces one)
+    uint32_t nring = kHitRing;
+    if constexpr (TRAV < 300) {
+        const size_t lds2 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRingMax);
+        static const size_t max_lds = [] {
+            int dev = 0, v = 0;
+            hipGetDevice(&dev);
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+            return (size_t)v;
+        }();
+        const bool fits = lds2 <= max_lds && (ws.trace_ring == (int)kHitRingMax ||
+                                                 (ws.trace_ring <= 0 && trace_blocks<LDS, TRAV, COUNT>(lds2) >= tblocks));
+        if (fits) {
+            lds = lds2;
+            tblocks = trace_blocks<LDS, TRAV, COUNT>(lds2);
+            nring = kHitRingMax;
+        }
+    }
     // k_wf_trace_pk (option packet): its LDS (per-lane replay stacks, per-wave packet stack and hit
     // slots, the scene when it fits) and an occupancy-derived grid
     const size_t pk_lds = (size_t)sc.max_stack * kPkBlock * 4 + (kPkBlock / 64) * kPkLdsPerWave + (LDS ? sc.span_bytes : 0);
@@ -1953,7 +1980,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                           dim3(kPkBlock), pk_lds, st, sc, w, in_q, ws.packet_nodes > 0 ? ws.packet_nodes : kPkMaxNodes);
             else
                 PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlockTr), lds, st, sc,
-                          w, in_q, cnt, watchdog, trace_dyn);
+                          w, in_q, cnt, watchdog, trace_dyn, nring);
             if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
             if ((it & 1) == 0)
                 PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
@@ -2013,6 +2040,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.trace_dyn = lo.trace_dyn;
     ws.trace_sparse = std::max(0, lo.trace_sparse);
     ws.region_perm = lo.region_perm > 0 ? 1 : 0;
+    ws.trace_ring = lo.trace_ring;
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
     ws.packet = lo.packet > 0 ? lo.packet : 0;

@@ -94,6 +94,10 @@ KERNELS = {
     "wavefront_tiles_nogen": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_FUSE_GEN": "0"},
     "wavefront_tiles_persist": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_PERSIST": "1"},
     "wavefront_tiles_trav": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_MAILBOX": "0"},
+    # the traversal kernel's hit ring forced to 128 / 256 entries (default: 256 when it costs no block)
+    "wavefront_ring128": {"PT_KERNEL": "wavefront", "PT_TRACE_RING": "128", "PT_MAILBOX": "0"},
+    "wavefront_ring256_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_RING": "256", "PT_MAILBOX": "0",
+                                 "PT_WF_TRACE_BLOCKS": "1"},
     # camera batches dealt to the fused kernel's regions by a permutation (option region_perm), with
     # the camera paths made by the first fused launch or by k_wf_generate, and on 3 blocks (24 regions)
     "wavefront_region_perm": {"PT_KERNEL": "wavefront", "PT_REGION_PERM": "1"},
@@ -145,7 +149,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
             "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN",
             "PT_TRACE_SPARSE", "PT_BATCH_PIPE", "PT_TILES", "PT_PACKET", "PT_PACKET_NODES", "PT_LEAF_BVH",
-            "PT_LEAF_WALK", "PT_SCATTER", "PT_REGION_PERM")
+            "PT_LEAF_WALK", "PT_SCATTER", "PT_REGION_PERM", "PT_TRACE_RING")
 
 
 @pytest.fixture(params=list(KERNELS))
