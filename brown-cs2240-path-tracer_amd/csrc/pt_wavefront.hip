@@ -238,7 +238,9 @@ constexpr uint32_t trace_block() { return TRAV >= 300 ? kTraceBlock : kTraceBloc
 #if PT_TRACE_WAVES > 0
 #define PT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES, PT_TRACE_WAVES)))
 #else
-#define PT_TRACE_OCC
+// at least 7 waves per SIMD (<= 72 VGPRs): the big-leaf instances sit at 71-73 VGPRs, and 73 would
+// round up to 80 and cost a wave (synthetic 100k / 1M: -10 %, profiles/r03l_ab_vs_r03j.log)
+#define PT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(7)))
 #endif
 template <bool LDS, int TRAV, bool COUNT>
 __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
@@ -248,8 +250,10 @@ __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneVi
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
     char* stage = stage_base + (threadIdx.x / 64u) * stage_bytes(nring);
     float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
-    int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [nring]
-    uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32 + nring * 8);  // [kWinTab] window ids
+    // the ring last, so both arrays sit at constant offsets from `stage` (immediate ds offsets: a
+    // ring-size-dependent offset cost 3 VGPRs and a wave per SIMD in the big-leaf instances)
+    uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32);        // [kWinTab] window ids
+    int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32 + kWinTab * 4);  // [nring]
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     if (blockIdx.x == 0 && threadIdx.x < kTraceGroups) *trace_counter(wb.rfetch, in_q ^ 1, threadIdx.x) = 0;  // next trace's
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip

@@ -38,9 +38,14 @@ def main():
     import torch  # one HIP runtime for the process (see pt_amd/_lib.py)
     torch.cuda.init()
     with tempfile.TemporaryDirectory() as td:
+        if a.scene.startswith("synthetic-"):  # scripts/synth_scene.py: N triangles in the Cornell box
+            sys.path.insert(0, os.path.join(ROOT, "scripts"))
+            import synth_scene
+            xml = synth_scene.write(int(a.scene.split("-")[1]), td)
+        else:
+            xml = os.path.join(ROOT, "scenes", "scene_assets", a.scene + ".xml")
         subprocess.run(["node", os.path.join(ROOT, "brown-cs2240-path-tracer_amd", "node", "bin", "pt-pack.js"),
-                        os.path.join(ROOT, "scenes", "scene_assets", a.scene + ".xml"), td, "--width", str(a.res),
-                        "--height", str(a.res)], check=True, capture_output=True)
+                        xml, td, "--width", str(a.res), "--height", str(a.res)], check=True, capture_output=True)
         tri = np.fromfile(os.path.join(td, "triangle_data.f32"), np.float32)
         bvh = np.fromfile(os.path.join(td, "bvh_data.f32"), np.float32)
         meta = np.fromfile(os.path.join(td, "meta.f32"), np.float32)
