@@ -208,10 +208,15 @@ constexpr uint32_t kWinRays = 32;
 constexpr uint32_t kHitRing = 128;
 constexpr uint32_t kHitRingMax = 256;
 // window ids of the windows between the last flushed and the prefetched one: the ring holds
-// kHitRing / kWinRays windows, plus the one in registers
-constexpr uint32_t kWinTab = 2 * kHitRingMax / kWinRays;
-static_assert(kWinTab >= kHitRingMax / kWinRays + 2, "wtab must name every window the ring can hold");
-__host__ __device__ constexpr uint32_t stage_bytes(uint32_t ring) { return kWinRays * 32 + ring * 8 + kWinTab * 4; }
+// RING / kWinRays windows, plus the one in registers (a compile-time size per kernel instance: a
+// ring size read at run time measured 10 % slower on the deep synthetic trees)
+__host__ __device__ constexpr uint32_t win_tab(uint32_t ring) { return 2 * ring / kWinRays > 8 ? 2 * ring / kWinRays : 8; }
+static_assert(win_tab(kHitRingMax) >= kHitRingMax / kWinRays + 2, "wtab must name every window the ring can hold");
+static_assert(win_tab(kHitRing) >= kHitRing / kWinRays + 2, "wtab must name every window the ring can hold");
+__host__ __device__ constexpr uint32_t stage_bytes(uint32_t ring) { return kWinRays * 32 + ring * 8 + win_tab(ring) * 4; }
+// the traversal flavours that have a 256-entry-ring instance (the defaults: lean16 + fast rcp,
+// with and without big-leaf turns); the others always use 128
+constexpr bool has_big_ring(int trav) { return trav == 17 || trav == 177; }
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 // k_wf_trace's block (the traversal scenes): its LDS is per lane (the traversal stack, max_stack
 // words) and per wave (kStageBytes), so the block size sets the LDS granularity, not the total
@@ -242,18 +247,17 @@ constexpr uint32_t trace_block() { return TRAV >= 300 ? kTraceBlock : kTraceBloc
 // round up to 80 and cost a wave (synthetic 100k / 1M: -10 %, profiles/r03l_ab_vs_r03j.log)
 #define PT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(7)))
 #endif
-template <bool LDS, int TRAV, bool COUNT>
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing>
 __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
-                                                          uint32_t watchdog, int dyn, uint32_t nring) {
+                                                          uint32_t watchdog, int dyn) {
+    constexpr uint32_t nring = RING, kWinTab = win_tab(RING);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;
     char* stage_base = smem + (uint32_t)sc.max_stack * blockDim.x * 4u;
     char* stage = stage_base + (threadIdx.x / 64u) * stage_bytes(nring);
     float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
-    // the ring last, so both arrays sit at constant offsets from `stage` (immediate ds offsets: a
-    // ring-size-dependent offset cost 3 VGPRs and a wave per SIMD in the big-leaf instances)
-    uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32);        // [kWinTab] window ids
-    int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32 + kWinTab * 4);  // [nring]
+    int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [RING]
+    uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32 + RING * 8);  // [kWinTab] window ids
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     if (blockIdx.x == 0 && threadIdx.x < kTraceGroups) *trace_counter(wb.rfetch, in_q ^ 1, threadIdx.x) = 0;  // next trace's
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip
@@ -1822,7 +1826,8 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     // k_wf_trace's hit ring: 256 entries when the extra 8 KB per block cost no block per CU (option
     // trace_ring: 128 / 256 forces one)
     uint32_t nring = kHitRing;
-    if constexpr (TRAV < 300) {
+    (void)nring;
+    if constexpr (TRAV < 300 && has_big_ring(TRAV)) {
         const size_t lds2 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRingMax);
         static const size_t max_lds = [] {
             int dev = 0, v = 0;
@@ -1983,8 +1988,19 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_pk<LDS, ((TRAV / 10) & 1) != 0>), dim3(pk_blocks(pk_lds)),
                           dim3(kPkBlock), pk_lds, st, sc, w, in_q, ws.packet_nodes > 0 ? ws.packet_nodes : kPkMaxNodes);
             else
-                PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlockTr), lds, st, sc,
-                          w, in_q, cnt, watchdog, trace_dyn, nring);
+            {
+                bool launched = false;
+                if constexpr (has_big_ring(TRAV)) {
+                    if (nring == kHitRingMax) {
+                        PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, kHitRingMax>), dim3(tblocks),
+                                  dim3(kTraceBlockTr), lds, st, sc, w, in_q, cnt, watchdog, trace_dyn);
+                        launched = true;
+                    }
+                }
+                if (!launched)
+                    PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT>), dim3(tblocks), dim3(kTraceBlockTr), lds, st,
+                              sc, w, in_q, cnt, watchdog, trace_dyn);
+            }
             if (stagger) HIP_RETURN_IF(hipEventRecord(ws.traced[h], st));
             if ((it & 1) == 0)
                 PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
