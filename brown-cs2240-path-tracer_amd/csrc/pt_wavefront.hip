@@ -243,9 +243,10 @@ constexpr uint32_t trace_block() { return TRAV >= 300 ? kTraceBlock : kTraceBloc
 #if PT_TRACE_WAVES > 0
 #define PT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES, PT_TRACE_WAVES)))
 #else
-// at least 7 waves per SIMD (<= 72 VGPRs): the big-leaf instances sit at 71-73 VGPRs, and 73 would
-// round up to 80 and cost a wave (synthetic 100k / 1M: -10 %, profiles/r03l_ab_vs_r03j.log)
-#define PT_TRACE_OCC __attribute__((amdgpu_waves_per_eu(7)))
+// no occupancy attribute: the big-leaf instances take 71 VGPRs (7 waves per SIMD); forcing
+// amdgpu_waves_per_eu(7) made them 72 and 11 % slower on the 100k synthetic scene (in process,
+// profiles/r03m_ab_trace_occ.log)
+#define PT_TRACE_OCC
 #endif
 template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing>
 __global__ __launch_bounds__(kTraceBlockTr) PT_TRACE_OCC void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
