@@ -100,14 +100,21 @@ def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int
     key = f"{W}x{H}x{spp}x{depth}x{world}"
     cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix) and field in v}
     # the timed instances: COUNT=false (template argument 4 of k_wf_step_bf<EXT, LDS, rcp, COUNT,
-    # CULL, GEN>, the last one of the others) and no opt-in CULL; averaged per launch, weighted
-    # by their dispatch counts when the summary has them (extension, shadow and the one camera
-    # GEN launch per batch), else the plain mean of the instances
+    # GEN> and of k_wf_trace<LDS, TRAV, COUNT, RING, S16> counted from 1 as 3; round 3's profiles name
+    # a sixth k_wf_step_bf argument, the removed opt-in CULL, after COUNT); averaged per launch,
+    # weighted by their dispatch counts when the summary has them (extension, shadow and the one
+    # camera GEN launch per batch), else the plain mean of the instances (GEN left out)
     def timed_instance(name):
         args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")]
         if name.startswith("k_wf_step_bf<"):
-            return len(args) >= 4 and args[3] == "false" and (len(args) < 5 or args[4] == "false")
+            return len(args) >= 4 and args[3] == "false" and (len(args) < 6 or args[4] == "false")
+        if name.startswith("k_wf_trace<"):
+            return len(args) >= 3 and args[2] == "false"
         return bool(args) and args[-1] == "false"
+
+    def gen_instance(name):
+        args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")]
+        return name.startswith("k_wf_step_bf<") and args[-1] == "true"
 
     timed = [k for k in cands if timed_instance(k)] or list(cands)
     if not timed:
@@ -116,7 +123,7 @@ def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int
     wts = [cands[k].get("dispatches") for k in timed]
     if all(wts):
         return sum(cands[k][field] * w for k, w in zip(timed, wts)) / sum(wts), src
-    timed = [k for k in timed if not k.endswith("true>")] or timed  # no counts: leave GEN out
+    timed = [k for k in timed if not gen_instance(k)] or timed  # no counts: leave GEN out
     return sum(cands[k][field] for k in timed) / len(timed), src
 
 
@@ -228,6 +235,10 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch HIP events")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option (pt_set_option) for A/B and profiling runs; repeatable")
+    ap.add_argument("--share-of", type=int, default=0, metavar="N",
+                    help="one GPU renders exactly rank --share-rank's frames of an N-rank run (frames r, r+N, ...; no "
+                         "reduce): the per-rank share whose time bounds N-GPU strong scaling (DESIGN.md section 7)")
+    ap.add_argument("--share-rank", type=int, default=0)
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the rank plumbing (launch, sharding, reduce, timing, JSON line); renders "
                          "nothing and reports no value")
@@ -278,6 +289,10 @@ def main():
     scene = pt_amd.Scene(tri, bvh, device=local_rank)
     # frames of this rank: k = rank, rank + world, ... (pt_amd/shard.py)
     frame0, nframes, fstride = frames_for_rank(rank, world, args.spp)
+    if args.share_of > 1:  # one rank's share of an N-rank run, rendered alone
+        if world != 1:
+            raise SystemExit("--share-of times one rank's share on one GPU (no launcher)")
+        frame0, nframes, fstride = frames_for_rank(args.share_rank, args.share_of, args.spp)
     stream = torch.cuda.Stream(device=dev)
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
 
@@ -337,7 +352,7 @@ def main():
         elapsed = float(t.item())
 
     scene.check()  # a device-side failure of any timed render (pt_scene_check) fails the bench
-    total_samples = W * H * args.spp
+    total_samples = W * H * (nframes if args.share_of > 1 else args.spp)
     ms_per_step = elapsed / args.steps * 1e3
     value = total_samples / (elapsed / args.steps) / 1e6
     r_ms = float(np.mean(render_ms))
@@ -362,12 +377,14 @@ def main():
     pipeline = b_alg / (r_ms * 1e-3) / 1e9
 
     if rank == 0:
-        prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<", "k_wf_persist_bf<")}
+        prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<",)}
         pre = prefixes.get(kernel, (kernel + "<",))
-        traffic = load_traffic(pre, W, H, args.spp, args.depth, world)
-        valu = load_traffic(pre, W, H, args.spp, args.depth, world, field="valu_issue")
+        # the committed PMC / trace figures describe the full configuration (not a rank's share)
+        full = args.share_of <= 1
+        traffic = load_traffic(pre, W, H, args.spp, args.depth, world) if full else None
+        valu = load_traffic(pre, W, H, args.spp, args.depth, world, field="valu_issue") if full else None
         valu_cal = traffic_note(pre, W, H, args.spp, args.depth, world, "valu_issue_calibration")
-        tu = load_trace_union(W, H, args.spp, args.depth, world)
+        tu = load_trace_union(W, H, args.spp, args.depth, world) if full else None
         if tu and tu.get("kernel") != kernel:
             tu = None
         out = {
@@ -393,7 +410,10 @@ def main():
                        "mode": args.mode, "bvh": args.bvh, "samples_per_step": total_samples,
                        "ranks": ranks_seen, "backend": backend if world > 1 else None,
                        "options": dict(kv.partition("=")[::2] for kv in args.opt) or None,
-                       "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size)},
+                       "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size),
+                       "share": ({"of": args.share_of, "rank": args.share_rank, "frames": nframes, "stride": fstride,
+                                  "implied_aggregate_before_reduce": round(value * args.share_of, 3)}
+                                 if args.share_of > 1 else None)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic[0] * launches_per_render / (busy_ms * 1e-3) / 1e9 if traffic and busy_ms else None,

@@ -69,19 +69,13 @@ struct OptSpec {
 constexpr OptSpec kOptSpecs[] = {
     {"kernel", OPT_ENUM, "auto|mega|wavefront|literal"},
     {"trav", OPT_ENUM, "nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32"},
-    {"lds", OPT_BOOL, nullptr},          {"fastrcp", OPT_BOOL, nullptr},     {"pipe", OPT_BOOL, nullptr},
-    {"ifif", OPT_BOOL, nullptr},         {"dual", OPT_BOOL, nullptr},        {"stagger", OPT_BOOL, nullptr},
+    {"lds", OPT_BOOL, nullptr},          {"fastrcp", OPT_BOOL, nullptr},     {"dual", OPT_BOOL, nullptr},
     {"fuse", OPT_BOOL, nullptr},         {"fuse_gen", OPT_BOOL, nullptr},    {"bf", OPT_BOOL, nullptr},
-    {"mailbox", OPT_BOOL, nullptr},      {"persist", OPT_BOOL, nullptr},     {"regen", OPT_BOOL, nullptr},
-    {"regen_bf", OPT_BOOL, nullptr},     {"bf_stackless", OPT_BOOL, nullptr}, {"trace_dyn", OPT_BOOL, nullptr},
-    {"trace_sparse", OPT_INT, nullptr},
-    {"tiles", OPT_BOOL, nullptr},        {"batch_pipe", OPT_BOOL, nullptr},  {"scatter", OPT_BOOL, nullptr},
-    {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
-    {"packet", OPT_INT, nullptr},       {"packet_nodes", OPT_INT, nullptr},
-    {"parts", OPT_INT, nullptr},         {"cull", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
+    {"mailbox", OPT_BOOL, nullptr},      {"bf_stackless", OPT_BOOL, nullptr}, {"trace_sparse", OPT_INT, nullptr},
+    {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},   {"stack16", OPT_BOOL, nullptr},
+    {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
-    {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr},
-    {"regen_target", OPT_INT, nullptr},  {"trace_watchdog", OPT_INT, nullptr},
+    {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
     {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
     {"reduce", OPT_ENUM, "rccl|ordered"},
@@ -147,8 +141,6 @@ struct HostLayout {
     std::vector<Light> lights;
     std::vector<uint64_t> lmask;  // mailbox scenes: uid set per leaf, indexed by first record
     std::vector<float4> tnorm;    // vertex-normal mode: 3 per record (SceneView::tnorm)
-    std::vector<float4> cull;     // mailbox scenes: 3 per distinct entry (SceneView::cull)
-    std::vector<float> bfpair;    // mailbox scenes: 20 per pair of distinct entries (SceneView::bfpair)
     std::vector<BfNode> bfnode;   // mailbox scenes with <= 64 internal nodes, <= 63 entries (SceneView::bfnode)
     std::vector<int32_t> bfmap;
     std::vector<LNode> lnodes;    // leaf BVHs (SceneView::lnodes), and per such leaf (first record, entries, nodes)
@@ -296,8 +288,7 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
         }
         const int32_t U = (int32_t)first.size();
         L.mailbox = U >= 1 && U <= 64;
-        // every record carries its entry's uid (k_wf_trace_pk keys its phase-1 hits by it; the
-        // mailbox scenes renumber below)
+        // every record carries its entry's uid (the mailbox scenes renumber below)
         for (size_t r = 0; r < entry.size(); ++r) L.tris[r].uid = uid[r];
         if (L.mailbox) {
             const bool rev = opts_snapshot().is("mb_uid_order", "reverse");
@@ -311,38 +302,6 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             for (size_t k = 0; k < first.size(); ++k)
                 for (int q = 0; q < 3; ++q) un[3 * (size_t)uid[first[k]] + q] = L.tnorm[3 * first[k] + q];
             L.tnorm.insert(L.tnorm.end(), un.begin(), un.end());
-            // entry cull records (bf_cull_mask): the box of the triangle the test sees (v0, v0 + e1,
-            // v0 + e2 of the stored record), tau = 1e-2 |e1| |e2| (the bundle's |det| floor, per
-            // unit |d|), the margin factor and w = 2 |v0| + |e1| + |e2| (margin = factor *
-            // (2 sqrt(3) max|o| + w), the bound on the test's rounding), e1 x e2
-            L.cull.resize(3 * (size_t)U);
-            for (int32_t u = 0; u < U; ++u) {
-                const Tri& t = L.tris[(size_t)(L.mb_base + u)];
-                const double v0[3] = {t.q0[0], t.q0[1], t.q0[2]}, e1[3] = {t.q0[3], t.q1[0], t.q1[1]},
-                             e2[3] = {t.q1[2], t.q1[3], t.e2z};
-                double lo[3], hi[3], n[3];
-                for (int a = 0; a < 3; ++a) {
-                    lo[a] = std::min({v0[a], v0[a] + e1[a], v0[a] + e2[a]});
-                    hi[a] = std::max({v0[a], v0[a] + e1[a], v0[a] + e2[a]});
-                }
-                n[0] = e1[1] * e2[2] - e1[2] * e2[1];
-                n[1] = e1[2] * e2[0] - e1[0] * e2[2];
-                n[2] = e1[0] * e2[1] - e1[1] * e2[0];
-                const double l1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
-                const double l2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
-                const double lv = std::sqrt(v0[0] * v0[0] + v0[1] * v0[1] + v0[2] * v0[2]);
-                auto dn = [](double x) { return std::nextafter((float)x, -INFINITY); };
-                auto upf = [](double x) { return std::nextafter((float)x, INFINITY); };
-                L.cull[3 * (size_t)u + 0] = make_float4(dn(lo[0]), dn(lo[1]), dn(lo[2]), upf(1e-2 * l1 * l2));
-                L.cull[3 * (size_t)u + 1] = make_float4(upf(hi[0]), upf(hi[1]), upf(hi[2]), 4e-3f);
-                L.cull[3 * (size_t)u + 2] = make_float4((float)n[0], (float)n[1], (float)n[2], upf(2.0 * lv + l1 + l2));
-            }
-            L.bfpair.assign(40 * (size_t)((U + 3) / 4), 0.0f);  // whole quads of entries (bf_quads); zero entries never hit
-            for (int32_t u = 0; u < U; ++u) {
-                const Tri& t = L.tris[(size_t)(L.mb_base + u)];
-                const float c[9] = {t.q0[0], t.q0[1], t.q0[2], t.q0[3], t.q1[0], t.q1[1], t.q1[2], t.q1[3], t.e2z};
-                for (int k = 0; k < 9; ++k) L.bfpair[20 * (size_t)(u / 2) + 2 * k + (u & 1)] = c[k];
-            }
             L.lmask.assign(std::max<size_t>(1, entry.size()), 0);
             for (const auto& lr : leaf_ranges)
                 for (int32_t k = 0; k < lr.second; ++k) L.lmask[(size_t)lr.first] |= 1ull << uid[(size_t)(lr.first + k)];
@@ -661,9 +620,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_bfmap = align_up(o_bfnode + L.bfnode.size() * sizeof(BfNode), 16);
     const size_t o_cnt = align_up(o_bfmap + L.bfmap.size() * sizeof(int32_t), 256);
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
-    const size_t o_cull = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
-    const size_t o_pair = align_up(o_cull + std::max<size_t>(1, L.cull.size()) * sizeof(float4), 256);
-    const size_t o_lnode = align_up(o_pair + std::max<size_t>(1, L.bfpair.size()) * sizeof(float), 256);
+    const size_t o_lnode = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
     const size_t total = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
     pt_scene* s = new pt_scene();
@@ -679,8 +636,6 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_bfnode, L.bfnode.data(), L.bfnode.size() * sizeof(BfNode)) != hipSuccess ||
         up(o_bfmap, L.bfmap.data(), L.bfmap.size() * sizeof(int32_t)) != hipSuccess ||
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
-        up(o_cull, L.cull.data(), L.cull.size() * sizeof(float4)) != hipSuccess ||
-        up(o_pair, L.bfpair.data(), L.bfpair.size() * sizeof(float)) != hipSuccess ||
         up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
         up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess) {
         pt_scene_destroy(s);
@@ -707,9 +662,6 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.mailbox = L.mailbox ? 1 : 0;
     s->view.tnorm = reinterpret_cast<const float4*>(base + o_tn);
     s->view.vnormals = 0;
-    s->view.cull = reinterpret_cast<const float4*>(base + o_cull);
-    s->view.cull_its = 0;  // per launch (launch_wavefront)
-    s->view.bfpair = reinterpret_cast<const float*>(base + o_pair);
     s->view.lnodes = L.lnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_lnode);
     s->view.ltris = L.lnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_lidx);
     s->leaf_min = L.leaf_min;
@@ -736,15 +688,8 @@ void pt_scene_destroy(pt_scene* s) {
     for (int h = 0; h < kMaxParts; ++h) {
         if (s->ws.aux[h]) { hipStreamSynchronize(s->ws.aux[h]); hipStreamDestroy(s->ws.aux[h]); }
         if (s->ws.join[h]) hipEventDestroy(s->ws.join[h]);
-        if (h < 2 && s->ws.traced[h]) hipEventDestroy(s->ws.traced[h]);
-        if (h < 2 && s->ws.acc_done[h]) hipEventDestroy(s->ws.acc_done[h]);
     }
     if (s->ws.fork) hipEventDestroy(s->ws.fork);
-    if (s->ws.mid) hipEventDestroy(s->ws.mid);
-    for (int h = 0; h < kMaxParts; ++h)
-        for (int k = 0; k < 2; ++k)
-            if (s->ws.poll_ev[h][k]) hipEventDestroy(s->ws.poll_ev[h][k]);
-    if (s->ws.h_poll) hipHostFree(s->ws.h_poll);
     if (s->d_rad) hipFree(s->d_rad);
     if (s->d_peer) hipFree(s->d_peer);
     if (s->d_rgba) hipFree(s->d_rgba);
@@ -802,11 +747,6 @@ int make_params(const float* meta, int max_depth, FrameParams& fp) {
 // leaves (MedievalBoat 256^2 x 1: 62 / 35); other scenes from about 2^19 paths (Glossy 512^2 x 1:
 // 7.1 / 9.1, 512^2 x 2: 13.1 / 9.6).
 constexpr uint64_t kWfAutoMinPaths = 1ull << 19;
-constexpr int kTilesDefault = 0;
-
-
-// two parts run their batches half a batch apart (option batch_pipe; wf_render_t)
-constexpr int kBatchPipeDefault = 0;
 // k_wf_trace narrows its windows when 32-entry ones would keep < 1/4 of the waves busy (option
 // trace_sparse=n; in-process A/B: MedievalBoat +16 %, Glossy and the synthetic scenes +-0.5 %)
 constexpr int kTraceSparseDefault = 4;
@@ -827,28 +767,17 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     }
     lo.lds = o.flag("lds", 1) != 0;
     lo.fast_rcp = o.flag("fastrcp", lo.fast_rcp);
-    lo.pipe = o.flag("pipe", lo.pipe);
-    lo.ifif = o.flag("ifif", lo.ifif);
     lo.parts = (int)o.num("parts", lo.parts);
-    lo.cull = (int)o.num("cull", lo.cull);
     lo.fuse_gen = o.flag("fuse_gen", lo.fuse_gen);
     lo.dual = o.flag("dual", lo.dual);
-    lo.stagger = o.flag("stagger", lo.stagger);
-    lo.pipeline = o.flag("batch_pipe", kBatchPipeDefault);
-    lo.regen_bf = o.flag("regen_bf", lo.regen_bf);
-    lo.persist = o.flag("persist", lo.persist);
     lo.fuse = o.flag("fuse", lo.fuse);
     lo.bf = o.flag("bf", lo.bf);
     lo.mailbox = o.flag("mailbox", lo.mailbox);
-    lo.regen = o.flag("regen", lo.regen);
-    lo.regen_target = o.num("regen_target", lo.regen_target);
     lo.sort = (int)o.num("sort", lo.sort);  // 1 / 8: direction octant; 64: + origin octant; 512: + 4^3 origin cells
-    lo.packet = (int)o.num("packet", lo.packet);
-    lo.packet_nodes = (int)o.num("packet_nodes", 0);
-    lo.trace_dyn = o.flag("trace_dyn", lo.trace_dyn);
     lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
     lo.region_perm = o.flag("region_perm", kRegionPermDefault);
     lo.trace_ring = (int)o.num("trace_ring", 0);
+    lo.stack16 = o.flag("stack16", 1);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);
@@ -867,10 +796,6 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
 // (probe of option wf_paths)
 constexpr uint64_t kWfTargetPaths = 64ull << 20;
 constexpr int kBigLeafDefault = 128;
-
-// radiance of finished paths: the batch's (capacity), or with streaming regeneration a whole
-// group of frames, up to kRadMaxPaths (12 B per path: 3.2 GB)
-constexpr uint64_t kRadMaxPaths = 1ull << 28;
 
 int ensure_rad(pt_scene* s, uint64_t paths) {
     if (s->d_rad && s->rad_cap >= paths) { s->wf.rad = s->d_rad; s->wf.rad_cap = s->rad_cap; return PT_OK; }
@@ -891,18 +816,15 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     if (paths > 0x7fffffffull) return fail(PT_ERR_INVALID, "image too large for one wavefront batch");
     if (s->d_wf) { hipDeviceSynchronize(); hipFree(s->d_wf); s->d_wf = nullptr; s->wf.capacity = 0; }
     const size_t n = paths;
-    // queue arrays carry slack so that each half can be cut into up to kQueueSlackRegions / 1.5
-    // regions of a whole number of 64-entry batches holding all its paths (k_wf_step_bf,
-    // k_wf_persist_bf)
+    // queue arrays carry slack so that each part can be cut into up to kRegions regions of a whole
+    // number of 64-entry batches holding all its paths (k_wf_step_bf)
     const size_t qn = n + 2 * (size_t)kQueueSlackRegions * 64;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
     size_t oq[6];
     for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * qn);
     const size_t o_p0 = take(16 * qn), o_p1 = take(16 * qn), o_p2 = take(8 * qn), o_hit = take(8 * qn),
-                 o_ctl = take(4 * kMaxParts * WF_CTL_WORDS), o_rcnt = take(4 * kMaxParts * 3 * kRegions),
-                 o_rgen = take(4 * kMaxParts * 2 * kRegions), o_live = take(4 * kMaxParts * kLiveRing),
-                 o_fetch = take(4 * kMaxParts * 3 * kRegions * kFetchStride);
+                 o_ctl = take(4 * kMaxParts * WF_CTL_WORDS), o_rcnt = take(4 * kMaxParts * 3 * kRegions);
     if (hipMalloc(&s->d_wf, off) != hipSuccess) {
         s->d_wf = nullptr;
         (void)hipGetLastError();  // the failed allocation is reported here, not by a later call
@@ -918,9 +840,6 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     w.hitq = reinterpret_cast<int2*>(b + o_hit);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
     w.rcnt = reinterpret_cast<uint32_t*>(b + o_rcnt);
-    w.rgen = reinterpret_cast<uint32_t*>(b + o_rgen);
-    w.live = reinterpret_cast<uint32_t*>(b + o_live);
-    w.rfetch = reinterpret_cast<uint32_t*>(b + o_fetch);
     if (hipMemset(w.ctl, 0, 4 * kMaxParts * WF_CTL_WORDS) != hipSuccess ||
         hipMemset(w.rcnt, 0, 4 * kMaxParts * 3 * kRegions) != hipSuccess)
         return fail(PT_ERR_HIP, "hipMemset wavefront control words");
@@ -929,14 +848,6 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
         for (int h = 0; h < kMaxParts && ok; ++h)
             ok = hipStreamCreateWithFlags(&s->ws.aux[h], hipStreamNonBlocking) == hipSuccess &&
                  hipEventCreateWithFlags(&s->ws.join[h], hipEventDisableTiming) == hipSuccess;
-        for (int h = 0; h < 2 && ok; ++h)
-            ok = hipEventCreateWithFlags(&s->ws.traced[h], hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&s->ws.acc_done[h], hipEventDisableTiming) == hipSuccess;
-        if (ok) ok = hipEventCreateWithFlags(&s->ws.mid, hipEventDisableTiming) == hipSuccess;
-        for (int h = 0; h < kMaxParts && ok; ++h)
-            for (int k = 0; k < 2 && ok; ++k)
-                ok = hipEventCreateWithFlags(&s->ws.poll_ev[h][k], hipEventDisableTiming) == hipSuccess;
-        if (ok) ok = hipHostMalloc(reinterpret_cast<void**>(&s->ws.h_poll), 2 * kMaxParts * sizeof(uint32_t)) == hipSuccess;
         if (!ok) return fail(PT_ERR_HIP, "creating the wavefront's streams");
     }
     if (!s->h_ctl) {
@@ -977,8 +888,8 @@ int take_watchdog(pt_scene* s) {
     char msg[360];
     std::snprintf(msg, sizeof(msg),
                   "wavefront trace gave up after its watchdog limit (result invalid); first wave: count=%u "
-                  "nwaves=%u w=%u g=%u G=%u jl=%u wv=%u nv=%u cur=%u flushed=%u in_flight=%u mask=%08x%08x queue=%u",
-                  v[0], v[1], v[2], v[3], v[13], v[4], v[5], v[6], v[7], v[8], v[9], v[11], v[10], v[12]);
+                  "nwaves=%u w=%u jl=%u wv=%u nv=%u cur=%u flushed=%u in_flight=%u mask=%08x%08x queue=%u",
+                  v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[10], v[9], v[11]);
     return fail(PT_ERR_HIP, msg);
 }
 
@@ -1004,13 +915,14 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     // big leaves (lean traversal): a ray reaching a leaf of >= big_leaf entries has it tested by the
     // whole wave (pt_device.h big_turn); default 128 (MedievalBoat 2.3x, in-process A/B; 64 is 1.5 %
     // faster there but 12 % slower on the 1M-triangle synthetic scene, whose many 64..127-entry
-    // leaves waste half a cooperative step each); option big_leaf=n sets it, 0 turns it off
+    // leaves waste half a cooperative step each); option big_leaf=n sets it, 0 turns big-leaf
+    // turns and leaf chunks off
     {
         const long big = o.num("big_leaf", kBigLeafDefault);
         view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? (int32_t)big : 0;
         // leaf BVHs (built at pt_scene_create, option leaf_bvh): lanes park at every leaf that has
         // chunks and test them chunk by chunk (chunk_turn); option leaf_walk=0 keeps them out (A/B)
-        if (s->leaf_min > 0 && o.flag("leaf_walk", 1) != 0)
+        if (big > 0 && s->leaf_min > 0 && o.flag("leaf_walk", 1) != 0)
             view.big_leaf = view.big_leaf > 0 ? std::min<int32_t>(view.big_leaf, s->leaf_min) : s->leaf_min;
         else
             view.lnodes = nullptr;
@@ -1018,19 +930,6 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);
-    // camera paths of the wavefront batches in 8x8 pixel tiles (slot_path; every path's bits are the same)
-    fp.tiles = o.flag("tiles", kTilesDefault);
-    // camera paths scattered over the image (slot_path; every path's bits are the same; opt-in:
-    // 4096^2 x 32, CornellBox: 2482 -> 2669 Msamples/s, but 1024^2: 2795 -> 2652 and Glossy -7.5 %,
-    // profiles/r03g_ab_scatter.txt; the default region permutation gives the 4096^2 gain without
-    // the 1024^2 loss, profiles/r03h_ab_region_perm.txt)
-    if (o.flag("scatter", 0) && !fp.tiles) {
-        fp.tiles = 2;
-        uint64_t m = std::max<uint64_t>(1, (uint64_t)((double)npix * 0.6180339887498949));
-        auto gcd = [](uint64_t a, uint64_t b) { while (b) { const uint64_t t = a % b; a = b; b = t; } return a; };
-        while (gcd(m, npix) != 1) ++m;
-        fp.scatter_mul = (uint32_t)(m % npix);
-    }
     if ((rc = take_watchdog(s)) != PT_OK) return rc;  // an earlier asynchronous render failed
     if (lo.wavefront) {
         // the target in whole pairs of frames (a batch's two parts take whole frames each): 4096^2
@@ -1053,15 +952,7 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         for (uint64_t w = want; rc2 == PT_ERR_NOMEM && w > floor_paths;)
             rc2 = ensure_wavefront(s, w = std::max<uint64_t>(w / 2, floor_paths));
         if (rc2 != PT_OK) return rc2;
-        // radiance: the batch's paths; with streaming regeneration (opt-in, when it can run) the
-        // call's frames up to kRadMaxPaths, whole frames
-        const bool regen = lo.regen > 0 && s->ws.h_poll != nullptr;
-        // batch pipelining (more than one batch): two batches' radiance, one per buffer
-        const uint64_t rad_want = regen ? std::max<uint64_t>(s->wf.capacity, std::min<uint64_t>(all, std::max<uint64_t>(npix, kRadMaxPaths / npix * npix)))
-                                  : lo.pipeline > 0 && all > s->wf.capacity ? 2ull * s->wf.capacity
-                                                                           : s->wf.capacity;
-        rc2 = ensure_rad(s, rad_want);
-        if (rc2 == PT_ERR_NOMEM && rad_want > s->wf.capacity) rc2 = ensure_rad(s, s->wf.capacity);
+        rc2 = ensure_rad(s, s->wf.capacity);
         if (rc2 != PT_OK) return rc2;
         HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
                                  stream, s->ws));

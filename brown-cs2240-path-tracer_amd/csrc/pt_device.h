@@ -10,6 +10,29 @@ namespace pt {
 
 constexpr int kStackMax = 32;  // > max traversal stack of any accepted tree (host checks)
 
+// Per-lane traversal stacks in LDS, lane-minor (the 64 entries of a wave at one level are
+// contiguous, so a stack access is conflict-free).  LStack32: entry k of a lane at word
+// k * stride.  LStack16 (trees below 65,536 nodes: entries are node indices): two levels share the
+// lane's word — entry k in half k & 1 of word k / 2 — half the LDS of 32-bit entries.
+struct LStack32 {
+    int32_t* p;
+    int stride;
+    static __device__ __forceinline__ LStack32 make(char* base, int stride) {
+        return LStack32{reinterpret_cast<int32_t*>(base) + threadIdx.x, stride};
+    }
+    __device__ __forceinline__ void put(int k, int v) const { p[k * stride] = v; }
+    __device__ __forceinline__ int get(int k) const { return p[k * stride]; }
+};
+struct LStack16 {
+    uint16_t* p;  // this lane's word of levels 0 and 1
+    int stride2;  // u16 between level pairs: 2 * stride
+    static __device__ __forceinline__ LStack16 make(char* base, int stride) {
+        return LStack16{reinterpret_cast<uint16_t*>(base) + 2 * threadIdx.x, 2 * stride};
+    }
+    __device__ __forceinline__ void put(int k, int v) const { p[(k >> 1) * stride2 + (k & 1)] = (uint16_t)v; }
+    __device__ __forceinline__ int get(int k) const { return p[(k >> 1) * stride2 + (k & 1)]; }
+};
+
 struct Ray {
     f3 o, d, inv;
 };
@@ -59,10 +82,10 @@ __device__ __forceinline__ void test_tri(const Tri* __restrict__ tris, int i, co
 // private stack; popping skips them, so the live entries behave exactly like
 // "pop node, push left then right (right on top)".  Here the right child is
 // taken directly and the left one parked on this lane's LDS stack
-// (stack[k * stride], lane-minor: conflict-free).  Same visit order, same
+// (stack.get(k), lane-minor: conflict-free).  Same visit order, same
 // pruning with the box's exit distance, same strict-< closest hit.
-template <bool COUNT>
-__device__ __forceinline__ int trace(const SceneView& sc, const Ray& r, float& t_out, int32_t* stack, int stride,
+template <bool COUNT, class ST>
+__device__ __forceinline__ int trace(const SceneView& sc, const Ray& r, float& t_out, const ST& stack,
                                      Counters& cnt) {
     float best_t = -1.0f;
     int best = -1;
@@ -85,7 +108,7 @@ __device__ __forceinline__ int trace(const SceneView& sc, const Ray& r, float& t
         bool tl = li && !lleaf && !(best_t > 0.0f && ld > best_t);
         bool tr = ri && !rleaf && !(best_t > 0.0f && rd > best_t);
         if (tl && tr) {
-            stack[sp * stride] = d.x;
+            stack.put(sp, d.x);
             ++sp;
             node = d.y;
         } else if (tl) {
@@ -95,7 +118,7 @@ __device__ __forceinline__ int trace(const SceneView& sc, const Ray& r, float& t
         } else {
             if (sp == 0) break;
             --sp;
-            node = stack[sp * stride];
+            node = stack.get(sp);
         }
     }
     t_out = best_t;
@@ -125,8 +148,8 @@ __device__ __forceinline__ void trav_init(TravState& s, bool active) {
 }
 
 // One scheduling step for the whole wave.  Returns false once no lane has work left.
-template <bool COUNT>
-__device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, TravState& s, int32_t* stack, int stride,
+template <bool COUNT, class ST>
+__device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, TravState& s, const ST& stack,
                                           Counters& cnt) {
     const uint64_t want_leaf = __ballot(!s.done && s.in_leaf);
     const uint64_t want_node = __ballot(!s.done && !s.in_leaf);
@@ -160,7 +183,7 @@ __device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, Tra
         const bool tl = s.lint && !(s.best_t > 0.0f && s.ld > s.best_t);
         const bool tr = s.rint && !(s.best_t > 0.0f && s.rd > s.best_t);
         if (tl && tr) {
-            stack[s.sp * stride] = s.lc;
+            stack.put(s.sp, s.lc);
             ++s.sp;
             s.node = s.rc;
         } else if (tl) {
@@ -171,7 +194,7 @@ __device__ __forceinline__ bool trav_step(const SceneView& sc, const Ray& r, Tra
             s.done = true;
         } else {
             --s.sp;
-            s.node = stack[s.sp * stride];
+            s.node = stack.get(s.sp);
         }
     }
     return true;
@@ -220,9 +243,9 @@ __device__ __forceinline__ bool tri_hit(const Tri* __restrict__ tris, int i, con
 // per VALU instruction).  All lanes run the chosen unit on a valid record; lanes for which
 // the unit is not meant keep their state.  The push/pop decision stores unconditionally
 // into stack[sp], the free slot just above the lane's stack top, and reads stack[sp-1].
-template <bool COUNT>
-__device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r, TravState& s, int32_t* stack,
-                                               int stride, Counters& cnt) {
+template <bool COUNT, class ST>
+__device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r, TravState& s, const ST& stack,
+                                               Counters& cnt) {
     const bool is_leaf = !s.done && s.in_leaf;
     const bool is_node = !s.done && !s.in_leaf;
     const uint64_t want_leaf = __ballot(is_leaf);
@@ -264,8 +287,8 @@ __device__ __forceinline__ bool trav_step_pred(const SceneView& sc, const Ray& r
     const bool tr = decide & s.rint & !((s.best_t > 0.0f) & (s.rd > s.best_t));
     const bool push = tl & tr;
     const bool pop = decide & !tl & !tr;
-    stack[s.sp * stride] = s.lc;  // slot above the top: free unless this is a push
-    const int top = stack[(s.sp > 0 ? s.sp - 1 : 0) * stride];
+    stack.put(s.sp, s.lc);  // slot above the top: free unless this is a push
+    const int top = stack.get(s.sp > 0 ? s.sp - 1 : 0);
     s.node = tr ? s.rc : (tl ? s.lc : (pop ? top : s.node));
     s.done = s.done | (pop & (s.sp == 0));
     s.sp += push ? 1 : ((pop & (s.sp > 0)) ? -1 : 0);
@@ -328,67 +351,45 @@ __device__ __forceinline__ void big_seg(const TravLean& s, int& rec0, int& n) {
     n = left ? s.na : s.nt - s.na;
 }
 
-template <int K, bool COUNT, bool FAST_RCP, bool PIPE, bool BIG = false>
+template <int K, bool COUNT, bool FAST_RCP, bool BIG = false>
 __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
     if constexpr (BIG) {  // park at a big leaf: now, or where this turn would enter it
         if (big_at(sc, s)) { s.fl |= TF_PARK; return false; }
     }
-    if constexpr (!PIPE) {
-        // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
-        const int lim = (BIG && s.k < s.na && s.nt - s.na >= sc.big_leaf) ? s.na : s.nt;
-        // test j of the turn is entry k0 + j (a lane stops at lim): the position is not counted
-        // up per test (v_cndmask + v_add per test and lane), it follows from k0 once the turn ends
-        const int k0 = s.k;
-        const int bl = s.la + k0, br = s.lb - s.na + k0;  // record of entry k0 + j: (left ? bl : br) + j
+    // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
+    const int lim = (BIG && s.k < s.na && s.nt - s.na >= sc.big_leaf) ? s.na : s.nt;
+    // test j of the turn is entry k0 + j (a lane stops at lim): the position is not counted
+    // up per test (v_cndmask + v_add per test and lane), it follows from k0 once the turn ends
+    const int k0 = s.k;
+    const int bl = s.la + k0, br = s.lb - s.na + k0;  // record of entry k0 + j: (left ? bl : br) + j
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const bool live = j == 0 || k0 + j < lim;  // the first test always is
-            if (j > 0 && !wave_any(live)) break;        // every lane's leaf pair is done
-            const int idx = (k0 + j < s.na ? bl : br) + j;
-            float t;
-            const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
-                              ((s.best_t < 0.0f) | (t < s.best_t));
-            s.best_t = take ? t : s.best_t;
-            s.best = take ? idx : s.best;
-            if (COUNT) cnt.tri_tests += live ? 1 : 0;
-        }
-        // tests made: 1, then one per j >= 1 with k0 + j < lim (a break comes only once every
-        // lane has k0 + j >= lim, so the count is the same with or without it)
-        s.k = max(k0 + 1, min(k0 + K, lim));
-    } else {
-        // the record of test j+1 is loaded (LDS) while test j computes; a lane whose leaf
-        // pair ends loads a valid record it will not use
-        int idx = s.k < s.na ? s.la + s.k : s.lb + (s.k - s.na);
-        TriRec cur = load_tri(sc.tris, idx);
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const bool live = j == 0 || s.k < s.nt;
-            if (j > 0 && !wave_any(live)) break;
-            const int k1 = s.k + 1;
-            const int idx1 = k1 < s.nt ? (k1 < s.na ? s.la + k1 : s.lb + (k1 - s.na)) : idx;
-            TriRec nxt;
-            if (j + 1 < K) nxt = load_tri(sc.tris, idx1);
-            float t;
-            const bool take = tri_hit<FAST_RCP>(cur, r, t) & live & ((s.best_t < 0.0f) | (t < s.best_t));
-            s.best_t = take ? t : s.best_t;
-            s.best = take ? idx : s.best;
-            if (COUNT) cnt.tri_tests += live ? 1 : 0;
-            s.k += live ? 1 : 0;
-            if (j + 1 < K) { cur = nxt; idx = idx1; }
-        }
+    for (int j = 0; j < K; ++j) {
+        const bool live = j == 0 || k0 + j < lim;  // the first test always is
+        if (j > 0 && !wave_any(live)) break;        // every lane's leaf pair is done
+        const int idx = (k0 + j < s.na ? bl : br) + j;
+        float t;
+        const bool take = tri_hit<FAST_RCP>(sc.tris, live ? idx : s.la, r, t) & live &
+                          ((s.best_t < 0.0f) | (t < s.best_t));
+        s.best_t = take ? t : s.best_t;
+        s.best = take ? idx : s.best;
+        if (COUNT) cnt.tri_tests += live ? 1 : 0;
     }
+    // tests made: 1, then one per j >= 1 with k0 + j < lim (a break comes only once every
+    // lane has k0 + j >= lim, so the count is the same with or without it)
+    s.k = max(k0 + 1, min(k0 + K, lim));
     const bool decide = s.k == s.nt;
     s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
     if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
     return decide;
 }
 
-__device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int stride) {
+template <class ST>
+__device__ __forceinline__ void lean_decide(TravLean& s, const ST& stack) {
     const bool tl = (s.fl & TF_LINT) && !((s.best_t > 0.0f) & (s.ld > s.best_t));
     const bool tr = (s.fl & TF_RINT) && !((s.best_t > 0.0f) & (s.rd > s.best_t));
     const bool pop = !tl & !tr;
-    stack[s.sp * stride] = s.la;  // a push keeps it, anything else leaves the slot free
-    const int top = stack[max(s.sp - 1, 0) * stride];
+    stack.put(s.sp, s.la);  // a push keeps it, anything else leaves the slot free
+    const int top = stack.get(max(s.sp - 1, 0));
     s.node = tr ? s.lb : (tl ? s.la : top);
     s.fl |= (pop & (s.sp == 0)) ? TF_DONE : 0;
     s.sp += (tl & tr) ? 1 : (pop ? -1 : 0);  // sp < 0 only once done
@@ -402,9 +403,9 @@ __device__ __forceinline__ void lean_decide(TravLean& s, int32_t* stack, int str
 // sequential strict-< loop ends with, when that t beats f's closest t so far (strict <, so an
 // equal t from an earlier leaf stays).  The ray's walk over the leaf takes n / 64 steps instead of
 // n, and the wave's lanes do all of it instead of idling while one lane walks.
-template <bool COUNT, bool FAST_RCP>
-__device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, int32_t* stack,
-                                         int stride, Counters& cnt) {
+template <bool COUNT, bool FAST_RCP, class ST>
+__device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, const ST& stack,
+                                         Counters& cnt) {
     const int f = (int)__builtin_ctzll(parked);
     int my0 = 0, myn = 0;
     big_seg(s, my0, myn);
@@ -422,12 +423,6 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
     float bt = 0.0f;
     int bk = 0x7fffffff;  // none
-#ifndef PT_DIAG_BIG_REPS
-#define PT_DIAG_BIG_REPS 1
-#endif
-    // diagnostic build only (PT_DIAG_BIG_REPS=2: every turn tests its leaf twice, same result —
-    // the render's extra time is one pass's cost; scripts/gpu_ab_bigleaf.sh)
-    for (int rep = 0; rep < PT_DIAG_BIG_REPS; ++rep)
     for (int c = me; c < n; c += na) {
         float t;
         const bool take = tri_hit<FAST_RCP>(sc.tris, rec0 + c, q, t) & ((bk == 0x7fffffff) | (t < bt));
@@ -469,7 +464,7 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
         s.fl &= ~TF_PARK;
         if (s.k == s.nt) {
             s.fl &= ~TF_LEAF;
-            lean_decide(s, stack, stride);
+            lean_decide(s, stack);
         } else if (big_at(sc, s)) {
             s.fl |= TF_PARK;  // its right leaf is big too
         }
@@ -579,9 +574,9 @@ __device__ __forceinline__ void chunk_leaf(const SceneView& sc, const Ray& q, in
 // The first parked lane f whose big leaf has chunks: chunk_leaf for f's ray, then big_turn's
 // bookkeeping (the leaf counts as n reference tests).  Needs every lane of the wave running (the
 // wavefront kernels; the megakernel reaches here only through the same step with all lanes on).
-template <bool COUNT, bool FAST_RCP>
-__device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, int32_t* stack,
-                                           int stride, Counters& cnt) {
+template <bool COUNT, bool FAST_RCP, class ST>
+__device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, const ST& stack,
+                                           Counters& cnt) {
     const int f = (int)__builtin_ctzll(parked);
     int my0 = 0, myn = 0;
     big_seg(s, my0, myn);
@@ -605,21 +600,18 @@ __device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, Tr
         s.fl &= ~TF_PARK;
         if (s.k == s.nt) {
             s.fl &= ~TF_LEAF;
-            lean_decide(s, stack, stride);
+            lean_decide(s, stack);
         } else if (big_at(sc, s)) {
             s.fl |= TF_PARK;  // its right leaf is big too
         }
     }
 }
 
-// IFIF = false: each iteration runs ONE unit type for the whole wave — a leaf turn (up to K
-// triangle tests) when leaf lanes >= node_bias * node lanes, else a node turn.  IFIF = true:
-// each iteration runs a node step for every lane that wants one and then the leaf loop for
-// every lane in a leaf (including lanes that just entered one), then one decision — no lane
-// waits a whole leaf turn for its node step.  Both keep each lane's unit order.
-template <int K, bool COUNT, bool FAST_RCP, bool PIPE = false, bool IFIF = false, bool BIG = false, bool CHUNKS = false>
-__device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack,
-                                               int stride, Counters& cnt) {
+// Each iteration runs ONE unit type for the whole wave — a leaf turn (up to K triangle tests)
+// when leaf lanes >= node_bias * node lanes, else a node turn — keeping each lane's unit order.
+template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, class ST>
+__device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, const ST& stack,
+                                               Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE | (BIG ? TF_PARK : 0));
     if constexpr (BIG) {  // a parked lane's big leaf goes first: the wave tests it for that ray
         const uint64_t parked = __ballot((state & TF_PARK) != 0);
@@ -628,9 +620,9 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
             big_seg(s, my0, myn);
             if (CHUNKS && sc.lnodes && __ballot(1) == ~0ull &&
                 sc.tris[__builtin_amdgcn_readlane(my0, (int)__builtin_ctzll(parked))].lbvh > 0)
-                chunk_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);  // its leaf has chunks
+                chunk_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);  // its leaf has chunks
             else
-                big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, stride, cnt);
+                big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
             return true;
         }
     }
@@ -638,18 +630,12 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     const uint64_t want_node = __ballot(state == 0);
     if ((want_leaf | want_node) == 0) return false;
     bool decide = false;
-    if constexpr (IFIF) {
-        if (want_node && state == 0) decide = lean_node_unit<COUNT>(sc, r, s, cnt);
-        const bool in_leaf = (s.fl & (TF_LEAF | TF_DONE)) == TF_LEAF;
-        if (wave_any(in_leaf) && in_leaf) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE>(sc, r, s, cnt);
-    } else {
-        if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
-            if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, PIPE, BIG>(sc, r, s, cnt);
-        } else if (state == 0) {
-            decide = lean_node_unit<COUNT>(sc, r, s, cnt);
-        }
+    if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
+        if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);
+    } else if (state == 0) {
+        decide = lean_node_unit<COUNT>(sc, r, s, cnt);
     }
-    if (decide) lean_decide(s, stack, stride);
+    if (decide) lean_decide(s, stack);
     return true;
 }
 
@@ -719,8 +705,8 @@ __device__ __forceinline__ bool mb_leaf_loop(const SceneView& sc, const Ray& r, 
     return decide;
 }
 
-template <int K, bool COUNT, bool FAST_RCP>
-__device__ __forceinline__ bool trav_step_mb(const SceneView& sc, const Ray& r, TravLean& s, int32_t* stack, int stride,
+template <int K, bool COUNT, bool FAST_RCP, class ST>
+__device__ __forceinline__ bool trav_step_mb(const SceneView& sc, const Ray& r, TravLean& s, const ST& stack,
                                              Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE);
     const uint64_t want_leaf = __ballot(state == TF_LEAF);
@@ -732,7 +718,7 @@ __device__ __forceinline__ bool trav_step_mb(const SceneView& sc, const Ray& r, 
     } else if (state == 0) {
         decide = mb_node_unit<COUNT>(sc, r, s, cnt);
     }
-    if (decide) lean_decide(s, stack, stride);
+    if (decide) lean_decide(s, stack);
     return true;
 }
 
@@ -747,31 +733,29 @@ struct TravSel<TRAV, true> { using type = TravLean; };
 
 // CHUNKS: big leaves with leaf chunks take chunk_turn (the wavefront traversal kernel; the
 // megakernel keeps the cooperative turn and its registers)
-template <int TRAV, bool COUNT, bool CHUNKS = false>
+template <int TRAV, bool COUNT, bool CHUNKS = false, class ST>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
-                                             int32_t* stack, int stride, Counters& cnt) {
+                                             const ST& stack, Counters& cnt) {
     if constexpr (TRAV >= 100 && TRAV < 160) {  // mailboxed lean<K> (SceneView::mailbox scenes); + 10: fast reciprocal
         constexpr int K = 1 << (TRAV % 10 - 3);
-        return trav_step_mb<K, COUNT, ((TRAV / 10) & 1) != 0>(sc, r, s, stack, stride, cnt);
+        return trav_step_mb<K, COUNT, ((TRAV / 10) & 1) != 0>(sc, r, s, stack, cnt);
     }
-    else if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 20: pipelined leaf loads; + 40: if-if step;
-                                     // + 160: big-leaf cooperation (a multiple of 80 keeps the bits above)
+    else if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 160: big-leaf cooperation
         constexpr int B = TRAV % 10;
         constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
-        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, ((TRAV / 20) & 1) != 0, ((TRAV / 40) & 1) != 0,
-                              TRAV >= 160, CHUNKS>(sc, r, s, stack, stride, cnt);
+        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, TRAV >= 160, CHUNKS>(sc, r, s, stack, cnt);
     }
-    else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, stride, cnt);
-    else return trav_step_pred<COUNT>(sc, r, s, stack, stride, cnt);
+    else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, cnt);
+    else return trav_step_pred<COUNT>(sc, r, s, stack, cnt);
 }
 
-template <int TRAV, bool COUNT>
-__device__ __forceinline__ int trace_any(const SceneView& sc, const Ray& r, float& t_out, int32_t* stack, int stride,
+template <int TRAV, bool COUNT, class ST>
+__device__ __forceinline__ int trace_any(const SceneView& sc, const Ray& r, float& t_out, const ST& stack,
                                          Counters& cnt) {
-    if (TRAV == 0) return trace<COUNT>(sc, r, t_out, stack, stride, cnt);
+    if (TRAV == 0) return trace<COUNT>(sc, r, t_out, stack, cnt);
     typename TravSel<TRAV>::type s;
     trav_init(s, true);
-    while (trav_advance<TRAV, COUNT>(sc, r, s, stack, stride, cnt)) {
+    while (trav_advance<TRAV, COUNT>(sc, r, s, stack, cnt)) {
     }
     t_out = s.best_t;
     return s.best;

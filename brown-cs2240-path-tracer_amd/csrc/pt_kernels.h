@@ -58,32 +58,21 @@ struct LaunchOpts {
     bool literal = false;  // k_mega: the reference's control flow
     bool lds = true;       // stage the scene in LDS when it fits
     int fast_rcp = -1;     // rcp_rn for 1/det where SceneView::fast_rcp says it is exact: -1 per-pipeline default
-    int pipe = -1;         // lean leaf turns load the next triangle while testing one: -1 per-pipeline default
-    int ifif = -1;         // lean step = node step for all lanes that want one, then leaf loop: -1 default
-    int dual = -1;         // wavefront batch split in two halves on two streams: -1 default
-    int stagger = -1;      // dual halves' traces alternate instead of overlapping: -1 default (off)
+    int dual = -1;         // wavefront batch split in parts on their own streams: -1 default (on)
     int fuse_gen = 1;      // fused kernel: the first launch makes the camera paths (0: k_wf_generate)
-    int cull = -1;         // entry cull for the first `cull` wavefront launches (bf kernels): -1 default
     int parts = -1;        // parts of a wavefront batch on their own streams (1..kMaxParts): -1 default (2)
     int mailbox = -1;      // mailboxed lean traversal where SceneView::mailbox allows it: -1 default (on)
     int bf = -1;           // wavefront, mailbox scenes: brute-force + replay trace kernel: -1 default (on)
     int fuse = -1;         // bf trace fused with the shading (k_wf_step_bf): -1 default (on)
-    int regen_bf = -1;     // megakernel with brute-force + replay on mailbox scenes: -1 default (off)
-    int persist = -1;      // fused bf as one workgroup-local launch per batch (k_wf_persist_bf): -1 default (off)
-    int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4/5/6 lean2/4/8
-    int regen = -1;        // fused kernel: streaming path regeneration (every extension launch refills): -1 default (off)
-    long regen_target = 0; // paths in flight per part with regeneration (0 = the batch capacity)
+    int trav = -1;         // traversal: -1 per-pipeline default, 0 nested, 1 flat, 2 predicated, 3 lean, 4..8 lean2..lean32
     int sort = -1;         // traversal pipeline: survivors grouped per shade block by 8 / 64 / 512 coherence keys (0 off): -1 default (512)
     int bf_slots = -1;     // brute-force kernels: hit slots per lane (< kBfSlots: tests of the recompute path): -1 default
     int trace_blocks = 0;  // traversal / step kernels: cap on the grid (tests): 0 = occupancy-derived
-    int trace_dyn = 0;     // k_wf_trace takes its windows from group counters (1) or the static split (0)
     int trace_sparse = -1; // k_wf_trace: narrower windows when 32-entry ones keep < 1/n of the waves busy (n; 0 off): -1 default
     int region_perm = -1;  // k_wf_step_bf: camera batches dealt to regions by a permutation (WfBuffers::rq); -1 default
     int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
+    int stack16 = 1;       // k_wf_trace: 16-bit stack entries on trees below 65,536 nodes (0: 32-bit)
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
-    int packet = -1;       // traversal scenes: packet walk + replay (k_wf_trace_pk) on 1 camera / 2 + shadow / 3 all launches: -1 default (off)
-    int packet_nodes = 0;  // k_wf_trace_pk's node budget per packet (0: kPkMaxNodes)
-    int pipeline = -1;     // two parts run their batches half a batch apart on two radiance buffers: -1 default
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -125,23 +114,12 @@ struct WfBuffers {
     // region_perm; 1, 1: j mod nreg, neighbouring regions — one block's waves — take neighbouring
     // batches)
     uint32_t rq, rqi;
-    // streaming path regeneration (k_wf_step_bf<..., REGEN>): every extension launch tops each
-    // region up to `target` entries with new camera paths of the region's share of the render;
-    // rgen[slot * kRegions + r] = camera batches of region r made so far (two slots, alternating
-    // by extension launch), live[it % kLiveRing] = regions with work in launch it (host polling)
-    uint32_t* rgen;
-    uint32_t* live;
-    uint32_t* rfetch;   // k_wf_regen_bf: per launch slot (3) and region, the region's next batch (kFetchStride apart)
-    uint32_t target;
-    uint64_t rad_cap;   // paths whose radiance `rad` holds (>= capacity; regeneration: a whole group of frames)
+    uint64_t rad_cap;   // paths whose radiance `rad` holds (>= capacity)
 };
-constexpr uint32_t kLiveRing = 64;
-constexpr uint32_t kFetchStride = 32;  // u32 between two regions' fetch counters: 128 B
 constexpr uint32_t kRegions = 512;
-// queue slack (entries per half = 64 * this): regions of R <= 2/3 of it hold ceil(batches / R)
-// 64-entry batches each (k_wf_persist_bf uses one region per workgroup, at most kPersistMaxBlocks)
+// queue slack (entries per part = 64 * this): regions of R <= kRegions hold ceil(batches / R)
+// 64-entry batches each
 constexpr uint32_t kQueueSlackRegions = 4096;
-constexpr uint32_t kPersistMaxBlocks = 2048;
 constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 
 // Dual-stream wavefront: two streams owned by the scene, created back to back so that HIP's
@@ -151,30 +129,17 @@ constexpr int kMaxParts = 4;  // parts of a wavefront batch on their own streams
 struct WfStreams {
     hipStream_t aux[kMaxParts] = {};
     hipEvent_t fork = nullptr, join[kMaxParts] = {};
-    hipEvent_t traced[2] = {nullptr, nullptr};  // "part h finished its trace i" (staggering, two parts)
-    // batch pipelining (LaunchOpts::pipeline): "part 0 is half-way through the first batch" and
-    // "the accumulation of the batches of radiance buffer k has been issued behind them"
-    hipEvent_t mid = nullptr, acc_done[2] = {nullptr, nullptr};
-    bool pipeline = false;
-    bool stagger = false;
     bool fuse_gen = true;  // LaunchOpts::fuse_gen
     int nparts = 2;
-    bool regen = true;     // LaunchOpts::regen
-    uint32_t regen_target = 0;  // LaunchOpts::regen_target (paths in flight per part; 0 = the queue capacity)
-    // host polling of the regeneration loop: pinned words (2 per part) and their events
-    uint32_t* h_poll = nullptr;
-    hipEvent_t poll_ev[kMaxParts][2] = {};
     int sort_bins = 0;     // LaunchOpts::sort: k_wf_shade groups a block's survivors by a coherence key of 8 / 64 / 512 values (0: off)
     // per-call launch shape (LaunchOpts, filled by launch_wavefront)
     int trace_blocks = 0;  // cap on the trace / step grid (0: occupancy-derived)
-    int trace_dyn = 0;     // k_wf_trace window hand-out from group counters
     int trace_sparse = 0;  // k_wf_trace windows below 32 entries for short queues (LaunchOpts::trace_sparse)
     int region_perm = 0;   // LaunchOpts::region_perm
     int trace_ring = 0;    // LaunchOpts::trace_ring
+    int stack16 = 1;       // LaunchOpts::stack16
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
-    int packet = 0;        // traversal scenes: packet walk + replay (k_wf_trace_pk; pk_launch)
-    int packet_nodes = 0;  // its node budget (0: kPkMaxNodes)
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
@@ -185,11 +150,6 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const Fra
 hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
                              uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
                              hipStream_t stream);
-
-// megakernel with brute-force + replay closest hits (mailbox scenes; pt_wavefront.hip)
-hipError_t launch_regen_bf(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, uint32_t frame0,
-                           uint32_t nframes, uint32_t stride, bool accum, bool count, float* out, Counters* cnt,
-                           hipStream_t stream);
 
 // display transform of program-raymarch.ts:295-316 on device (pt_image.hip)
 hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t* rgba, hipStream_t stream);

@@ -18,7 +18,7 @@
 namespace pt {
 
 template <bool COUNT>
-__device__ f3 radiance(const SceneView& sc, const FrameParams& fp, Ray ray, uint32_t seed_in, int32_t* stack, int stride,
+__device__ f3 radiance(const SceneView& sc, const FrameParams& fp, Ray ray, uint32_t seed_in, const LStack32& stack,
                        Counters& cnt) {
     // program-raymarch.wgsl:104-303, literal control flow
     f3 L = mk(0.0f, 0.0f, 0.0f), beta = mk(1.0f, 1.0f, 1.0f);
@@ -30,7 +30,7 @@ __device__ f3 radiance(const SceneView& sc, const FrameParams& fp, Ray ray, uint
         seed = hash1u(seed);
         if (COUNT) cnt.ext_queries++;
         float t;
-        int rec = trace<COUNT>(sc, ray, t, stack, stride, cnt);
+        int rec = trace<COUNT>(sc, ray, t, stack, cnt);
         if (rec < 0) break;
         Hit h = hit_data(sc, ray, rec, t);
         Mat m = load_mat(sc, h.mat);
@@ -45,7 +45,7 @@ __device__ f3 radiance(const SceneView& sc, const FrameParams& fp, Ray ray, uint
         sray.o = off; sray.d = ldir; sray.inv = rcp3(ldir);
         if (COUNT) cnt.shadow_queries++;
         float st;
-        int srec = trace<COUNT>(sc, sray, st, stack, stride, cnt);
+        int srec = trace<COUNT>(sc, sray, st, stack, cnt);
         if (srec >= 0) {
             Hit sh = hit_data(sc, sray, srec, st);
             Mat nm = load_mat(sc, sh.mat);
@@ -69,6 +69,7 @@ template <bool ACCUM, bool COUNT>
 __global__ __launch_bounds__(kMegaBlock) void k_mega(SceneView sc, FrameParams fp, uint32_t frame0, uint32_t nframes,
                                                     uint32_t stride, float* __restrict__ out, Counters* cnt_out) {
     __shared__ int32_t s_stack[kStackMax * kMegaBlock];
+    const LStack32 stack = LStack32::make(reinterpret_cast<char*>(s_stack), kMegaBlock);
     uint32_t x, y;
     pixel_of(x, y);
     Counters c = {};
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(kMegaBlock) void k_mega(SceneView sc, FrameParams f
             uint32_t seed;
             Ray r = camera_ray(fp, x, y, t, seed);
             if (COUNT) c.samples++;
-            f3 L = radiance<COUNT>(sc, fp, r, seed, s_stack + threadIdx.x, kMegaBlock, c);
+            f3 L = radiance<COUNT>(sc, fp, r, seed, stack, c);
             acc = ACCUM ? add_clamped(acc, L) : L;
         }
         o[0] = acc.x; o[1] = acc.y; o[2] = acc.z;
@@ -95,7 +96,7 @@ template <bool LDS, int TRAV, bool ACCUM, bool COUNT>
 __global__ __launch_bounds__(kMegaBlock) void k_regen(SceneView sc, FrameParams fp, uint32_t frame0, uint32_t nframes,
                                                      uint32_t stride, float* __restrict__ out, Counters* cnt_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    int32_t* stack = reinterpret_cast<int32_t*>(smem) + threadIdx.x;  // [max_stack][256] int32, lane-minor
+    const LStack32 stack = LStack32::make(smem, kMegaBlock);  // [max_stack][256] int32, lane-minor
     if (LDS) stage_scene_lds(sc, smem + (uint32_t)sc.max_stack * kMegaBlock * 4u);
     uint32_t x, y;
     pixel_of(x, y);
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(kMegaBlock) void k_regen(SceneView sc, FrameParams 
             if (COUNT) { c.samples++; c.ext_queries++; }
         }
         float t;
-        const int rec = trace_any<TRAV, COUNT>(sc, ray, t, stack, kMegaBlock, c);
+        const int rec = trace_any<TRAV, COUNT>(sc, ray, t, stack, c);
         bool more;
         if (phase == kExt) {
             more = path_after_ext(sc, rec, t, ray, ps);
@@ -441,8 +442,6 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& scene, const
 #undef LIT
         return hipGetLastError();
     }
-    if (lo.regen_bf > 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0)
-        return launch_regen_bf(lo, sc, fp, frame0, nframes, stride, accum, count, out, cnt, stream);
     const bool lds = lo.lds && scene_fits_lds(sc);
     // lean4 + node bias 8 + fast reciprocal by default (measured at 1024^2 64 spp: 848 vs 611
     // for lean2 with majority turns and the division; scripts/perf_variants.py)

@@ -135,18 +135,9 @@ struct SceneView {
     // i2 < vn_range (the branch applies); global memory, read for the winning record only
     const float4* tnorm;
     int32_t vnormals;
-    // entry cull of the brute-force kernels (mailbox scenes; pt_wavefront.hip bf_cull_mask): per
-    // distinct entry u, cull[3u..3u+2] = {box lo, tau}, {box hi, margin factor}, {e1 x e2, w}
-    // (pt_capi.hip build_layout); cull_its = the wavefront launches that use it (it < cull_its)
-    const float4* cull;
-    int32_t cull_its;
     // big leaves in step (lean traversal, TRAV + 160): the lanes of a wave walk a leaf of at least
     // big_leaf entries in one shared rotated order (lean_leaf_loop; 0 = off)
     int32_t big_leaf;
-    // the distinct entries in pairs for phase 1's packed-f32 test (mailbox scenes): pair j =
-    // entries 2j, 2j+1 as 20 floats {v0.x of 2j, v0.x of 2j+1, v0.y, v0.y, ..., e2.z, e2.z, 0, 0};
-    // an odd count ends with an all-zero entry (det = 0: never a hit)
-    const float* bfpair;
     // leaf chunks (pt_leafbvh.cpp; nullptr when the scene has none or option leaf_walk=0): chunks,
     // and per chunk slot a copy of its entry's record whose lbvh field holds the entry's position
     // in its leaf (ltris: one load per test, no index indirection)
@@ -168,8 +159,6 @@ struct FrameParams {
     uint32_t width, height;  // u32(meta[0]), u32(meta[1])
     int32_t direct_only;  // meta[46] > 0
     int32_t max_depth;    // literal 16 in `while(depth <= 16)`, program-raymarch.wgsl:118
-    int32_t tiles;        // wavefront camera paths: 0 row order, 1 in 8x8 pixel tiles, 2 scattered (slot_path; results unchanged)
-    uint32_t scatter_mul; // tiles == 2: the multiplier of the scatter order, coprime with width * height
 };
 
 }  // namespace pt

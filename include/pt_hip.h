@@ -147,11 +147,10 @@ int pt_set_hw_queues(int n);
  * values fail with PT_ERR_INVALID.  Render calls read the options when they start.
  *   "kernel"        auto | mega | wavefront | literal    pipeline (auto = PT_MODE_* and the scene)
  *   "trav"          nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32   traversal flavour
- *   "lds" "fastrcp" "pipe" "ifif" "dual" "stagger" "fuse" "fuse_gen" "bf" "mailbox" "persist"
- *   "regen" "regen_bf" "bf_stackless" "trace_dyn" "tiles" "batch_pipe" "leaf_walk"   0 | 1 switches
- *   "parts" "cull" "sort" "node_bias" "big_leaf" "bf_slots" "wf_paths" "wf_trace_blocks" "packet"
- *   "packet_nodes" "trace_sparse"
- *   "regen_target" "trace_watchdog"                                         integers
+ *   "lds" "fastrcp" "dual" "fuse" "fuse_gen" "bf" "mailbox" "bf_stackless" "region_perm"
+ *   "stack16" "leaf_walk"                                                   0 | 1 switches
+ *   "parts" "sort" "node_bias" "big_leaf" "bf_slots" "wf_paths" "wf_trace_blocks" "trace_sparse"
+ *   "trace_ring" "trace_watchdog"                                           integers
  *   "mb_uid_order"  forward | reverse   (read by pt_scene_create: uid numbering of mailbox scenes)
  *   "leaf_bvh"      integer             (read by pt_scene_create: leaves with a leaf BVH, >= this many entries)
  *   "reduce"        rccl | ordered      (pt_render_multi's reduction)

@@ -63,29 +63,14 @@ VARIANTS = {
     "mega_lean4_bias8_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "8", "PT_FASTRCP": "1"},
     "mega_lean4_bias16_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "16", "PT_FASTRCP": "1"},
     "mega_lean2_bias8_fast": {"PT_KERNEL": "mega", "PT_TRAV": "lean2", "PT_NODE_BIAS": "8", "PT_FASTRCP": "1"},
-    "wf_lean16_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_PIPE": "1"},
-    "wf_lean16_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_IFIF": "1"},
-    "wf_lean8_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_IFIF": "1"},
-    "wf_lean4_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_IFIF": "1"},
-    "wf_lean8_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_PIPE": "1"},
-    "wf_lean4_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_PIPE": "1"},
     "wf_bf": {"PT_KERNEL": "wavefront"},
     "wf_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
     "wf_bf_nofuse_2blk": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "512"},
-    "mega_bf": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1"},
     "wf_gen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1"},
     "wf_nogen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "0"},
-    "wf_cull0": {"PT_KERNEL": "wavefront", "PT_CULL": "0"},
-    "wf_cull1": {"PT_KERNEL": "wavefront", "PT_CULL": "1"},
-    "wf_cull2": {"PT_KERNEL": "wavefront", "PT_CULL": "2"},
-    "wf_cull4": {"PT_KERNEL": "wavefront", "PT_CULL": "4"},
-    "wf_cull_all": {"PT_KERNEL": "wavefront", "PT_CULL": "99"},
     "wf_parts4": {"PT_KERNEL": "wavefront", "PT_PARTS": "4"},
     "wf_parts3": {"PT_KERNEL": "wavefront", "PT_PARTS": "3"},
     "wf_parts4_16M": {"PT_KERNEL": "wavefront", "PT_PARTS": "4", "PT_WF_PATHS": "16777216"},
-    "wf_bf_step": {"PT_KERNEL": "wavefront", "PT_PERSIST": "0"},
-    "wf_persist_2blk": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "512"},
-    "wf_persist_1024": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "1024"},
     "wf_bf_single": {"PT_KERNEL": "wavefront", "PT_DUAL": "0"},
     "wf_bf_32M_single": {"PT_KERNEL": "wavefront", "PT_DUAL": "0", "PT_WF_PATHS": "33554432"},
     "wf_bf_16M": {"PT_KERNEL": "wavefront", "PT_WF_PATHS": "16777216"},

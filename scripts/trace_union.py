@@ -15,14 +15,15 @@ import csv
 import json
 import sys
 
-PREFIX = {"k_wf_step": ("k_wf_step_bf<", "k_wf_persist_bf<", "k_wf_regen_bf<"),
-          "k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<", "k_wf_trace_pk<")}
+PREFIX = {"k_wf_step": ("k_wf_step_bf<",), "k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<")}
 
 
 def uncounted(name: str, kernel: str) -> bool:
     args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")]
-    if name.startswith("k_wf_step_bf<") or name.startswith("k_wf_regen_bf<"):
+    if name.startswith("k_wf_step_bf<"):  # <EXT, LDS, rcp, COUNT, GEN>
         return len(args) >= 4 and args[3] == "false"
+    if name.startswith("k_wf_trace<"):  # <LDS, TRAV, COUNT, RING, S16>
+        return len(args) >= 3 and args[2] == "false"
     return bool(args) and args[-1] == "false"
 
 

@@ -1,5 +1,7 @@
 """bench.py's roofline traffic: the PMC bytes per launch of the timed k_wf_step instances
-(COUNT=false, no opt-in CULL), weighted by their dispatch counts (scripts/summarize_traffic.py)."""
+(COUNT=false), weighted by their dispatch counts (scripts/summarize_traffic.py).  Kernel names of
+round 3's profiles carry a sixth template argument (the removed entry cull: CULL=true instances
+are not timed)."""
 import json
 import os
 import sys
@@ -23,15 +25,29 @@ def test_weighted_by_dispatches(tmp_path, monkeypatch):
         "k_wf_accum": {"hbm_bytes_per_launch": 9e9, "dispatches": 1},
     })
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    got, src = bench.load_traffic(("k_wf_step_bf<", "k_wf_persist_bf<"), 64, 64, 4, 8, 1)
+    got, src = bench.load_traffic(("k_wf_step_bf<",), 64, 64, 4, 8, 1)
     assert got == (200.0 * 8 + 100.0 * 9 + 1000.0) / 18
     assert src.startswith("profiles/traffic.json[64x64x4x8x1]")
+
+
+def test_weighted_five_argument_names(tmp_path, monkeypatch):
+    """k_wf_step_bf<EXT, LDS, rcp, COUNT, GEN> (round 4): the GEN launch is timed, COUNT is not."""
+    _write(tmp_path, {
+        "k_wf_step_bf<true, true, true, false, false>": {"hbm_bytes_per_launch": 200.0, "dispatches": 8},
+        "k_wf_step_bf<false, true, true, false, false>": {"hbm_bytes_per_launch": 100.0, "dispatches": 9},
+        "k_wf_step_bf<true, true, true, false, true>": {"hbm_bytes_per_launch": 1000.0, "dispatches": 1},
+        "k_wf_step_bf<true, true, true, true, false>": {"hbm_bytes_per_launch": 9e9, "dispatches": 8},
+    })
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    got, _ = bench.load_traffic(("k_wf_step_bf<",), 64, 64, 4, 8, 1)
+    assert got == (200.0 * 8 + 100.0 * 9 + 1000.0) / 18
 
 
 def test_unweighted_without_counts(tmp_path, monkeypatch):
     _write(tmp_path, {
         "k_wf_step_bf<true, true, true, false, false>": {"hbm_bytes_per_launch": 200.0},
         "k_wf_step_bf<false, true, true, false, false>": {"hbm_bytes_per_launch": 100.0},
+        "k_wf_step_bf<true, true, true, false, true>": {"hbm_bytes_per_launch": 9e9},
         "k_wf_step_bf<true, true, true, true, false>": {"hbm_bytes_per_launch": 9e9},
         "k_wf_trace<true, 17, false>": {"hbm_bytes_per_launch": 7.0},
         "k_wf_trace<true, 17, true>": {"hbm_bytes_per_launch": 9e9},

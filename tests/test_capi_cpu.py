@@ -89,12 +89,17 @@ def test_options_set_get_reset_and_validate():
     assert pt_amd.get_option("trav") == "" and pt_amd.get_option("parts") == ""
 
 
-def test_round3_layout_options():
-    """The queue-layout switches of round 3 are options like the others: flags
-    that take 0/1 and reject anything else; the batch target is an integer."""
+def test_layout_options():
+    """The queue-layout and stack switches are options like the others:
+    flags that take 0/1 and reject anything else; the batch target is an integer; the
+    experiments removed in round 4 are unknown names."""
     pt_amd.reset_options()
     try:
-        for name in ("region_perm", "scatter"):
+        for name in ("packet", "persist", "regen", "regen_bf", "cull", "tiles", "scatter", "batch_pipe",
+                     "trace_dyn", "stagger", "pipe", "ifif"):
+            with pytest.raises(pt_amd.PtError):
+                pt_amd.set_option(name, "1")
+        for name in ("region_perm", "stack16"):
             pt_amd.set_option(name, 0)
             assert pt_amd.get_option(name) == "0"
             pt_amd.set_option(name, 1)

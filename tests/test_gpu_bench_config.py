@@ -25,10 +25,9 @@ from conftest import SCENES
 
 pytestmark = pytest.mark.gpu
 
-ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
-            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS",
-            "PT_REGEN_BF", "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
-            "PT_BIG_LEAF", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN", "PT_BATCH_PIPE")
+ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
+            "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_BF_STACKLESS", "PT_SORT", "PT_STACK16")
 ORACLE_THREADS = 16  # the GPU box's CPU share
 
 
@@ -100,35 +99,6 @@ def test_multi_batch_ragged_parts_vs_oracle(packed, clean_env, parts):
         gpu = s.render(meta, 2, 7, 3, 8, pt_amd.MODE_AUTO, accum=init.copy())
     ref, _ = oracle.render(p.triangle_data, p.bvh_data, meta, 2, 7, 3, 8, acc=init.copy())
     assert_same_bits(gpu, ref, f"parts={parts}")
-
-
-@pytest.mark.parametrize("variant", ["fused", "nogen", "traversal", "traversal_1block", "parts4", "count"])
-def test_batch_pipe_vs_oracle(packed, clean_env, variant):
-    """Batch pipelining (option batch_pipe): two parts half a batch apart over two radiance
-    buffers — five batches (2 + 2 + 2 + 2 + 1 frames), the accumulation in frame order, a second
-    call on the same scene reusing the events; four parts (not pipelined) and the counted build
-    take the same option."""
-    p = packed["CornellBox"]
-    meta = p.meta_for(64, 64)
-    clean_env.set("PT_KERNEL", "wavefront")
-    clean_env.set("PT_WF_PATHS", "8192")  # 2 frames per batch
-    clean_env.set("PT_BATCH_PIPE", "1")
-    extra = {"nogen": {"PT_FUSE_GEN": "0"}, "traversal": {"PT_MAILBOX": "0"},
-             "traversal_1block": {"PT_MAILBOX": "0", "PT_WF_TRACE_BLOCKS": "1"}, "parts4": {"PT_PARTS": "4"}}
-    for k, v in extra.get(variant, {}).items():
-        clean_env.set(k, v)
-    init = np.random.default_rng(11).uniform(0, 1, (64, 64, 3)).astype(np.float32)
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        if variant == "count":
-            gpu, gc = s.render(meta, 3, 9, 2, 8, pt_amd.MODE_AUTO, accum=init.copy(), counters=True)
-        else:
-            gpu = s.render(meta, 3, 9, 2, 8, pt_amd.MODE_AUTO, accum=init.copy())
-        again = s.render(meta, 3, 9, 2, 8, pt_amd.MODE_AUTO, accum=init.copy())
-    ref, rc = oracle.render(p.triangle_data, p.bvh_data, meta, 3, 9, 2, 8, acc=init.copy(), nthreads=ORACLE_THREADS)
-    assert_same_bits(gpu, ref, variant)
-    assert_same_bits(again, ref, variant + " (second call)")
-    if variant == "count":
-        assert gc == rc, (gc, rc)
 
 
 # ---------------------------------------------------------------------------------------------

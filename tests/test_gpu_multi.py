@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def env(ptopts):
-    for k in ("PT_KERNEL", "PT_REDUCE", "PT_PARTS", "PT_WF_PATHS", "PT_REGEN"):
+    for k in ("PT_KERNEL", "PT_REDUCE", "PT_PARTS", "PT_WF_PATHS"):
         ptopts.unset(k, raising=False)
     return ptopts
 

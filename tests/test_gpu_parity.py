@@ -42,36 +42,23 @@ KERNELS = {
     "wavefront_lean16_majority_div": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_NODE_BIAS": "1",
                                       "PT_FASTRCP": "0"},
     "mega_lean4_majority": {"PT_KERNEL": "mega", "PT_TRAV": "lean4", "PT_NODE_BIAS": "1"},
-    "wavefront_lean16_pipe": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_PIPE": "1"},
-    "wavefront_lean8_ifif": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean8", "PT_IFIF": "1"},
     "wavefront_single_stream": {"PT_KERNEL": "wavefront", "PT_DUAL": "0"},
     "wavefront_dual_1block": {"PT_KERNEL": "wavefront", "PT_DUAL": "1", "PT_WF_TRACE_BLOCKS": "1"},
     "wavefront_nomailbox": {"PT_KERNEL": "wavefront", "PT_MAILBOX": "0"},
     "wavefront_mailbox_rev": {"PT_KERNEL": "wavefront", "PT_MB_UID_ORDER": "reverse"},
     "wavefront_mb_lean16_rev": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
     "wavefront_bf_nofuse": {"PT_KERNEL": "wavefront", "PT_FUSE": "0"},
-    "wavefront_persist": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1"},
-    "mega_bf": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1"},
-    "mega_bf_global_1slot": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1", "PT_LDS": "0", "PT_BF_SLOTS": "1"},
     "wavefront_4parts": {"PT_KERNEL": "wavefront", "PT_PARTS": "4"},
     "wavefront_3parts_nofuse": {"PT_KERNEL": "wavefront", "PT_PARTS": "3", "PT_FUSE": "0"},
     "wavefront_bf_step_3blocks": {"PT_KERNEL": "wavefront", "PT_WF_TRACE_BLOCKS": "3"},
-    "wavefront_persist_3blocks_div": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1", "PT_WF_TRACE_BLOCKS": "3",
-                                      "PT_FASTRCP": "0"},
     "wavefront_bf_nofuse_1block": {"PT_KERNEL": "wavefront", "PT_FUSE": "0", "PT_WF_TRACE_BLOCKS": "1"},
     "wavefront_bf_global_noslots": {"PT_KERNEL": "wavefront", "PT_LDS": "0", "PT_BF_SLOTS": "0"},
     "wavefront_bf_2slots_div": {"PT_KERNEL": "wavefront", "PT_BF_SLOTS": "2", "PT_FASTRCP": "0"},
     "wavefront_mailbox_lean4_global": {"PT_KERNEL": "wavefront", "PT_TRAV": "lean4", "PT_LDS": "0"},
     "wavefront_3blocks_flat1": {"PT_KERNEL": "wavefront", "PT_TRAV": "flat1", "PT_WF_TRACE_BLOCKS": "3"},
-    # entry cull of the fused kernel: on its default launches, on every launch (incoherent
-    # bundles: mostly nothing culled, all paths through the cull code), with the division
-    "wavefront_cull": {"PT_KERNEL": "wavefront", "PT_CULL": "2"},
-    "wavefront_cull_all": {"PT_KERNEL": "wavefront", "PT_CULL": "99"},
-    "wavefront_cull_all_div_global": {"PT_KERNEL": "wavefront", "PT_CULL": "99", "PT_FASTRCP": "0", "PT_LDS": "0"},
     # camera paths made in the first fused launch (GEN) or by k_wf_generate
     "wavefront_gen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1"},
     "wavefront_nogen": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "0"},
-    "wavefront_gen_cull_1block": {"PT_KERNEL": "wavefront", "PT_FUSE_GEN": "1", "PT_CULL": "2", "PT_WF_TRACE_BLOCKS": "1"},
     # big leaves tested by the whole wave (default from 128 entries: the boat; forced onto small leaves
     # here so every scene runs many cooperative turns), and off
     "wavefront_big8": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0"},
@@ -80,20 +67,10 @@ KERNELS = {
     "wavefront_nobig": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "0"},
     "mega_big8": {"PT_KERNEL": "mega", "PT_BIG_LEAF": "8"},
     "mega_nobig": {"PT_KERNEL": "mega", "PT_BIG_LEAF": "0"},
-    # streaming path regeneration (opt-in): one and four parts, a small in-flight target
-    "wavefront_regen": {"PT_KERNEL": "wavefront", "PT_REGEN": "1"},
-    "wavefront_regen_4parts_small": {"PT_KERNEL": "wavefront", "PT_REGEN": "1", "PT_PARTS": "4",
-                                     "PT_REGEN_TARGET": "4096"},
     # brute-force replay: the stack walk instead of the stackless pre-order walk (the default)
     "wavefront_bf_stack_replay": {"PT_KERNEL": "wavefront", "PT_BF_STACKLESS": "0"},
-    "mega_bf_stack_replay": {"PT_KERNEL": "mega", "PT_REGEN_BF": "1", "PT_BF_STACKLESS": "0"},
     # traversal pipeline: survivors grouped by 8 / 64 / 512 coherence keys per shade block (queue order only; 512 is the default)
     "wavefront_sort8": {"PT_KERNEL": "wavefront", "PT_SORT": "8"},
-    # camera paths generated in 8x8 pixel tiles (slot_path): every generator, both pipelines
-    "wavefront_tiles": {"PT_KERNEL": "wavefront", "PT_TILES": "1"},
-    "wavefront_tiles_nogen": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_FUSE_GEN": "0"},
-    "wavefront_tiles_persist": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_PERSIST": "1"},
-    "wavefront_tiles_trav": {"PT_KERNEL": "wavefront", "PT_TILES": "1", "PT_MAILBOX": "0"},
     # the traversal kernel's hit ring forced to 128 / 256 entries (default: 256 when it costs no block)
     "wavefront_ring128": {"PT_KERNEL": "wavefront", "PT_TRACE_RING": "128", "PT_MAILBOX": "0"},
     "wavefront_ring256_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_RING": "256", "PT_MAILBOX": "0",
@@ -103,29 +80,12 @@ KERNELS = {
     "wavefront_region_perm": {"PT_KERNEL": "wavefront", "PT_REGION_PERM": "1"},
     "wavefront_region_perm_nofusegen_3blocks": {"PT_KERNEL": "wavefront", "PT_REGION_PERM": "1", "PT_FUSE_GEN": "0",
                                                 "PT_WF_TRACE_BLOCKS": "3"},
-    # camera paths scattered over the image (option scatter: slot q -> pixel q * m mod npix)
-    "wavefront_scatter": {"PT_KERNEL": "wavefront", "PT_SCATTER": "1"},
-    "wavefront_scatter_trav_nofusegen": {"PT_KERNEL": "wavefront", "PT_SCATTER": "1", "PT_MAILBOX": "0",
-                                         "PT_FUSE_GEN": "0"},
-    # packet walk + replay (k_wf_trace_pk): camera launches, camera + shadow, every launch; with a
-    # node budget so small that every packet gives up (the real-test replay), and on one block
-    "wavefront_packet1": {"PT_KERNEL": "wavefront", "PT_PACKET": "1", "PT_MAILBOX": "0"},
-    "wavefront_packet2": {"PT_KERNEL": "wavefront", "PT_PACKET": "2", "PT_MAILBOX": "0"},
-    "wavefront_packet3_div": {"PT_KERNEL": "wavefront", "PT_PACKET": "3", "PT_MAILBOX": "0", "PT_FASTRCP": "0"},
-    "wavefront_packet3_1block": {"PT_KERNEL": "wavefront", "PT_PACKET": "3", "PT_MAILBOX": "0", "PT_WF_TRACE_BLOCKS": "1"},
-    "wavefront_packet3_giveup": {"PT_KERNEL": "wavefront", "PT_PACKET": "3", "PT_MAILBOX": "0", "PT_PACKET_NODES": "1"},
-    # traversal kernel with windows from group counters (PT_TRACE_DYN=1), also on a 1-block grid
-    "wavefront_trace_dyn": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_MAILBOX": "0"},
-    "wavefront_trace_dyn_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_DYN": "1", "PT_WF_TRACE_BLOCKS": "1"},
     # short queues in windows below 32 entries (option trace_sparse=n; default 4): n = 1 on the full
-    # grid (windows of 1..4 entries), on 3 blocks (the last depths only), with the group counters;
-    # n = 8 on one block; off
+    # grid (windows of 1..4 entries), on 3 blocks (the last depths only); n = 8 on one block; off
     "wavefront_trace_sparse_off": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "0", "PT_MAILBOX": "0"},
     "wavefront_trace_sparse": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "1", "PT_MAILBOX": "0"},
     "wavefront_trace_sparse_3blocks": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "1", "PT_MAILBOX": "0",
                                        "PT_WF_TRACE_BLOCKS": "3"},
-    "wavefront_trace_sparse_dyn": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "1", "PT_TRACE_DYN": "1",
-                                   "PT_MAILBOX": "0"},
     "wavefront_trace_sparse8_1block": {"PT_KERNEL": "wavefront", "PT_TRACE_SPARSE": "8", "PT_MAILBOX": "0",
                                        "PT_WF_TRACE_BLOCKS": "1"},
     # leaf BVHs (option leaf_bvh, read at scene creation; default off): on every leaf of >= 4 / >= 2
@@ -141,15 +101,22 @@ KERNELS = {
     "wavefront_sort512_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "512", "PT_MAILBOX": "0"},
     "wavefront_sort64_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_SORT": "64", "PT_MAILBOX": "0",
                                           "PT_WF_TRACE_BLOCKS": "1"},
+    # the traversal kernel's per-lane stacks with 32-bit entries (option stack16=0; the default packs
+    # two 16-bit levels per word on trees below 65,536 nodes), on the full grid and on one block
+    # with the 256-entry ring; and 16-bit stacks with the big-leaf turns forced onto small leaves
+    "wavefront_stack32_nomailbox": {"PT_KERNEL": "wavefront", "PT_STACK16": "0", "PT_MAILBOX": "0"},
+    "wavefront_stack32_ring256_1block": {"PT_KERNEL": "wavefront", "PT_STACK16": "0", "PT_MAILBOX": "0",
+                                         "PT_TRACE_RING": "256", "PT_WF_TRACE_BLOCKS": "1"},
+    "wavefront_stack16_big4_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_MAILBOX": "0",
+                                      "PT_WF_TRACE_BLOCKS": "1"},
 }
 
 
-ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS", "PT_PIPE", "PT_IFIF",
-            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PERSIST", "PT_PARTS", "PT_REGEN_BF",
-            "PT_CULL", "PT_FUSE_GEN", "PT_WF_PATHS", "PT_REGEN", "PT_REGEN_TARGET",
-            "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS", "PT_SORT", "PT_TRACE_DYN",
-            "PT_TRACE_SPARSE", "PT_BATCH_PIPE", "PT_TILES", "PT_PACKET", "PT_PACKET_NODES", "PT_LEAF_BVH",
-            "PT_LEAF_WALK", "PT_SCATTER", "PT_REGION_PERM", "PT_TRACE_RING")
+ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
+            "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
+            "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
+            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING",
+            "PT_STACK16")
 
 
 @pytest.fixture(params=list(KERNELS))
@@ -375,14 +342,6 @@ def test_profile_records_every_launch(packed, ptopts):
         wfg = s.profile_read()
     assert set(wfg) == {"k_wf_step", "k_wf_accum"}
     assert wfg["k_wf_step"]["launches"] == 2 * 2 * (depth + 1) and wfg["k_wf_accum"]["launches"] == 1
-    ptopts.set("PT_PERSIST", "1")  # one workgroup-local trace + shade launch per batch
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        s.profile_enable(True)
-        s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
-        wf1 = s.profile_read()
-    assert set(wf1) == {"k_wf_step", "k_wf_accum"}
-    assert wf1["k_wf_step"]["launches"] == 1 and wf1["k_wf_accum"]["launches"] == 1
-    ptopts.unset("PT_PERSIST")
     ptopts.set("PT_FUSE", "0")  # separate trace and shade kernels
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
@@ -391,7 +350,7 @@ def test_profile_records_every_launch(packed, ptopts):
     assert set(wf2) == {"k_wf_generate", "k_wf_trace", "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum"}
     assert wf2["k_wf_trace"]["launches"] == 2 * 2 * (depth + 1)
     assert wf2["k_wf_shade_ext"]["launches"] == wf2["k_wf_shade_shadow"]["launches"] == 2 * (depth + 1)
-    for v in list(mega.values()) + list(wf.values()) + list(wf1.values()) + list(wf2.values()):
+    for v in list(mega.values()) + list(wf.values()) + list(wfg.values()) + list(wf2.values()):
         assert 0.0 < v["min_ms"] <= v["avg_ms"] <= v["max_ms"] and v["total_ms"] > 0.0
 
 
@@ -464,10 +423,9 @@ def packed_tie(tmp_path_factory):
                                  {"PT_MB_UID_ORDER": "reverse", "PT_BF_SLOTS": "1"},
                                  {"PT_TRAV": "lean16", "PT_MB_UID_ORDER": "reverse"},
                                  {"PT_FUSE": "0", "PT_MB_UID_ORDER": "reverse"},
-                                 {"PT_PERSIST": "1", "PT_MB_UID_ORDER": "reverse"},
                                  {"PT_BF_STACKLESS": "0", "PT_MB_UID_ORDER": "reverse"}],
                          ids=["bf", "bf_reverse_uids", "no_mailbox", "bf_reverse_1slot", "mb_lean16_reverse",
-                              "bf_nofuse_reverse", "persist_reverse", "bf_stack_reverse"])
+                              "bf_nofuse_reverse", "bf_stack_reverse"])
 def test_mailbox_exact_ties(packed_tie, ptopts, env):
     for k in ENV_KEYS:
         ptopts.unset(k, raising=False)
@@ -539,28 +497,20 @@ def test_large_image_single_part_matches_megakernel(packed, ptopts):
     assert same_bits(a1, m), mismatch_report(a1, m)
 
 
-@pytest.mark.parametrize("scene", ["CornellBox", "CornellBox-Mirror"])
-def test_entry_cull_full_size(packed, ptopts, scene):
-    """The entry cull (bf_cull_mask) at the bench's image size: every launch culled, the default
-    launches culled and none culled give the same bits (1024^2, 2 frames, the full depth)."""
+def test_fuse_gen_full_size(packed, ptopts):
+    """Camera paths from k_wf_generate or made in the first fused launch give the same bits at the
+    bench's image size (1024^2, 2 frames, the full depth)."""
     for k in ENV_KEYS:
         ptopts.unset(k, raising=False)
     ptopts.set("PT_KERNEL", "wavefront")
-    p = packed[scene]
+    p = packed["CornellBox"]
     meta = p.meta_for(1024, 1024)
     out = {}
-    for cull in ("0", "2", "99"):
-        ptopts.set("PT_CULL", cull)
-        with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-            out[cull] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
-    ptopts.set("PT_CULL", "0")
-    for gen in ("0", "1"):  # camera paths from k_wf_generate / made in the first fused launch
+    for gen in ("0", "1"):
         ptopts.set("PT_FUSE_GEN", gen)
         with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-            out["gen" + gen] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
-    assert same_bits(out["2"], out["0"]), mismatch_report(out["2"], out["0"])
-    assert same_bits(out["99"], out["0"]), mismatch_report(out["99"], out["0"])
-    assert same_bits(out["gen0"], out["gen1"]), mismatch_report(out["gen0"], out["gen1"])
+            out[gen] = s.render(meta, 0, 2, 1, -1, pt_amd.MODE_WAVEFRONT)
+    assert same_bits(out["0"], out["1"]), mismatch_report(out["0"], out["1"])
 
 
 # ---------------------------------------------------------------------------------------------
