@@ -38,6 +38,7 @@ struct BNode {
     double stride[3] = {0, 0, 0};  // js-geometry Bounds.stride_* as constructed: the parent's extent
     std::vector<int32_t> objs;  // indices into the triangle list
     std::unique_ptr<BNode> l, r;
+    bool objs_empty() const { return leaf && objs.empty(); }  // an empty leaf keeps its zero box
 };
 
 constexpr int kMaxDepth = 16;
@@ -99,7 +100,16 @@ struct Builder {
     }
 };
 
-void pack(const BNode& n, const int32_t* tris, std::vector<double>& out) {
+// pad (the SAH tree only; the reference's tree is packed as its builder made it): child boxes are
+// written as the f32 values one ulp outside the round-to-nearest conversion of their double
+// bounds, so every box has a positive extent on every axis.  The slab test
+// (ray-bbox-intersection.wgsl:1-31) reports a hit only when tmax > max(tmin, 0): a zero-thickness
+// box — a leaf of coplanar axis-aligned triangles such as a Cornell wall or the light — is never
+// entered (the synthetic sweep scenes lost their light this way and rendered black).
+double pad_lo(double v) { return (double)std::nextafter((float)v, -std::numeric_limits<float>::infinity()); }
+double pad_hi(double v) { return (double)std::nextafter((float)v, std::numeric_limits<float>::infinity()); }
+
+void pack(const BNode& n, const int32_t* tris, std::vector<double>& out, bool pad = false) {
     const size_t cur = out.size();
     const size_t nchild = n.leaf ? 4 * n.objs.size() : 0;
     const double z3[3] = {0, 0, 0};
@@ -111,16 +121,21 @@ void pack(const BNode& n, const int32_t* tris, std::vector<double>& out) {
     for (const BNode* ch : {n.l.get(), n.r.get()}) {
         const double* mn = ch ? ch->box.mn : z3;
         const double* mx = ch ? ch->box.mx : z3;
-        out.insert(out.end(), mn, mn + 3);
-        out.insert(out.end(), mx, mx + 3);
+        if (pad && ch && !ch->objs_empty()) {
+            for (int k = 0; k < 3; ++k) out.push_back(pad_lo(mn[k]));
+            for (int k = 0; k < 3; ++k) out.push_back(pad_hi(mx[k]));
+        } else {
+            out.insert(out.end(), mn, mn + 3);
+            out.insert(out.end(), mx, mx + 3);
+        }
     }
     if (n.leaf)
         for (int32_t o : n.objs)
             for (int q = 0; q < 4; ++q) out.push_back(tris[4 * (size_t)o + q]);
-    if (!n.leaf && n.l) pack(*n.l, tris, out);
+    if (!n.leaf && n.l) pack(*n.l, tris, out, pad);
     if (!n.leaf && n.r) {
         out[cur + 3] = (double)out.size();
-        pack(*n.r, tris, out);
+        pack(*n.r, tris, out, pad);
     }
 }
 
@@ -264,9 +279,20 @@ struct SahBuilder {
 
 }  // namespace
 
-extern "C" int pt_bvh_build_sah(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count,
-                                float* bvh_out, size_t bvh_cap, size_t* bvh_len) {
-    if (!vertices || !tris || !bvh_len || vertex_count == 0 || tri_count == 0 || (bvh_cap && !bvh_out))
+// The fast tree keeps the reference's traversal, and with it the exit-distance pruning quirk
+// (intersection-logic.wgsl:178-181 with ray-bbox-intersection.wgsl:22-27): a subtree whose box
+// holds the ray's origin is skipped once the closest hit so far is nearer than the box's EXIT.
+// With tight SAH boxes that skip can hide the light from every shadow ray (the synthetic 1,000 and
+// 12,500-triangle sweep scenes rendered black).  A leaf child of the root is tested whenever the
+// ray meets its box (intersection-logic.wgsl:47-176: no pruning for leaf children), so the
+// triangles of the flagged materials (the emitters, program-raymarch.wgsl:136's sum(Ke) > 0) go
+// into the root's left child — one leaf when they are at most kSahMaxLeaf, else their own SAH
+// subtree — and the rest of the scene into its right child.
+extern "C" int pt_bvh_build_sah2(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count,
+                                 const uint8_t* isolate_material, size_t material_count, float* bvh_out,
+                                 size_t bvh_cap, size_t* bvh_len) {
+    if (!vertices || !tris || !bvh_len || vertex_count == 0 || tri_count == 0 || (bvh_cap && !bvh_out) ||
+        (material_count && !isolate_material))
         return PT_ERR_INVALID;
     std::vector<Box> tb(tri_count);
     std::vector<double> cen(3 * tri_count);
@@ -288,11 +314,35 @@ extern "C" int pt_bvh_build_sah(const double* vertices, size_t vertex_count, con
             if (i == 0 || x <= root.mn[k]) root.mn[k] = x;
             if (i == 0 || x >= root.mx[k]) root.mx[k] = x;
         }
+    std::vector<int32_t> lit, rest;
+    for (size_t t = 0; t < tri_count; ++t) {
+        const int32_t m = tris[4 * t + 3];
+        const bool iso = m >= 0 && (size_t)m < material_count && isolate_material[m];
+        (iso ? lit : rest).push_back((int32_t)t);
+    }
+    SahBuilder sb{tb, std::move(cen)};
     BNode top;
     top.axis = 0;
-    top.objs.resize(tri_count);
-    for (size_t t = 0; t < tri_count; ++t) top.objs[t] = (int32_t)t;
-    SahBuilder{tb, std::move(cen)}.build(top, 1);
+    if (!lit.empty() && !rest.empty()) {
+        top.box = empty_box();
+        for (size_t t = 0; t < tri_count; ++t) grow(top.box, tb[t]);
+        top.l = std::make_unique<BNode>();
+        top.r = std::make_unique<BNode>();
+        top.l->objs = std::move(lit);
+        top.r->objs = std::move(rest);
+        if ((int)top.l->objs.size() <= kSahMaxLeaf) {  // one leaf under the root
+            top.l->leaf = true;
+            top.l->box = empty_box();
+            for (int32_t o : top.l->objs) grow(top.l->box, tb[o]);
+        } else {
+            sb.build(*top.l, 2);
+        }
+        sb.build(*top.r, 2);
+    } else {
+        top.objs.resize(tri_count);
+        for (size_t t = 0; t < tri_count; ++t) top.objs[t] = (int32_t)t;
+        sb.build(top, 1);
+    }
     if (top.leaf) {  // the layout needs an internal root: two leaves under it
         top.leaf = false;
         top.l = std::make_unique<BNode>();
@@ -305,7 +355,7 @@ extern "C" int pt_bvh_build_sah(const double* vertices, size_t vertex_count, con
     }
     std::vector<double> out(root.mn, root.mn + 3);
     out.insert(out.end(), root.mx, root.mx + 3);
-    pack(top, tris, out);
+    pack(top, tris, out, true);
     if (out.size() >= (1u << 24)) return PT_ERR_INVALID;  // float offsets exact below 2^24 (packer.ts layout)
     *bvh_len = out.size();
     if (bvh_cap < out.size()) return bvh_cap ? PT_ERR_INVALID : PT_OK;
@@ -313,3 +363,7 @@ extern "C" int pt_bvh_build_sah(const double* vertices, size_t vertex_count, con
     return PT_OK;
 }
 
+extern "C" int pt_bvh_build_sah(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count,
+                                float* bvh_out, size_t bvh_cap, size_t* bvh_len) {
+    return pt_bvh_build_sah2(vertices, vertex_count, tris, tri_count, nullptr, 0, bvh_out, bvh_cap, bvh_len);
+}

@@ -532,22 +532,39 @@ static napi_value js_tonemap(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
-/* bvhBuild(Float64Array vertices, Int32Array tris (i0,i1,i2,mat)[, sah=false]) -> Float32Array bvh_data
- * (native twin of node/lib/bvh.js + packer.js:pack_bvh, byte-identical; sah: the fast binned-SAH
- * mode, pt_bvh_build_sah, same layout, not the reference's tree) */
+/* bvhBuild(Float64Array vertices, Int32Array tris (i0,i1,i2,mat)[, sah=false[, Uint8Array isolate]])
+ * -> Float32Array bvh_data (native twin of node/lib/bvh.js + packer.js:pack_bvh, byte-identical; sah:
+ * the fast binned-SAH mode, pt_bvh_build_sah, same layout, not the reference's tree; isolate: per
+ * material a flag — the emitters — whose triangles go under the root's left child,
+ * pt_bvh_build_sah2) */
 static napi_value js_bvh_build(napi_env env, napi_callback_info info) {
-    size_t argc = 3;
-    napi_value argv[3];
+    size_t argc = 4;
+    napi_value argv[4];
     CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     bool sah = false;
     if (argc > 2) {
         napi_valuetype t;
         if (napi_typeof(env, argv[2], &t) != napi_ok || (t != napi_undefined && napi_get_value_bool(env, argv[2], &sah) != napi_ok)) {
-            napi_throw_type_error(env, NULL, "bvhBuild(Float64Array vertices, Int32Array tris, sah?)");
+            napi_throw_type_error(env, NULL, "bvhBuild(Float64Array vertices, Int32Array tris, sah?, isolate?)");
             return NULL;
         }
     }
-    int (*build)(const double*, size_t, const int32_t*, size_t, float*, size_t, size_t*) = sah ? pt_bvh_build_sah : pt_bvh_build;
+    const uint8_t* iso = NULL;
+    size_t niso = 0;
+    if (argc > 3) {
+        napi_valuetype t;
+        napi_typedarray_type ti;
+        void* di = NULL;
+        size_t oi;
+        napi_value abi;
+        if (napi_typeof(env, argv[3], &t) != napi_ok ||
+            (t != napi_undefined && (napi_get_typedarray_info(env, argv[3], &ti, &niso, &di, &abi, &oi) != napi_ok ||
+                                     ti != napi_uint8_array))) {
+            napi_throw_type_error(env, NULL, "bvhBuild(..., isolate: Uint8Array of material flags)");
+            return NULL;
+        }
+        iso = (const uint8_t*)di;
+    }
     napi_typedarray_type t0, t1;
     size_t n0 = 0, n1 = 0, off;
     void *d0 = NULL, *d1 = NULL;
@@ -559,12 +576,15 @@ static napi_value js_bvh_build(napi_env env, napi_callback_info info) {
         return NULL;
     }
     size_t len = 0;
-    int rc = build((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, NULL, 0, &len);
+    int rc = !sah ? pt_bvh_build((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, NULL, 0, &len)
+                  : pt_bvh_build_sah2((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, iso, iso ? niso : 0, NULL, 0, &len);
     if (rc) return throw_pt(env, rc);
     napi_value buf, arr;
     void* data = NULL;
     CHECK_NAPI(env, napi_create_arraybuffer(env, len * sizeof(float), &data, &buf));
-    rc = build((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, (float*)data, len, &len);
+    rc = !sah ? pt_bvh_build((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, (float*)data, len, &len)
+              : pt_bvh_build_sah2((const double*)d0, n0 / 3, (const int32_t*)d1, n1 / 4, iso, iso ? niso : 0, (float*)data,
+                                  len, &len);
     if (rc) return throw_pt(env, rc);
     CHECK_NAPI(env, napi_create_typedarray(env, napi_float32_array, len, buf, 0, &arr));
     return arr;

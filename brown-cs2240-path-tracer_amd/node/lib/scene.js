@@ -119,11 +119,18 @@ function pack_group(intermediate, opts) {
         }
     });
     // native_bvh: the same build in C++ (pt_bvh_build), byte-identical, for big meshes; bvh 'sah':
-    // the fast binned-SAH tree (pt_bvh_build_sah) in the same layout — not the reference's topology
+    // the fast binned-SAH tree (pt_bvh_build_sah2) in the same layout — not the reference's topology —
+    // with the emitters (sum(Ke) > 0, program-raymarch.wgsl:136) in a leaf under the root, where the
+    // exit-distance pruning of the unchanged traversal cannot hide them
     if (opts && (opts.native_bvh || opts.bvh === 'sah')) {
         const tris = new Int32Array(bvh_objects.length * 4);
         bvh_objects.forEach((o, t) => tris.set(o.obj, 4 * t));
-        const bvh_data = require('./addon').load().bvhBuild(Float64Array.from(vertices), tris, opts.bvh === 'sah');
+        const emit = Uint8Array.from(intermediate.objects.map((o) => {
+            const ke = o.material.Ke || [0, 0, 0];
+            return ke[0] + ke[1] + ke[2] > 0 ? 1 : 0;
+        }));
+        const bvh_data = require('./addon').load().bvhBuild(Float64Array.from(vertices), tris, opts.bvh === 'sah',
+                                                             opts.bvh === 'sah' ? emit : undefined);
         return { triangle_data: packed_array, bvh_data, bounds: bvh_bounds };
     }
     const bvh = new BVH(bvh_objects, bvh_bounds, opts);

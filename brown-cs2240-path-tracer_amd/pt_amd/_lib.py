@@ -119,6 +119,7 @@ def load_library():
     L.pt_selftest_rcp.argtypes = [i, i, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
     L.pt_bvh_build.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_bvh_build_sah.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
+    L.pt_bvh_build_sah2.argtypes = [p, sz, p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_tonemap_async.argtypes = [p, p, sz, u32, p, p]
     L.pt_render_image.argtypes = [p, p, u32, u32, u32, i, i, p, p]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
@@ -134,7 +135,7 @@ def load_library():
     i32p = ctypes.POINTER(ctypes.c_int32)
     L.pt_scene_leaf_bvh.argtypes = [p, i, i32p, i32p, i32p]
     L.pt_selftest_leaf.argtypes = [p, i, i, u32, u32, p]
-    for fn in ("pt_scene_leaf_bvh", "pt_selftest_leaf", "pt_selftest_valu", "pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
+    for fn in ("pt_scene_leaf_bvh", "pt_selftest_leaf", "pt_selftest_valu", "pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_bvh_build_sah2", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
                "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
@@ -405,14 +406,22 @@ def selftest_valu(iters: int = 20000, reps: int = 5, packed: int = 0, device: in
     return float(ms.value), int(n.value)
 
 
-def bvh_build(vertices, tris, sah: bool = False) -> np.ndarray:
+def bvh_build(vertices, tris, sah: bool = False, isolate=None) -> np.ndarray:
     """Native BVH build + pack (host only, no GPU): vertices f64 [n, 3] (post-CTM), tris
     int32 [m, 4] = (i0, i1, i2, material) with 1-based vertex indices -> packed bvh_data (f32).
-    sah=True: the fast binned-SAH tree (pt_bvh_build_sah), same layout, not the reference's tree."""
+    sah=True: the fast binned-SAH tree (pt_bvh_build_sah), same layout, not the reference's tree;
+    isolate: per material id a flag (the emitters) — their triangles go under the root's left child
+    (pt_bvh_build_sah2)."""
     L = load_library()
-    fn = L.pt_bvh_build_sah if sah else L.pt_bvh_build
     v = np.ascontiguousarray(vertices, dtype=np.float64).reshape(-1)
     t = np.ascontiguousarray(tris, dtype=np.int32).reshape(-1)
+    if sah and isolate is not None:
+        iso = np.ascontiguousarray(isolate, dtype=np.uint8).reshape(-1)
+
+        def fn(vp, nv, tp, nt, op, cap, nref):
+            return L.pt_bvh_build_sah2(vp, nv, tp, nt, _ptr(iso), iso.size, op, cap, nref)
+    else:
+        fn = L.pt_bvh_build_sah if sah else L.pt_bvh_build
     n = ctypes.c_size_t(0)
     _check(fn(_ptr(v), v.size // 3, _ptr(t), t.size // 4, None, 0, ctypes.byref(n)))
     out = np.empty(n.value, np.float32)

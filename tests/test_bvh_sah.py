@@ -9,6 +9,8 @@ reference's packed layout (src/packer.ts:83-137) for the unchanged traversal
   * leaves of at most kSahMaxLeaf = 8 entries, except at the depth cap (kSahMaxDepth = 28, root 1);
   * every child box (the parent's [o+5..10] / [o+11..16]) contains the f32 vertices of every
     triangle below that child, and the outer bounds [0..5] contain all of them;
+  * every non-empty child box has a positive extent on every axis (ray-bbox-intersection.wgsl's
+    `tmax > max(tmin, 0)` never enters a flat box; the builder pads by one f32 ulp);
   * pre-order layout: an internal node's left child follows it at o + 17 (packer.ts:112).
 The GPU renders on these buffers are compared with the oracle bit for bit in
 tests/test_gpu_fast_trees.py.
@@ -72,6 +74,8 @@ def check_sah(verts64, recs, bvh):
         if len(e):
             p = v32[e[:, :3].reshape(-1) - 1]
             assert np.all(p >= lo) and np.all(p <= hi), "a leaf's box must contain its triangles"
+            # positive extent on every axis: the slab test never enters a zero-thickness box
+            assert np.all(lo < hi), "a leaf box must not be flat (coplanar axis-aligned triangles)"
     for lo, hi, below in inner:
         e = np.concatenate([leaves[i][0] for i in below])
         if len(e):
@@ -95,6 +99,63 @@ def scene_inputs(xml_path, assets):
         for i in range(0, len(ind), 3):
             recs.append([int(ind[i]), int(ind[i + 1]), int(ind[i + 2]), mat_i])
     return np.array(g["vertices"], np.float64).reshape(-1, 3), np.array(recs, np.int32)
+
+
+def emitter_flags(xml_path, assets):
+    """Per material id: sum(Ke) > 0 (program-raymarch.wgsl:136), as the Node host flags them."""
+    with open(xml_path) as f:
+        _, prims = so.load_scene_xml(f.read())
+    p = prims[0]
+    path = os.path.join(assets, p["path"].lstrip("/").split("/", 1)[1])
+    mtl = open(path[:-3] + "mtl").read() if os.path.exists(path[:-3] + "mtl") else ""
+    g = so.parse_obj(open(path).read(), mtl, p["ctm"])
+    return np.array([1 if sum(o["material"]["Ke"]) > 0 else 0 for o in g["objects"]], np.uint8)
+
+
+def check_isolated(verts, recs, flags):
+    """pt_bvh_build_sah2: the emitters' triangles in the root's left child — one leaf when they are
+    at most 8 — the rest on the right; still a valid SAH tree over all triangles."""
+    bvh = pt_amd.bvh_build(verts, recs, sah=True, isolate=flags)
+    check_sah(verts, recs, bvh)
+    lit = recs[flags[recs[:, 3]] != 0]
+    left = int(bvh[6 + 2])
+    if 0 < len(lit) <= K_MAX_LEAF:
+        assert bvh[left] == 1.0, "the emitters form one leaf under the root"
+        got = bvh[left + 17: left + 17 + int(bvh[left + 4])].reshape(-1, 4).astype(np.int64)
+        assert sorted(map(tuple, got)) == sorted(map(tuple, lit.astype(np.int64)))
+    return bvh
+
+
+@pytest.mark.parametrize("scene", ALL_SCENES)
+def test_sah_emitters_under_the_root(scene):
+    assets = os.path.join(SCENES, "scene_assets")
+    xml = os.path.join(assets, scene + ".xml")
+    verts, recs = scene_inputs(xml, assets)
+    flags = emitter_flags(xml, assets)
+    assert flags.any()  # every scene has its light
+    check_isolated(verts, recs, flags)
+    # no flags: pt_bvh_build_sah itself
+    assert np.array_equal(pt_amd.bvh_build(verts, recs, sah=True, isolate=np.zeros_like(flags)).view(np.uint32),
+                          pt_amd.bvh_build(verts, recs, sah=True).view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [1000, 12500])
+def test_sah_emitters_under_the_root_synthetic(n, tmp_path):
+    xml = synth_scene.write(n, str(tmp_path))
+    assets = os.path.join(str(tmp_path), "scene_assets")
+    verts, recs = scene_inputs(xml, assets)
+    check_isolated(verts, recs, emitter_flags(xml, assets))
+
+
+def test_node_sah_pack_isolates_emitters(tmp_path):
+    """The Node host's --bvh sah packs through pt_bvh_build_sah2 with the emitter flags."""
+    from conftest import pack_with_node
+    assets = os.path.join(SCENES, "scene_assets")
+    xml = os.path.join(assets, "CornellBox-Glossy.xml")
+    p = pack_with_node(xml, str(tmp_path / "p"), "--bvh", "sah")
+    verts, recs = scene_inputs(xml, assets)
+    want = pt_amd.bvh_build(verts, recs, sah=True, isolate=emitter_flags(xml, assets))
+    assert np.array_equal(p.bvh_data.view(np.uint32), want.view(np.uint32))
 
 
 @pytest.mark.parametrize("scene", ALL_SCENES)
