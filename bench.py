@@ -435,12 +435,16 @@ def main():
                          "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3),
                          "pipeline": {"bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
                                       "achieved": round(pipeline, 2), "frac": round(pipeline / HBM_PEAK_GBS, 4)},
-                         "valu_issue": ({"bound": "valu_issue", "frac": round(valu[0], 4),
-                                         "def": "k x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE): VALU issue over "
-                                                "the SIMDs' peak issue rate, kernel alone (PMC pass); k calibrated so "
-                                                "that a kernel issuing v_fma_f32 at peak reads 1.0",
-                                         "calibration": valu_cal or "uncalibrated (k = 4)",
-                                         "source": valu[1]} if valu else None),
+                         # not a utilisation (it can exceed 1): VALU wave-instructions priced at the
+                         # SIMD cycles of a chain of v_fma_f32, over all SIMD cycles
+                         "valu_fma_equiv_density": ({"value": round(valu[0], 4),
+                                                     "def": "k x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE), kernel "
+                                                            "alone (PMC pass), k = the SIMD cycles per v_fma_f32 "
+                                                            "wave-instruction at peak (pt_selftest_valu reads 1.0); "
+                                                            "an FMA-equivalent issue density, above 1 when the mix "
+                                                            "issues faster than FMA chains",
+                                                     "calibration": valu_cal or "uncalibrated (k = 4)",
+                                                     "source": valu[1]} if valu else None),
                          "kernels_ms_warmup_step": {k: round(v["total_ms"] / max(args.warmup, 1), 3)
                                                     for k, v in prof_warm.items()},
                          "render_ms_steps": [round(x, 2) for x in render_ms]},

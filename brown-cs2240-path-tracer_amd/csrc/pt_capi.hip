@@ -1179,6 +1179,26 @@ int pt_selftest_leaf(pt_scene* s, int leaf, int mode, uint32_t seed, uint32_t nr
     return PT_OK;
 }
 
+int pt_selftest_div(int device, int mode, uint32_t b_first, uint32_t b_count, uint32_t a_first, uint32_t a_count,
+                    uint32_t seed, uint64_t* mismatches, uint32_t* failing_a, uint32_t* failing_b) {
+    if (!mismatches || mode < 0 || mode > 1 || b_count == 0 || a_count == 0) return fail(PT_ERR_INVALID, "bad argument");
+    if (mode == 0 && ((uint64_t)b_first + b_count > (1u << 23) || (uint64_t)a_first + a_count > (1u << 23)))
+        return fail(PT_ERR_INVALID, "mantissa range beyond 2^23");
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 3 * sizeof(unsigned long long)));
+    unsigned long long h[3] = {0, 0, 0};
+    hipError_t e = hipMemset(d, 0, sizeof(h));
+    if (e == hipSuccess) e = launch_selftest_div(mode, b_first, b_count, a_first, a_count, seed, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
+    *mismatches = h[0];
+    if (failing_a) *failing_a = (uint32_t)h[1];
+    if (failing_b) *failing_b = (uint32_t)h[2];
+    return PT_OK;
+}
+
 int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
                     uint32_t* failing_bits) {
     if (!mismatches || steps < -1 || steps > 2 || lo_bits > hi_bits || hi_bits >= 0x80000000u)

@@ -386,10 +386,20 @@ __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ra
             const int n = (int)__builtin_ctzll(pend);
             pend &= pend - 1;
             const BfNode& bn = sc.bfnode[n];
-            const float ld = ray_box(r, bn.lmin[0], bn.lmin[1], bn.lmin[2], bn.lmax[0], bn.lmax[1], bn.lmax[2]);
-            const float rd = ray_box(r, bn.rmin[0], bn.rmin[1], bn.rmin[2], bn.rmax[0], bn.rmax[1], bn.rmax[2]);
-            const bool li = 0.0f < ld, ri = 0.0f < rd;
             const bool lint = (bn.lm & kInner) != 0, rint = (bn.rm & kInner) != 0;
+            // A leaf child matters only while it holds a hit entry not yet tested: its other
+            // entries cannot change best (misses, or repeats the mailbox skips).  So its box test
+            // — the reference's li — is needed only then (internal children always: their box
+            // value drives the pruning), and is skipped when no lane of the wave needs it.  An
+            // irrelevant leaf taken as unhit changes nothing: tested gains no bit a later rh
+            // reads, and the tie-break scan (mb_first_node) only looks for the pair's untested
+            // hit entries, none of which sit in it.
+            const bool lneed = lint || (bn.lm & hits & ~tested) != 0;
+            const bool rneed = rint || (bn.rm & hits & ~tested) != 0;
+            float ld = -1.0f, rd = -1.0f;
+            if (wave_any(lneed)) ld = ray_box(r, bn.lmin[0], bn.lmin[1], bn.lmin[2], bn.lmax[0], bn.lmax[1], bn.lmax[2]);
+            if (wave_any(rneed)) rd = ray_box(r, bn.rmin[0], bn.rmin[1], bn.rmin[2], bn.rmax[0], bn.rmax[1], bn.rmax[2]);
+            const bool li = lneed & (0.0f < ld), ri = rneed & (0.0f < rd);
             const uint64_t m = ((li & !lint) ? bn.lm : 0ull) | ((ri & !rint) ? bn.rm : 0ull);
             uint64_t rh = m & ~tested & hits;
             tested |= m;
