@@ -14,7 +14,7 @@ L=brown-cs2240-path-tracer_amd/lib/libpt_hip.so
 AB=gpurun_out/profiles/r04c_ab_replay_div.log
 : > $AB
 for sc in CornellBox CornellBox-Mirror; do
-  for order in "$L ablib/base/libpt_hip.so ablib/skip/libpt_hip.so ablib/div/libpt_hip.so" "ablib/div/libpt_hip.so ablib/skip/libpt_hip.so ablib/base/libpt_hip.so $L"; do
+  for order in "$L ablib/base/libpt_hip.so ablib/skip/libpt_hip.so ablib/div/libpt_hip.so ablib/rcp/libpt_hip.so" "ablib/rcp/libpt_hip.so ablib/div/libpt_hip.so ablib/skip/libpt_hip.so ablib/base/libpt_hip.so $L"; do
     d=8; [ $sc = CornellBox-Mirror ] && d=16
     echo "== $sc depth $d order: $order" >> $AB
     timeout -k 10 300 python3 scripts/ab_libs.py $order --scene $sc --res 1024 --spp 64 --depth $d --rounds 5 --async-torch >> $AB 2>&1
