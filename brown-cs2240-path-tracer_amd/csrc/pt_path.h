@@ -196,6 +196,7 @@ __device__ __forceinline__ void stage_scene_lds(SceneView& sc, char* base) {
     if (sc.bfnode) {
         sc.bfnode = reinterpret_cast<const BfNode*>(base + sc.off_bfnode);
         sc.bfmap = reinterpret_cast<const int32_t*>(base + sc.off_bfmap);
+        sc.bfsub = reinterpret_cast<const uint64_t*>(base + sc.off_bfsub);
     }
 }
 

@@ -35,9 +35,26 @@ def make_case(rng):
     return children, leaves, tvals, hits, boxes
 
 
-def replay(case, skip):
+def subtree_uids(children, leaves):
+    """uid union below each internal node (BfNode's subtree masks, pt_capi.hip build_layout)."""
+    memo = {}
+
+    def rec(n):
+        if n not in memo:
+            u = set()
+            for side, c in enumerate(children[n]):
+                u |= rec(c) if c is not None else set(leaves.get((n, side), []))
+            memo[n] = u
+        return memo[n]
+    for n in range(len(children)):
+        rec(n)
+    return memo
+
+
+def replay(case, skip, skip_subtrees=False):
     children, leaves, tvals, hits, boxes = case
     pre, order = preorder_right_first(children)
+    sub = subtree_uids(children, leaves)
     tmin = min((tvals[u] for u in hits), default=3.0e38)
     if not hits:
         return -1, -1.0
@@ -75,6 +92,9 @@ def replay(case, skip):
         else:
             tl = li and lint and not (best_t > 0.0 and ld > best_t)
             tr = ri and rint and not (best_t > 0.0 and rd > best_t)
+            if skip_subtrees:  # a subtree without an untested hit entry cannot change best
+                tl = tl and bool((sub[l] & hits) - tested)
+                tr = tr and bool((sub[r] & hits) - tested)
             if tl:
                 pend |= 1 << pre[l]
             if tr:
@@ -87,7 +107,9 @@ def test_skipping_unneeded_leaf_boxes_changes_nothing(seed):
     rng = random.Random(seed)
     for _ in range(50):
         case = make_case(rng)
-        assert replay(case, True) == replay(case, False)
+        want = replay(case, False)
+        assert replay(case, True) == want
+        assert replay(case, True, skip_subtrees=True) == want  # and whole subtrees without one
 
 
 def test_the_model_has_teeth():
