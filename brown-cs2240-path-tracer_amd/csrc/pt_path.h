@@ -56,22 +56,27 @@ __device__ __forceinline__ void bsdf_continue(const Mat& m, f3 hp, f3 hn, Ray& r
     bool fresnel_reflect = false;
     if (m.illum == 7.0f) {
         f3 wi = ray.d;
-        float eta_i = 1.0f, eta_t = 2.5f;
         float cos_i = clampf(dot(wi, hn), -1.0f, 1.0f);
         f3 nn = hn;
-        if (cos_i < 0.0f) {
+        // eta_i, eta_t = 1, 2.5 (entering) or 2.5, 1; the quotients of these constants are folded
+        // by the compiler with the same IEEE rounding: q = (eta_i - eta_t) / (eta_i + eta_t),
+        // ratio = eta_i / eta_t
+        constexpr float kQin = (1.0f - 2.5f) / (1.0f + 2.5f), kQout = (2.5f - 1.0f) / (2.5f + 1.0f);
+        constexpr float kRatioIn = 1.0f / 2.5f, kRatioOut = 2.5f / 1.0f;
+        const bool entering = cos_i < 0.0f;
+        if (entering) {
             cos_i = -cos_i;
         } else {
-            eta_i = 2.5f; eta_t = 1.0f; nn = -nn;
+            nn = -nn;
         }
-        float q = (eta_i - eta_t) / (eta_i + eta_t);
+        float q = entering ? kQin : kQout;
         float r0 = q * q;
         float r_theta = fmaf(1.0f - r0, pow5_lit(1.0f - cos_i), r0);
         seed = hash1u(seed + 7u);
         if (hash1(seed) < r_theta) {
             fresnel_reflect = true;
         } else {
-            float ratio = eta_i / eta_t;
+            float ratio = entering ? kRatioIn : kRatioOut;
             float k = fmaf(-(ratio * ratio), fmaf(-cos_i, cos_i, 1.0f), 1.0f);
             float cf = fmaf(ratio, cos_i, -sqrtf(clampf(k, 0.0f, 1.0f)));
             f3 nd = mk(fmaf(cf, nn.x, ratio * wi.x), fmaf(cf, nn.y, ratio * wi.y), fmaf(cf, nn.z, ratio * wi.z));
