@@ -21,7 +21,13 @@ for sc in CornellBox CornellBox-Mirror; do
     rc=$?; echo "ab $sc rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
 done
-grep -v "^ *$" $AB | tail -30
+# a rank's share at N = 8 (32 frames: one batch, its tails weigh twice) — the early exit of idle blocks
+for order in "$L ablib/rcp/libpt_hip.so ablib/base/libpt_hip.so" "ablib/base/libpt_hip.so ablib/rcp/libpt_hip.so $L"; do
+  echo "== CornellBox depth 8, 32 frames, order: $order" >> $AB
+  timeout -k 10 300 python3 scripts/ab_libs.py $order --scene CornellBox --res 1024 --spp 32 --depth 8 --rounds 7 --async-torch >> $AB 2>&1
+  rc=$?; echo "ab share rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+grep -v "^ *$" $AB | tail -40
 bash scripts/gpu_r04b.sh
 # the box's own toolchain builds HEAD: the sources of the shipped library, built from scratch in a
 # scratch directory, give a library whose build id is the shipped one's
