@@ -143,7 +143,6 @@ struct HostLayout {
     std::vector<float4> tnorm;    // vertex-normal mode: 3 per record (SceneView::tnorm)
     std::vector<BfNode> bfnode;   // mailbox scenes with <= 64 internal nodes, <= 63 entries (SceneView::bfnode)
     std::vector<int32_t> bfmap;
-    std::vector<uint64_t> bfsub;  // per pre-order node: uid set below it (SceneView::bfsub)
     std::vector<LNode> lnodes;    // leaf BVHs (SceneView::lnodes), and per such leaf (first record, entries, nodes)
     std::vector<int32_t> lidx;
     std::vector<Tri> ltris;       // per chunk slot: its entry's record, lbvh = the entry's position in its leaf
@@ -323,15 +322,6 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                     if (nd.rcnt < 0) st.push_back(nd.rref);
                 }
                 L.bfnode.resize(L.nodes.size());
-                // subtree uid sets, children before parents: pre-order numbers of children are larger
-                L.bfsub.assign(L.bfmap.size(), 0);
-                for (size_t i = L.bfmap.size(); i-- > 0;) {
-                    const Node& nd = L.nodes[(size_t)L.bfmap[i]];
-                    uint64_t u = 0;
-                    u |= nd.lcnt < 0 ? L.bfsub[(size_t)pre[(size_t)nd.lref]] : (nd.lcnt > 0 ? L.lmask[(size_t)nd.lref] : 0ull);
-                    u |= nd.rcnt < 0 ? L.bfsub[(size_t)pre[(size_t)nd.rref]] : (nd.rcnt > 0 ? L.lmask[(size_t)nd.rref] : 0ull);
-                    L.bfsub[i] = u;
-                }
                 for (size_t i = 0; i < L.bfmap.size(); ++i) {
                     const Node& nd = L.nodes[(size_t)L.bfmap[i]];
                     BfNode& b = L.bfnode[i];
@@ -628,8 +618,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_lmask = align_up(o_lights + L.lights.size() * sizeof(Light), 16);
     const size_t o_bfnode = align_up(o_lmask + L.lmask.size() * sizeof(uint64_t), 16);
     const size_t o_bfmap = align_up(o_bfnode + L.bfnode.size() * sizeof(BfNode), 16);
-    const size_t o_bfsub = align_up(o_bfmap + L.bfmap.size() * sizeof(int32_t), 16);
-    const size_t o_cnt = align_up(o_bfsub + L.bfsub.size() * sizeof(uint64_t), 256);
+    const size_t o_cnt = align_up(o_bfmap + L.bfmap.size() * sizeof(int32_t), 256);
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
     const size_t o_lnode = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
@@ -646,7 +635,6 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_lmask, L.lmask.data(), L.lmask.size() * sizeof(uint64_t)) != hipSuccess ||
         up(o_bfnode, L.bfnode.data(), L.bfnode.size() * sizeof(BfNode)) != hipSuccess ||
         up(o_bfmap, L.bfmap.data(), L.bfmap.size() * sizeof(int32_t)) != hipSuccess ||
-        up(o_bfsub, L.bfsub.data(), L.bfsub.size() * sizeof(uint64_t)) != hipSuccess ||
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
         up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess) {
@@ -683,9 +671,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.bfmap = L.bfmap.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_bfmap);
     s->view.off_bfnode = (uint32_t)(o_bfnode - o_nodes);
     s->view.off_bfmap = (uint32_t)(o_bfmap - o_nodes);
-    s->view.bfsub = L.bfsub.empty() ? nullptr : reinterpret_cast<const uint64_t*>(base + o_bfsub);
-    s->view.off_bfsub = (uint32_t)(o_bfsub - o_nodes);
-    s->view.span_bytes = (uint32_t)align_up(o_bfsub + L.bfsub.size() * sizeof(uint64_t) - o_nodes, 16);
+    s->view.span_bytes = (uint32_t)align_up(o_bfmap + L.bfmap.size() * sizeof(int32_t) - o_nodes, 16);
     s->d_counters = reinterpret_cast<Counters*>(base + o_cnt);
     s->info = L.info;
     s->info.device_bytes = total;
@@ -1190,26 +1176,6 @@ int pt_selftest_leaf(pt_scene* s, int leaf, int mode, uint32_t seed, uint32_t nr
     if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)nrays * 6 * sizeof(int32_t), hipMemcpyDeviceToHost);
     hipFree(d);
     if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
-    return PT_OK;
-}
-
-int pt_selftest_div(int device, int mode, uint32_t b_first, uint32_t b_count, uint32_t a_first, uint32_t a_count,
-                    uint32_t seed, uint64_t* mismatches, uint32_t* failing_a, uint32_t* failing_b) {
-    if (!mismatches || mode < 0 || mode > 1 || b_count == 0 || a_count == 0) return fail(PT_ERR_INVALID, "bad argument");
-    if (mode == 0 && ((uint64_t)b_first + b_count > (1u << 23) || (uint64_t)a_first + a_count > (1u << 23)))
-        return fail(PT_ERR_INVALID, "mantissa range beyond 2^23");
-    HIP_TRY(hipSetDevice(device));
-    unsigned long long* d = nullptr;
-    HIP_TRY(hipMalloc(&d, 3 * sizeof(unsigned long long)));
-    unsigned long long h[3] = {0, 0, 0};
-    hipError_t e = hipMemset(d, 0, sizeof(h));
-    if (e == hipSuccess) e = launch_selftest_div(mode, b_first, b_count, a_first, a_count, seed, d, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-    hipFree(d);
-    if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));
-    *mismatches = h[0];
-    if (failing_a) *failing_a = (uint32_t)h[1];
-    if (failing_b) *failing_b = (uint32_t)h[2];
     return PT_OK;
 }
 

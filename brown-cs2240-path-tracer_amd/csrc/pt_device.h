@@ -772,7 +772,7 @@ __device__ __forceinline__ Hit hit_data(const SceneView& sc, const Ray& r, int r
     Hit h;
     h.p = madd(r.o, r.d, t);
     const f3 e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
-    h.n = normalize_r(cross(e1, e2));
+    h.n = normalize(cross(e1, e2));
     h.mat = sc.tris[rec].mat;
     if (sc.vnormals) {
         const float4 n0 = sc.tnorm[3 * rec];
@@ -785,7 +785,7 @@ __device__ __forceinline__ Hit hit_data(const SceneView& sc, const Ray& r, int r
             const float u = inv_det * dot(s, rce2);
             const float v = inv_det * dot(r.d, cross(s, e1));
             const float w = (1.0f - u) - v;
-            h.n = normalize_r(mk(fmaf(v, n2.x, fmaf(u, n1.x, w * n0.x)), fmaf(v, n2.y, fmaf(u, n1.y, w * n0.y)),
+            h.n = normalize(mk(fmaf(v, n2.x, fmaf(u, n1.x, w * n0.x)), fmaf(v, n2.y, fmaf(u, n1.y, w * n0.y)),
                                fmaf(v, n2.z, fmaf(u, n1.z, w * n0.z))));
         }
     }
@@ -826,7 +826,7 @@ __device__ __forceinline__ f3 sample_area_lights(const SceneView& sc, f3 x, uint
     const float4* lp = reinterpret_cast<const float4*>(sc.lights + k);
     float4 a = lp[0], b = lp[1], c = lp[2];
     f3 pt = sample_triangle(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), seed * 11u + 17u);
-    return normalize_r(pt - x);
+    return normalize(pt - x);
 }
 
 // samplers.wgsl:15-46: cosine hemisphere around n (Duff et al. 2017 ONB)
@@ -840,11 +840,11 @@ __device__ __forceinline__ f3 sample_hemisphere(f3 N, uint32_t seed, float& pdf)
     sincos_p(theta, st, ct);
     float nx = cp * st, ny = sp * st, nz = ct;
     float s = N.z < 0.0f ? -1.0f : 1.0f;
-    float a = -div_r(1.0f, recip(s + N.z));  // = -1.0f / (s + N.z), bit for bit
+    float a = -1.0f / (s + N.z);
     float b = (N.x * N.y) * a;
     f3 T = mk(fmaf((s * N.x) * N.x, a, 1.0f), s * b, (-s) * N.x);
     f3 B = mk(b, fmaf(N.y * N.y, a, s), -N.y);
-    pdf = div_r(ct, recip_const(kPI));  // = ct / kPI
+    pdf = ct / kPI;
     return mk(fmaf(N.x, nz, fmaf(B.x, ny, T.x * nx)), fmaf(N.y, nz, fmaf(B.y, ny, T.y * nx)),
               fmaf(N.z, nz, fmaf(B.z, ny, T.z * nx)));
 }
@@ -882,7 +882,7 @@ __device__ __forceinline__ Ray camera_ray(const FrameParams& fp, uint32_t x, uin
     float len = sqrtf(fmaf(dw, dw, fmaf(dz, dz, fmaf(dy, dy, dx * dx))));  // vec4 normalize
     Ray r;
     r.o = mk(fp.cam[0], fp.cam[1], fp.cam[2]);
-    r.d = div_r(mk(dx, dy, dz), recip(len));  // = (dx / len, dy / len, dz / len)
+    r.d = mk(dx / len, dy / len, dz / len);
     r.inv = rcp3(r.d);
     seed_out = hash1u(ts + (index * 67u + t));
     return r;

@@ -157,8 +157,6 @@ hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t*
 hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t stream);
 
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
-hipError_t launch_selftest_div(int mode, uint32_t b0, uint32_t nb, uint32_t a0, uint32_t na, uint32_t seed,
-                               unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);
 hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, hipStream_t stream);
 hipError_t launch_selftest_leaf(const SceneView& sc, int rec0, int n, int mode, uint32_t seed, uint32_t nrays, int32_t* out,

@@ -156,56 +156,6 @@ __global__ void k_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned lon
     }
 }
 
-// pt_math.h div_r against the IEEE division.  mode 0: every a mantissa in [a0, a0 + na) against
-// every b mantissa in [b0, b0 + nb), both in [1, 2) (thread = b, loop over a): the case every
-// in-range quotient scales to.  mode 1: nb * na random bit patterns of a and b (any exponent,
-// zeros, subnormals, infinities, NaNs: the range check must send each case the fast path cannot
-// take to the division; NaN results compare equal).  bad[0] += mismatches, bad[1] / bad[2] = the
-// bits of some failing a / b.
-__global__ __launch_bounds__(256) void k_selftest_div(int mode, uint32_t b0, uint32_t nb, uint32_t a0, uint32_t na,
-                                                      uint32_t seed, unsigned long long* bad) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nb) return;
-    unsigned long long mis = 0;
-    uint32_t fa = 0, fb = 0;
-    if (mode == 0) {
-        const float b = __builtin_bit_cast(float, 0x3f800000u | (b0 + i));
-        const Recip d = recip(b);
-        for (uint32_t k = 0; k < na; ++k) {
-            const float a = __builtin_bit_cast(float, 0x3f800000u | (a0 + k));
-            const float q = div_r(a, d), want = a / b;
-            if (__builtin_bit_cast(uint32_t, q) != __builtin_bit_cast(uint32_t, want)) { ++mis; fa = f_bits(a); fb = f_bits(b); }
-        }
-    } else {
-        uint32_t st = (i + b0) * 0x9e3779b9u ^ seed;
-        for (uint32_t k = 0; k < na; ++k) {
-            st = hmix(st + k);
-            const uint32_t ua = st;
-            st = hmix(st ^ 0x5bd1e995u);
-            const uint32_t ub = st;
-            // bias half of the pairs towards the range limits: exponents within +-60 of the bias
-            const uint32_t sa = (k & 1) ? ((ua & 0x807fffffu) | ((67u + (ua >> 24) % 120u) << 23)) : ua;
-            const uint32_t sb = (k & 1) ? ((ub & 0x807fffffu) | ((67u + (ub >> 24) % 120u) << 23)) : ub;
-            const float a = __builtin_bit_cast(float, sa), b = __builtin_bit_cast(float, sb);
-            const float q = div_r(a, recip(b)), want = a / b;
-            const bool same = __builtin_bit_cast(uint32_t, q) == __builtin_bit_cast(uint32_t, want) ||
-                              (__builtin_isnan(q) && __builtin_isnan(want));
-            if (!same) { ++mis; fa = sa; fb = sb; }
-        }
-    }
-    if (mis) {
-        atomicAdd(&bad[0], mis);
-        atomicExch(&bad[1], (unsigned long long)fa);
-        atomicExch(&bad[2], (unsigned long long)fb);
-    }
-}
-
-hipError_t launch_selftest_div(int mode, uint32_t b0, uint32_t nb, uint32_t a0, uint32_t na, uint32_t seed,
-                               unsigned long long* bad, hipStream_t stream) {
-    hipLaunchKernelGGL(k_selftest_div, dim3((nb + 255) / 256), dim3(256), 0, stream, mode, b0, nb, a0, na, seed, bad);
-    return hipGetLastError();
-}
-
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream) {
     hipLaunchKernelGGL(k_selftest_rcp, dim3(8192), dim3(256), 0, stream, steps, lo, hi, bad);
     return hipGetLastError();

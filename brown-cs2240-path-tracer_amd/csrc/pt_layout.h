@@ -129,10 +129,7 @@ struct SceneView {
     // the LDS span at off_bfnode / off_bfmap
     const BfNode* bfnode;
     const int32_t* bfmap;
-    // bfsub[i] = the uid set of every leaf entry below pre-order node i (the replay skips a subtree
-    // without an untested hit entry: it cannot change the closest hit); inside the LDS span
-    const uint64_t* bfsub;
-    uint32_t off_bfnode, off_bfmap, off_bfsub;
+    uint32_t off_bfnode, off_bfmap;
     // vertex-normal mode (pt_scene_set_vertex_normals; the reference's commented-out branch,
     // intersection-logic.wgsl:81-108): per record (v0n, v1n, v2n) as 3 float4, v0n.w = 1 where
     // i2 < vn_range (the branch applies); global memory, read for the winning record only

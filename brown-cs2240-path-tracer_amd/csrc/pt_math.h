@@ -73,34 +73,6 @@ __device__ __forceinline__ float rcp_rn(float x, int steps = kRcpSteps) {
 }
 PT_HD float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 
-// ---- Division from the correctly rounded reciprocal -------------------------------------------
-// a / b as q0 = a y, r = a - b q0 (exact: one FMA), q = q0 + r y (Markstein's correction) with
-// y = rcp_rn(b) = RN(1 / b).  Equals the IEEE quotient bit for bit whenever 2^-50 <= |b| <= 2^50
-// and 2^-50 <= |q0| <= 2^50: no step under- or overflows and the residual's grid
-// (2^(e_b + e_q0 - 46) >= 2^-146) lies above the subnormal floor, so every such case is the
-// [1, 2) x [1, 2) case scaled by powers of two — which pt_selftest_div checks on the device for
-// every pair of mantissas (2^46 pairs, scripts/check_div.py; sampled in tests/test_gpu_parity.py).
-// Outside that range the IEEE division runs (a divergent branch no lane takes in practice).
-// ~5 VALU per quotient plus ~5 per denominator instead of ~11 per IEEE division: the shared
-// denominators of normalize, the NEE attenuation and the BSDF weight pay one reciprocal.
-__device__ __forceinline__ bool quot_range(float x) { return fabsf(x) >= 0x1p-50f && fabsf(x) <= 0x1p50f; }
-struct Recip {
-    float b, y;
-    bool ok;
-};
-__device__ __forceinline__ Recip recip(float b) { return Recip{b, rcp_rn(b), quot_range(b)}; }
-// a compile-time denominator: y = RN(1 / b) folded by the compiler
-__device__ __forceinline__ constexpr Recip recip_const(float b) { return Recip{b, 1.0f / b, true}; }
-__device__ __forceinline__ float div_r(float a, const Recip& d) {
-    const float q0 = a * d.y;
-    float q = fmaf(fmaf(-d.b, q0, a), d.y, q0);
-    if (!(d.ok & quot_range(q0))) q = a / d.b;
-    return q;
-}
-__device__ __forceinline__ f3 div_r(f3 a, const Recip& d) { return f3{div_r(a.x, d), div_r(a.y, d), div_r(a.z, d)}; }
-// normalize(a) = a / length(a), the three quotients from one reciprocal (bit-identical)
-__device__ __forceinline__ f3 normalize_r(f3 a) { return div_r(a, recip(length(a))); }
-
 PT_HD float bits_f(uint32_t u) { return __builtin_bit_cast(float, u); }
 PT_HD uint32_t f_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
 

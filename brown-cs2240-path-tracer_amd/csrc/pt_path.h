@@ -31,9 +31,9 @@ __device__ __forceinline__ f3 nee_contrib(const Mat& m, f3 wi, f3 hp, f3 hn, f3 
         f3 refl = reflect(wi, hn);
         float q = dot(refl, ldir);
         if (q < 0.0f) {
-            brdf = div_r(m.Kd * (-q), recip_const(kPI));  // = (m.Kd * (-q)) / kPI
+            brdf = (m.Kd * (-q)) / kPI;
         } else {
-            float sf = div_r((m.Ns + 2.0f) * pow_p(q, m.Ns), recip_const(2.0f * kPI));  // = (...) / (2 kPI)
+            float sf = ((m.Ns + 2.0f) * pow_p(q, m.Ns)) / (2.0f * kPI);
             brdf = m.Ks * sf;
         }
     } else {
@@ -44,7 +44,7 @@ __device__ __forceinline__ f3 nee_contrib(const Mat& m, f3 wi, f3 hp, f3 hn, f3 
     f3 c = (beta * nm.Ke) * brdf;
     c = c * d1;
     c = c * d2;
-    c = div_r(c, recip(att));  // = c / att (pt_math.h div_r: bit for bit)
+    c = c / att;
     return c * inv_ntri;
 }
 
@@ -82,14 +82,14 @@ __device__ __forceinline__ void bsdf_continue(const Mat& m, f3 hp, f3 hn, Ray& r
             f3 nd = mk(fmaf(cf, nn.x, ratio * wi.x), fmaf(cf, nn.y, ratio * wi.y), fmaf(cf, nn.z, ratio * wi.z));
             ray = ray_eps(hp, nd);
             spec = true;
-            beta = beta * div_r(1.0f, recip(rr));  // = beta * (1.0f / rr)
+            beta = beta * (1.0f / rr);
             return;
         }
     }
     if (m.Ns > 500.0f || fresnel_reflect) {
         ray = ray_eps(hp, reflect(ray.d, hn));
         spec = true;
-        beta = beta * div_r(1.0f, recip(rr));  // = beta * (1.0f / rr)
+        beta = beta * (1.0f / rr);
         return;
     }
     float pdf;
@@ -110,7 +110,7 @@ __device__ __forceinline__ void bsdf_continue(const Mat& m, f3 hp, f3 hn, Ray& r
         brdf = m.Kd_pi;  // = m.Kd / kPI, bit for bit (precomputed per material)
     }
     float cosn = dot(nr.d, hn) + 0.0f;  // vec4 dot: + w*w (= +0)
-    f3 f = div_r(brdf * cosn, recip(pdf * rr));  // = (brdf * cosn) / (pdf * rr)
+    f3 f = (brdf * cosn) / (pdf * rr);
     beta = beta * f;
     ray = nr;
 }
@@ -201,7 +201,6 @@ __device__ __forceinline__ void stage_scene_lds(SceneView& sc, char* base) {
     if (sc.bfnode) {
         sc.bfnode = reinterpret_cast<const BfNode*>(base + sc.off_bfnode);
         sc.bfmap = reinterpret_cast<const int32_t*>(base + sc.off_bfmap);
-        sc.bfsub = reinterpret_cast<const uint64_t*>(base + sc.off_bfsub);
     }
 }
 

@@ -386,23 +386,10 @@ __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ra
             const int n = (int)__builtin_ctzll(pend);
             pend &= pend - 1;
             const BfNode& bn = sc.bfnode[n];
+            const float ld = ray_box(r, bn.lmin[0], bn.lmin[1], bn.lmin[2], bn.lmax[0], bn.lmax[1], bn.lmax[2]);
+            const float rd = ray_box(r, bn.rmin[0], bn.rmin[1], bn.rmin[2], bn.rmax[0], bn.rmax[1], bn.rmax[2]);
+            const bool li = 0.0f < ld, ri = 0.0f < rd;
             const bool lint = (bn.lm & kInner) != 0, rint = (bn.rm & kInner) != 0;
-            // A child matters only while it holds — a leaf child in its entries, an internal child
-            // anywhere below it (bfsub) — a hit entry the ray has not tested yet: the rest are
-            // misses or mailbox repeats, which cannot change best.  So its box test (the
-            // reference's li / ri) is needed only then, and skipped when no lane of the wave needs
-            // it; an unneeded child is taken as not hit.  That changes nothing: a skipped leaf or
-            // subtree adds to tested no bit a later rh reads, the tie-break scan (mb_first_node)
-            // only looks for the pair's untested hit entries, none of which sit in it, and the
-            // pruning of the other nodes reads only best_t (tests/test_replay_skip.py checks it on
-            // a host model of this loop).
-            const uint64_t lset = lint ? sc.bfsub[bn.lm & 63u] : bn.lm, rset = rint ? sc.bfsub[bn.rm & 63u] : bn.rm;
-            const bool lneed = (lset & hits & ~tested) != 0;
-            const bool rneed = (rset & hits & ~tested) != 0;
-            float ld = -1.0f, rd = -1.0f;
-            if (wave_any(lneed)) ld = ray_box(r, bn.lmin[0], bn.lmin[1], bn.lmin[2], bn.lmax[0], bn.lmax[1], bn.lmax[2]);
-            if (wave_any(rneed)) rd = ray_box(r, bn.rmin[0], bn.rmin[1], bn.rmin[2], bn.rmax[0], bn.rmax[1], bn.rmax[2]);
-            const bool li = lneed & (0.0f < ld), ri = rneed & (0.0f < rd);
             const uint64_t m = ((li & !lint) ? bn.lm : 0ull) | ((ri & !rint) ? bn.rm : 0ull);
             uint64_t rh = m & ~tested & hits;
             tested |= m;

@@ -117,8 +117,6 @@ def load_library():
     L.pt_profile_enable.argtypes = [p, i]
     L.pt_profile_select.argtypes = [p, ctypes.c_char_p]
     L.pt_selftest_rcp.argtypes = [i, i, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32)]
-    L.pt_selftest_div.argtypes = [i, i, u32, u32, u32, u32, u32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(u32),
-                                  ctypes.POINTER(u32)]
     L.pt_bvh_build.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_bvh_build_sah.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_bvh_build_sah2.argtypes = [p, sz, p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
@@ -138,7 +136,7 @@ def load_library():
     L.pt_scene_leaf_bvh.argtypes = [p, i, i32p, i32p, i32p]
     L.pt_selftest_leaf.argtypes = [p, i, i, u32, u32, p]
     for fn in ("pt_scene_leaf_bvh", "pt_selftest_leaf", "pt_selftest_valu", "pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_bvh_build_sah2", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_selftest_div", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
     _lib = L
@@ -397,19 +395,6 @@ def selftest_rcp(steps: int = -1, lo_bits: int = 0x00800000, hi_bits: int = 0x7E
     b = ctypes.c_uint32(0)
     _check(L.pt_selftest_rcp(device, steps, lo_bits, hi_bits, ctypes.byref(m), ctypes.byref(b)))
     return int(m.value), int(b.value)
-
-
-def selftest_div(mode: int = 0, b_first: int = 0, b_count: int = 1 << 23, a_first: int = 0, a_count: int = 1024,
-                 seed: int = 1, device: int = 0):
-    """pt_selftest_div: (mismatches, failing a bits, failing b bits) of the core's reciprocal-based
-    division (pt_math.h div_r) vs IEEE a / b.  mode 0: mantissa ranges of a, b in [1, 2); mode 1:
-    b_count x a_count random bit patterns."""
-    L = load_library()
-    m = ctypes.c_uint64(0)
-    fa, fb = ctypes.c_uint32(0), ctypes.c_uint32(0)
-    _check(L.pt_selftest_div(device, mode, b_first, b_count, a_first, a_count, seed, ctypes.byref(m), ctypes.byref(fa),
-                             ctypes.byref(fb)))
-    return int(m.value), int(fa.value), int(fb.value)
 
 
 def selftest_valu(iters: int = 20000, reps: int = 5, packed: int = 0, device: int = 0):

@@ -256,15 +256,6 @@ int pt_selftest_math(int device, int fn, const float* a, const float* b, float* 
 int pt_selftest_rcp(int device, int steps, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
                     uint32_t* failing_bits);
 
-/* Self-test of the core's division from the correctly rounded reciprocal (pt_math.h div_r: the
- * shared-denominator quotients of normalize, the NEE attenuation and the BSDF weight) against
- * IEEE a / b on the device.  mode 0: a and b in [1, 2), a's mantissa over [a_first, a_first +
- * a_count), b's over [b_first, b_first + b_count) (each < 2^23; all 2^46 pairs in slices = the
- * exhaustive check every in-range quotient scales to); mode 1: b_count x a_count random bit
- * patterns (seed), NaN results equal.  *mismatches; failing_a / failing_b: one failing pair. */
-int pt_selftest_div(int device, int mode, uint32_t b_first, uint32_t b_count, uint32_t a_first, uint32_t a_count,
-                    uint32_t seed, uint64_t* mismatches, uint32_t* failing_a, uint32_t* failing_b);
-
 /* VALU issue calibration: `reps` timed launches (after one untimed) of a kernel whose threads run 8
  * independent v_fma_f32 chains (packed 1: v_pk_fma_f32, two FMAs per lane each; 2: packed and plain
  * chains interleaved 1 : 2; 32 instructions

@@ -210,17 +210,6 @@ def test_rcp_rn_exhaustive():
     assert pt_amd.selftest_rcp(0)[0] > 0                                    # the check can fail
 
 
-def test_div_r_sampled():
-    """pt_math.h div_r (a / b from the correctly rounded reciprocal, Markstein's correction) equals
-    the IEEE division: every b mantissa in [1, 2) against a stride of a mantissas (2^23 x 8192
-    pairs; the full 2^46 sweep is scripts/check_div.py, profiles/r04_check_div.log), plus 2^28
-    random bit patterns of any exponent (zeros, subnormals, infinities and NaNs take the IEEE
-    branch)."""
-    for a_first in range(0, 1 << 23, 1 << 20):  # 8 slices of 1024 consecutive a mantissas
-        assert pt_amd.selftest_div(0, 0, 1 << 23, a_first + 12345, 1024)[0] == 0
-    assert pt_amd.selftest_div(1, 0, 1 << 20, 0, 256, seed=7)[0] == 0
-
-
 def test_hash_bitexact():
     n = np.concatenate([RNG.integers(0, 2**32, 20000, dtype=np.uint64), [0, 1, 2**31 - 1, 2**32 - 1]]).astype(np.uint32)
     x = n.view(np.float32)
