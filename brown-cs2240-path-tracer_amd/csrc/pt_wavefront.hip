@@ -689,11 +689,8 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     }
     uint32_t* out_count = &wb.rcnt[((it + 1) % 3) * kRegions + rg];
     const Tri* gtris = sc.tris;  // global records for phase 1
-    const uint32_t nb = nqb + nnew;
-    // a block none of whose waves has a batch (the launches of the last depths, whose queues fill
-    // a few regions) leaves before staging the scene: a launch's tail is then the blocks that work
-    if (!__syncthreads_or(g < nb)) return;  // block-uniform
     if (LDS) stage_scene_lds(sc, l.scene);
+    const uint32_t nb = nqb + nnew;
     const GenArgs ga{frame0, stride, fbase, R, tg, P, raw_salt};
     Counters c = {};
     for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves

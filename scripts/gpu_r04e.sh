@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 4: 16-bit stacks, second layout.  The paired layout (two levels per lane word) raised
+# k_wf_trace's occupancy 6 -> 8 waves/SIMD on Glossy but issued +12 % VALU (r04d PMC); ablib/s16s
+# keeps level k of lane i at u16 index k * lanes + i — the 32-bit stack's addressing at half the
+# bytes.  In process against the product build with stack16 off and on (paired).
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/profiles
+L=brown-cs2240-path-tracer_amd/lib/libpt_hip.so
+S=ablib/s16s/libpt_hip.so
+AB=gpurun_out/profiles/r04e_ab_stack16_layout.log
+: > $AB
+ab() {
+  for order in "$L@stack16=0 $L@stack16=1 $S@stack16=1" "$S@stack16=1 $L@stack16=1 $L@stack16=0"; do
+    echo "== $* order: $order" >> $AB
+    timeout -k 10 300 python3 scripts/ab_libs.py $order "$@" --rounds 5 --async-torch >> $AB 2>&1
+    rc=$?; echo "ab $* rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+}
+ab --scene CornellBox-Glossy --res 1024 --spp 32 --depth 16
+ab --scene MedievalBoat --res 960 --spp 8 --depth 16
+ab --scene synthetic-1000 --res 1024 --spp 16 --depth 8
+ab --scene synthetic-100000 --res 1024 --spp 8 --depth 8
+grep -v "^ *$" $AB | grep -v amdgpu.ids
