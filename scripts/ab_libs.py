@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--async-torch", action="store_true", help="pt_render_async on a torch stream (as bench.py)")
+    ap.add_argument("--counters", action="store_true",
+                    help="after the timed rounds, one counted render per variant; print its work counters")
     a = ap.parse_args()
     import torch  # one HIP runtime for the process (see pt_amd/_lib.py)
     torch.cuda.init()
@@ -121,6 +123,15 @@ def main():
         for r in runs:
             r["ref"] = r["dacc"].cpu().numpy()
     base = runs[0]["ref"]
+    if a.counters:  # pt_counters (include/pt_hip.h): six uint64
+        names = ("samples", "ext_queries", "shadow_queries", "nodes", "tri_tests", "box_tests")
+        for r in runs:
+            c = (ctypes.c_uint64 * 6)()
+            acc = np.zeros((a.res, a.res, 3), np.float32)
+            rc = with_env(r["L"], r["env"], lambda: r["L"].pt_render(r["h"], p(meta), 0, a.spp, 1, a.depth, a.mode,
+                                                             p(acc), ctypes.cast(c, ctypes.c_void_p)))
+            assert rc == 0
+            print(json.dumps({"lib": r["lib"], "counters": dict(zip(names, map(int, c)))}), flush=True)
     for r in runs:
         ms = float(np.median(r["ms"]))
         print(json.dumps({"lib": r["lib"], "ms_median": round(ms, 3), "msamples_s": round(a.res * a.res * a.spp / ms / 1e3, 1),

@@ -23,3 +23,13 @@ ab --scene MedievalBoat --res 960 --spp 8 --depth 16
 ab --scene synthetic-1000 --res 1024 --spp 16 --depth 8
 ab --scene synthetic-100000 --res 1024 --spp 8 --depth 8
 grep -v "^ *$" $AB | grep -v amdgpu.ids
+# verdict r03 item 3 step 3: lanes parked at the same big leaf per cooperative turn (the boat), from
+# the diagnostic build's counters minus the product's (scripts/build_park_diag.sh)
+P=gpurun_out/profiles/r04e_park_diag.log
+: > $P
+for sc in "--scene MedievalBoat --res 960 --spp 2 --depth 16" "--scene CornellBox-Glossy --res 1024 --spp 4 --depth 16"; do
+  echo "== $sc" >> $P
+  timeout -k 10 300 python3 scripts/ab_libs.py $L ablib/parkdiag/libpt_hip.so $sc --rounds 1 --counters >> $P 2>&1
+  rc=$?; echo "park diag rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+grep -v amdgpu.ids $P
