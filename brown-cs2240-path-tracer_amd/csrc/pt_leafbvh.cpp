@@ -211,7 +211,7 @@ void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<
 }  // namespace
 
 void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
-                    int32_t& root, int32_t& end) {
+                    int32_t& root, int32_t& end, std::vector<LNode>* tree_out) {
     std::vector<Item> it((size_t)n);
     for (int32_t k = 0; k < n; ++k) {
         const Tri& t = tris[rec0 + k];
@@ -261,6 +261,7 @@ void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>
     for (const LNode& nd : tree)
         if (nd.info >= 0) nodes.push_back(nd);
     end = (int32_t)nodes.size();
+    if (tree_out) *tree_out = tree;
 }
 
 }  // namespace pt
