@@ -72,7 +72,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"lds", OPT_BOOL, nullptr},          {"fastrcp", OPT_BOOL, nullptr},     {"dual", OPT_BOOL, nullptr},
     {"fuse", OPT_BOOL, nullptr},         {"fuse_gen", OPT_BOOL, nullptr},    {"bf", OPT_BOOL, nullptr},
     {"mailbox", OPT_BOOL, nullptr},      {"bf_stackless", OPT_BOOL, nullptr}, {"trace_sparse", OPT_INT, nullptr},
-    {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},   {"stack16", OPT_BOOL, nullptr},
+    {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
@@ -777,7 +777,6 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
     lo.region_perm = o.flag("region_perm", kRegionPermDefault);
     lo.trace_ring = (int)o.num("trace_ring", 0);
-    lo.stack16 = o.flag("stack16", 1);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);

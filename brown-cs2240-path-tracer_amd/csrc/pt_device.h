@@ -11,9 +11,9 @@ namespace pt {
 constexpr int kStackMax = 32;  // > max traversal stack of any accepted tree (host checks)
 
 // Per-lane traversal stacks in LDS, lane-minor (the 64 entries of a wave at one level are
-// contiguous, so a stack access is conflict-free).  LStack32: entry k of a lane at word
-// k * stride.  LStack16 (trees below 65,536 nodes: entries are node indices): two levels share the
-// lane's word — entry k in half k & 1 of word k / 2 — half the LDS of 32-bit entries.
+// contiguous, so a stack access is conflict-free): entry k of a lane at word k * stride.  (Round
+// 4 measured 16-bit entries, two layouts, in k_wf_trace: occupancy 6 -> 8 waves per SIMD on
+// Glossy and no faster anywhere but the 1k synthetic scene)
 struct LStack32 {
     int32_t* p;
     int stride;
@@ -22,15 +22,6 @@ struct LStack32 {
     }
     __device__ __forceinline__ void put(int k, int v) const { p[k * stride] = v; }
     __device__ __forceinline__ int get(int k) const { return p[k * stride]; }
-};
-struct LStack16 {
-    uint16_t* p;  // this lane's word of levels 0 and 1
-    int stride2;  // u16 between level pairs: 2 * stride
-    static __device__ __forceinline__ LStack16 make(char* base, int stride) {
-        return LStack16{reinterpret_cast<uint16_t*>(base) + 2 * threadIdx.x, 2 * stride};
-    }
-    __device__ __forceinline__ void put(int k, int v) const { p[(k >> 1) * stride2 + (k & 1)] = (uint16_t)v; }
-    __device__ __forceinline__ int get(int k) const { return p[(k >> 1) * stride2 + (k & 1)]; }
 };
 
 struct Ray {

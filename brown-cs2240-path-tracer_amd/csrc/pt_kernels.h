@@ -71,7 +71,6 @@ struct LaunchOpts {
     int trace_sparse = -1; // k_wf_trace: narrower windows when 32-entry ones keep < 1/n of the waves busy (n; 0 off): -1 default
     int region_perm = -1;  // k_wf_step_bf: camera batches dealt to regions by a permutation (WfBuffers::rq); -1 default
     int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
-    int stack16 = 1;       // k_wf_trace: 16-bit stack entries on trees below 65,536 nodes (0: 32-bit)
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
 };
 
@@ -137,7 +136,6 @@ struct WfStreams {
     int trace_sparse = 0;  // k_wf_trace windows below 32 entries for short queues (LaunchOpts::trace_sparse)
     int region_perm = 0;   // LaunchOpts::region_perm
     int trace_ring = 0;    // LaunchOpts::trace_ring
-    int stack16 = 1;       // LaunchOpts::stack16
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
 };

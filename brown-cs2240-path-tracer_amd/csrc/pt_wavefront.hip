@@ -174,16 +174,12 @@ __host__ __device__ constexpr uint32_t win_tab(uint32_t ring) { return 2 * ring 
 static_assert(win_tab(kHitRingMax) >= kHitRingMax / kWinRays + 2, "wtab must name every window the ring can hold");
 static_assert(win_tab(kHitRing) >= kHitRing / kWinRays + 2, "wtab must name every window the ring can hold");
 __host__ __device__ constexpr uint32_t stage_bytes(uint32_t ring) { return kWinRays * 32 + ring * 8 + win_tab(ring) * 4; }
-// the traversal flavours that have a 256-entry-ring and a 16-bit-stack instance (the defaults:
-// lean16 + fast rcp, with and without big-leaf turns); the others always use 128 and 32-bit entries
+// the traversal flavours that have a 256-entry-ring instance (the defaults: lean16 + fast rcp, with
+// and without big-leaf turns); the others always use 128
 constexpr bool has_big_ring(int trav) { return trav == 17 || trav == 177; }
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
-// LDS of k_wf_trace per block: the lanes' traversal stacks (max_stack entries of 4 B, or 2 B on
-// trees below 65,536 nodes: LStack16) and per wave stage_bytes(ring)
-template <bool S16>
-__host__ __device__ constexpr uint32_t stack_bytes_per_lane(uint32_t max_stack) {
-    return S16 ? 4u * ((max_stack + 1u) / 2u) : 4u * max_stack;
-}
+// LDS of k_wf_trace per block: the lanes' traversal stacks (max_stack entries of 4 B) and per wave
+// stage_bytes(ring)
 
 // Work split: the queue is cut into windows of 32 entries; wave w of N takes windows w, w+N,
 // w+2N, ... (interleaving, not contiguous chunks, because queue order is spatially coherent —
@@ -198,16 +194,13 @@ __host__ __device__ constexpr uint32_t stack_bytes_per_lane(uint32_t max_stack) 
 // busy (the last depths), windows of wr / 2 .. 1 entries spread the queue over more waves, so each
 // wave's traversal is the slowest of fewer rays.  A window still takes kWinRays sequence numbers
 // (ring and flush bookkeeping unchanged); only its queue span is wr.
-// S16: the per-lane stacks hold 16-bit node indices (LStack16; trees below 65,536 nodes), half the
-// LDS of 32-bit entries, so more blocks fit a CU.
-template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, bool S16 = false>
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing>
 __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
                                                           uint32_t watchdog, int sparse) {
     constexpr uint32_t nring = RING, kWinTab = win_tab(RING);
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    using Stack = typename std::conditional<S16, LStack16, LStack32>::type;
-    const Stack stack = Stack::make(smem, blockDim.x);
-    char* stage_base = smem + stack_bytes_per_lane<S16>((uint32_t)sc.max_stack) * blockDim.x;
+    const LStack32 stack = LStack32::make(smem, blockDim.x);
+    char* stage_base = smem + (uint32_t)sc.max_stack * 4u * blockDim.x;
     char* stage = stage_base + (threadIdx.x / 64u) * stage_bytes(nring);
     float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
     int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [RING]
@@ -846,32 +839,28 @@ __global__ __launch_bounds__(256) void k_wf_accum(const float* __restrict__ rad,
     } while (0)
 // TRAV >= 300: the brute-force + replay kernel (k_wf_trace_bf; + 10: fast reciprocal); >= 400: fused
 // with the shading (k_wf_step_bf)
-template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, bool S16 = false>
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing>
 constexpr const void* trace_kernel() {
     if constexpr (TRAV >= 400) return (const void*)k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>;
     else if constexpr (TRAV >= 300) return (const void*)k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
-    else return (const void*)k_wf_trace<LDS, TRAV, COUNT, RING, S16>;
+    else return (const void*)k_wf_trace<LDS, TRAV, COUNT, RING>;
 }
-// the k_wf_trace instances with a 256-entry ring or 16-bit stacks: the default flavours, uncounted
+// the k_wf_trace instances with a 256-entry ring: the default flavours, uncounted
 template <int TRAV, bool COUNT>
 constexpr bool has_variants() { return TRAV < 300 && has_big_ring(TRAV) && !COUNT; }
 template <bool LDS, int TRAV, bool COUNT>
-static const void* trace_instance(uint32_t ring, bool s16) {
+static const void* trace_instance(uint32_t ring) {
     if constexpr (has_variants<TRAV, COUNT>()) {
-        if (ring == kHitRingMax)
-            return s16 ? trace_kernel<LDS, TRAV, COUNT, kHitRingMax, true>() : trace_kernel<LDS, TRAV, COUNT, kHitRingMax, false>();
-        return s16 ? trace_kernel<LDS, TRAV, COUNT, kHitRing, true>() : trace_kernel<LDS, TRAV, COUNT, kHitRing, false>();
+        if (ring == kHitRingMax) return trace_kernel<LDS, TRAV, COUNT, kHitRingMax>();
     }
     (void)ring;
-    (void)s16;
     return trace_kernel<LDS, TRAV, COUNT>();
 }
 template <bool LDS, int TRAV, bool COUNT>
-static size_t trace_lds(const SceneView& sc, uint32_t ring = kHitRing, bool s16 = false) {
+static size_t trace_lds(const SceneView& sc, uint32_t ring = kHitRing) {
     const size_t span = LDS ? sc.span_bytes : 0;
     if (TRAV >= 300) return (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * ((size_t)kBfSlots * 64 * 4) + span;
-    const size_t per_lane = s16 ? stack_bytes_per_lane<true>((uint32_t)sc.max_stack) : stack_bytes_per_lane<false>((uint32_t)sc.max_stack);
-    return per_lane * kTraceBlock + (kTraceBlock / 64) * stage_bytes(ring) + span;
+    return (size_t)sc.max_stack * 4 * kTraceBlock + (kTraceBlock / 64) * stage_bytes(ring) + span;
 }
 // resident blocks of `kernel` per CU at `lds` bytes of dynamic LDS, times the CUs: the persistent
 // grid of the trace and step kernels (cached per kernel instance and LDS size)
@@ -938,22 +927,19 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     int np = ws.aux[0] != nullptr ? ws.nparts : 1;
     while (np > 1 && (nframes < (uint32_t)np || wb.capacity / np < npix)) np /= 2;
     const uint32_t F = np * std::max<uint32_t>(1, std::min<uint32_t>((nframes + np - 1) / np, (uint32_t)(wb.capacity / np / npix)));
-    // k_wf_trace's instance: 16-bit stack entries where the tree has fewer than 65,536 nodes (option
-    // stack16=0: 32-bit), and the 256-entry hit ring when its extra 8 KB per block cost no block per
+    // k_wf_trace's instance: the 256-entry hit ring when its extra 8 KB per block cost no block per
     // CU (option trace_ring: 128 / 256 forces one)
-    bool s16 = false;
     uint32_t nring = kHitRing;
     if constexpr (has_variants<TRAV, COUNT>()) {
-        s16 = ws.stack16 && sc.n_nodes <= 65535;
-        const size_t l1 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRing, s16), l2 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRingMax, s16);
+        const size_t l1 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRing), l2 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRingMax);
         const bool fits = l2 <= max_block_lds() &&
                           (ws.trace_ring == (int)kHitRingMax ||
-                           (ws.trace_ring <= 0 && occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRingMax, s16), l2) >=
-                                                      occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRing, s16), l1)));
+                           (ws.trace_ring <= 0 && occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRingMax), l2) >=
+                                                      occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRing), l1)));
         if (fits) nring = kHitRingMax;
     }
-    const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc, nring, s16);
-    int tblocks = occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(nring, s16), lds);
+    const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc, nring);
+    int tblocks = occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(nring), lds);
     if (ws.trace_blocks > 0) tblocks = std::min(tblocks, ws.trace_blocks);  // option wf_trace_blocks (tests)
     const int iters = 2 * (fp.max_depth + 1);
     // option trace_watchdog: tests of the failure report
@@ -1030,13 +1016,13 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
                           dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
             } else {
-#define PT_TRACE(RG, SB) PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, RG, SB>), dim3(tblocks), \
-                                   dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, watchdog, sparse)
+#define PT_TRACE(RG) PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, RG>), dim3(tblocks), \
+                               dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, watchdog, sparse)
                 if constexpr (has_variants<TRAV, COUNT>()) {
-                    if (nring == kHitRingMax) { if (s16) PT_TRACE(kHitRingMax, true); else PT_TRACE(kHitRingMax, false); }
-                    else { if (s16) PT_TRACE(kHitRing, true); else PT_TRACE(kHitRing, false); }
+                    if (nring == kHitRingMax) PT_TRACE(kHitRingMax);
+                    else PT_TRACE(kHitRing);
                 } else {
-                    PT_TRACE(kHitRing, false);
+                    PT_TRACE(kHitRing);
                 }
 #undef PT_TRACE
             }
@@ -1081,7 +1067,6 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.trace_sparse = std::max(0, lo.trace_sparse);
     ws.region_perm = lo.region_perm > 0 ? 1 : 0;
     ws.trace_ring = lo.trace_ring;
-    ws.stack16 = lo.stack16 != 0 ? 1 : 0;
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
     if (!accum) { nframes = 1; stride = 1; }

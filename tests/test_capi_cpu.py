@@ -96,10 +96,10 @@ def test_layout_options():
     pt_amd.reset_options()
     try:
         for name in ("packet", "persist", "regen", "regen_bf", "cull", "tiles", "scatter", "batch_pipe",
-                     "trace_dyn", "stagger", "pipe", "ifif"):
+                     "trace_dyn", "stagger", "pipe", "ifif", "stack16"):
             with pytest.raises(pt_amd.PtError):
                 pt_amd.set_option(name, "1")
-        for name in ("region_perm", "stack16"):
+        for name in ("region_perm",):
             pt_amd.set_option(name, 0)
             assert pt_amd.get_option(name) == "0"
             pt_amd.set_option(name, 1)

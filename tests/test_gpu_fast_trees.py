@@ -5,8 +5,7 @@
   MedievalBoat 1920x1080 (depth 16, 4 frames);
 * the Cornell-sized synthetic scenes of the BVH sweep (scripts/synth_scene.py, seed 1234,
   BASELINE.json north_star) on the reference's tree: 1,000 and 12,500 triangles (1024^2,
-  depth 8, 8 frames, three bands), 100,000 (one band, 8 frames; also with the traversal kernel's
-  32-bit stacks, option stack16=0) and 1,000,000 (one band, 2 frames: the reference builder's
+  depth 8, 8 frames, three bands), 100,000 (one band, 8 frames) and 1,000,000 (one band, 2 frames: the reference builder's
   depth cap of 16 keeps even this tree at <= 32,767 internal nodes), plus 12,500 on the SAH tree.
 The bands are rows that see light (the light at rows ~190-210; the random triangles shade the
 rest of the box more and more as N grows).
@@ -16,7 +15,7 @@ batches (identical bits), and 16-row bands of it are compared with the C oracle
 (oracle/pt_oracle.c: the literal restatement of src/wgsl-util/intersection-logic.wgsl:1-215)
 rendering the same rows of the same packed buffers.  These trees run k_wf_trace's code paths that
 the reference scenes do not reach: deep stacks, leaf sizes of the SAH builder (<= 8), the
-synthetic reference trees' many mid-size leaves (1M: ~30+ entries per leaf), and both stack widths.
+synthetic reference trees' many mid-size leaves (1M: ~30+ entries per leaf).
 """
 import os
 import sys
@@ -87,15 +86,9 @@ def test_synthetic_12500_sah_rows_bitexact(synth_packed):
     _trace_kernel_ran(profs)
 
 
-def test_synthetic_100k_band_bitexact(synth_packed, ptopts):
-    p = synth_packed(100000)
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        assert s.info["nodes"] <= 65535  # 16-bit traversal stacks by default
-    img, profs = _render_bands(p, 1024, 1024, 8, 8, [(192, 208)])
+def test_synthetic_100k_band_bitexact(synth_packed):
+    _, profs = _render_bands(synth_packed(100000), 1024, 1024, 8, 8, [(192, 208)])
     _trace_kernel_ran(profs)
-    ptopts.set("stack16", "0")  # the same render with 32-bit stack entries: the same bits
-    img32, _ = _render_bands(p, 1024, 1024, 8, 8, [(192, 208)])
-    assert_same_bits(img32, img, "stack16=0 vs default")
 
 
 def test_synthetic_1m_band_bitexact(synth_packed):

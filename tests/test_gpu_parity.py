@@ -101,22 +101,16 @@ KERNELS = {
     "wavefront_sort512_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "512", "PT_MAILBOX": "0"},
     "wavefront_sort64_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_SORT": "64", "PT_MAILBOX": "0",
                                           "PT_WF_TRACE_BLOCKS": "1"},
-    # the traversal kernel's per-lane stacks with 32-bit entries (option stack16=0; the default packs
-    # two 16-bit levels per word on trees below 65,536 nodes), on the full grid and on one block
-    # with the 256-entry ring; and 16-bit stacks with the big-leaf turns forced onto small leaves
-    "wavefront_stack32_nomailbox": {"PT_KERNEL": "wavefront", "PT_STACK16": "0", "PT_MAILBOX": "0"},
-    "wavefront_stack32_ring256_1block": {"PT_KERNEL": "wavefront", "PT_STACK16": "0", "PT_MAILBOX": "0",
-                                         "PT_TRACE_RING": "256", "PT_WF_TRACE_BLOCKS": "1"},
-    "wavefront_stack16_big4_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_MAILBOX": "0",
-                                      "PT_WF_TRACE_BLOCKS": "1"},
+    # the traversal kernel on one block with the big-leaf turns forced onto small leaves
+    "wavefront_big4_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_MAILBOX": "0",
+                              "PT_WF_TRACE_BLOCKS": "1"},
 }
 
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
-            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING",
-            "PT_STACK16")
+            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING")
 
 
 @pytest.fixture(params=list(KERNELS))
