@@ -462,10 +462,57 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
     }
 }
 
+// Cross-lane minima by DPP (gfx9 lane moves inside the VALU: no LDS round trip, unlike the
+// ds_bpermute a __shfl_xor becomes).  dpp_mov: lanes the move does not write keep `old`.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int dpp_mov(int v, int old) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, 0xF, false);
+}
+// the wave's smallest (t, k), lexicographic, returned in every lane (t never NaN; `none` is
+// (+inf, 0x7fffffff)): quad_perm [1,0,3,2] and [2,3,0,1], the 8-lane and 16-lane mirrors leave each
+// row's minimum in all its lanes; row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry it
+// to lane 63, which is read back.  A minimum under a total order: any pairing gives the same.
+__device__ __forceinline__ void wave_min_tk(float& t, int& k) {
+    constexpr int kInfBits = 0x7f800000, kNone = 0x7fffffff;
+    auto step = [&](auto mov) {
+        const float ot = __builtin_bit_cast(float, mov(__builtin_bit_cast(int, t), kInfBits));
+        const int ok = mov(k, kNone);
+        const bool b = (ot < t) | ((ot == t) & (ok < k));
+        t = b ? ot : t;
+        k = b ? ok : k;
+    };
+    step([](int v, int o) { return dpp_mov<0xB1, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x4E, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x141, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x140, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x142, 0xA>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x143, 0xC>(v, o); });
+    t = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
+    k = __builtin_amdgcn_readlane(k, 63);
+}
+// the wave's smallest t (never NaN; +inf for none), in every lane, the same way
+__device__ __forceinline__ float wave_min_t(float t) {
+    constexpr int kInfBits = 0x7f800000;
+    auto step = [&](auto mov) {
+        const float ot = __builtin_bit_cast(float, mov(__builtin_bit_cast(int, t), kInfBits));
+        t = ot < t ? ot : t;
+    };
+    step([](int v, int o) { return dpp_mov<0xB1, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x4E, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x141, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x140, 0xF>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x142, 0xA>(v, o); });
+    step([](int v, int o) { return dpp_mov<0x143, 0xC>(v, o); });
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
+}
+
 // Leaf chunks (SceneView::lnodes; pt_leafbvh.cpp groups a big leaf's entries into chunks of at
 // most 8, pt_layout.h LNode states the skip rule).  chunk_skip: no entry of the chunk (its LNode as
-// a, b, c, e) can report a
-// hit at t <= bound for ray r (idl = 1 / |d|, on = |o|).
+// a, b, c, e) can report a hit at t <= bound for ray r (idl = 1 / |d|, on = |o|).  Branch-free: the
+// rule's two escapes (a cone admitting no bound, an unbounded delta) are masks, not early returns,
+// so every operand of the check is used unconditionally and the node's four loads issue together
+// (with the returns the compiler sank the last load into the branch: two memory round trips per
+// check); a lane whose escape holds computes the box on meaningless values and is not skipped.
 __device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const float4 c, const float4 e, const Ray& r,
                                            float idl, float on, float bound) {
     // |cos(d, n)| >= cos(angle(d, axis) + half-angle) over the chunk's normals, less a slack for
@@ -473,10 +520,9 @@ __device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const
     const float cb = fabsf(r.d.x * a.w + r.d.y * b.w + r.d.z * c.x) * idl;
     const float sb = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cb * cb));
     const float cf = cb * c.y - sb * c.z - 1e-5f;
-    if (!(cf > 1e-4f)) return false;
     // delta, rounded up by 1e-5 relative against the approximate reciprocal
     const float dl = (e.x + c.w * on) * __builtin_amdgcn_rcpf(cf) * 1.00001f + 1e-5f * on + e.y;
-    if (!(dl < 1e30f)) return false;
+    const bool bounded = (cf > 1e-4f) & (dl < 1e30f);
     float tn = -3.0e38f, tf = 3.0e38f;
     float t1 = (a.x - dl - r.o.x) * r.inv.x, t2 = (b.x + dl - r.o.x) * r.inv.x;
     tn = fmaxf(tn, fminf(t1, t2));
@@ -487,7 +533,7 @@ __device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const
     t1 = (a.z - dl - r.o.z) * r.inv.z; t2 = (b.z + dl - r.o.z) * r.inv.z;
     tn = fmaxf(tn, fminf(t1, t2));
     tf = fminf(tf, fmaxf(t1, t2));
-    return (tf < tn) | (tf < 0.0f) | (tn > bound);
+    return bounded & ((tf < tn) | (tf < 0.0f) | (tn > bound));
 }
 
 // The leaf whose records start at rec0, for ONE ray q (wave-uniform: every lane holds it), by
@@ -528,37 +574,39 @@ __device__ __forceinline__ void chunk_leaf(const SceneView& sc, const Ray& q, in
                 if (hit & ((t < bt) | ((t == bt) & (k < bk)))) { bt = t; bk = k; }
             }
         }
-        float w = bt;  // the next checks against the best so far (a lane without a hit holds +inf)
-        for (int off = 1; off < 64; off <<= 1) w = fminf(w, __shfl_xor(w, off, 64));
-        bound = fminf(prior, w);
+        bound = fminf(prior, wave_min_t(bt));
         filled = 0;
     };
     const int cl = max(c0, c1 - 1);  // a valid chunk for lanes past the end (their check is off)
+    // a block's gathered chunks arrive from ds_permute into lanes [plo, phi); they are merged into
+    // `mine` only when the next block has opened chunks (or before a test), so the permute's LDS
+    // latency hides behind the next block's loads and checks
+    int pgot = 0, plo = 0, phi = 0;
+    auto merge = [&]() {
+        mine = (lane >= plo && lane < phi) ? pgot : mine;
+        phi = plo;
+    };
     for (int cb = c0; cb < c1; cb += 64) {
         const int c = cb + lane, cn = min(c, cl);
         const float4 a = nodes[4 * cn], b = nodes[4 * cn + 1], cc = nodes[4 * cn + 2], e = nodes[4 * cn + 3];
         const int info = __builtin_bit_cast(int, e.w);
-        const bool open = c < c1 && !chunk_skip(a, b, cc, e, q, idl, on, bound);
+        const bool open = (c < c1) & !chunk_skip(a, b, cc, e, q, idl, on, bound);
         const uint64_t m = __ballot(open);
         const int cnt = (int)__popcll(m);
         if (STATS) *chunks += cnt;
         if (!cnt) continue;
+        merge();
         if (filled + cnt > 64) test_gathered();
         const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const int dest = open ? filled + below : (filled + cnt + (lane - below)) & 63;
-        const int got = __builtin_amdgcn_ds_permute(dest << 2, info);
-        mine = (lane >= filled && lane < filled + cnt) ? got : mine;
+        pgot = __builtin_amdgcn_ds_permute(dest << 2, info);
+        plo = filled;
+        phi = filled + cnt;
         filled += cnt;
     }
+    merge();
     if (filled) test_gathered();
-    // every lane ends with the wave's smallest (t, position)
-    for (int off = 1; off < 64; off <<= 1) {
-        const float ot = __shfl_xor(bt, off, 64);
-        const int ok = __shfl_xor(bk, off, 64);
-        const bool b = (ok != 0x7fffffff) & ((bk == 0x7fffffff) | (ot < bt) | ((ot == bt) & (ok < bk)));
-        bt = b ? ot : bt;
-        bk = b ? ok : bk;
-    }
+    wave_min_tk(bt, bk);  // every lane ends with the wave's smallest (t, position)
     bt_out = bt;
     bk_out = bk;
 }
