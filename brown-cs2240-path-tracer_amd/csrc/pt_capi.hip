@@ -1166,7 +1166,7 @@ int pt_scene_leaf_bvh(const pt_scene* s, int leaf, int32_t* first_record, int32_
 int pt_selftest_leaf(pt_scene* s, int leaf, int mode, uint32_t seed, uint32_t nrays, int32_t* out) {
     if (!s || !out) return fail(PT_ERR_INVALID, "null argument");
     if (leaf < 0 || (size_t)leaf >= s->lleaves.size()) return fail(PT_ERR_INVALID, "no such leaf BVH");
-    if (mode < 0 || mode > 3 || nrays == 0 || nrays > (1u << 24)) return fail(PT_ERR_INVALID, "bad mode or ray count");
+    if (mode < 0 || mode > 7 || nrays == 0 || nrays > (1u << 24)) return fail(PT_ERR_INVALID, "bad mode or ray count");
     HIP_TRY(hipSetDevice(s->device));
     const auto& l = s->lleaves[(size_t)leaf];
     int32_t* d = nullptr;

@@ -646,6 +646,143 @@ __device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, Tr
     }
 }
 
+// Several rays at one big leaf (the wavefront kernel's chunk walk; verdict r03 item 3 step 3):
+// when a turn starts, ~11 lanes of a wave on average are parked at the SAME big leaf of the boat
+// (profiles/r04e_park_diag.log) and chunk_turn served them one walk each.  Here up to kMultiRays
+// of them (the first parked lane f and the lanes parked at f's leaf) share ONE walk: each block of
+// 64 chunks is loaded once and checked against every ray (its o, d, 1/d, |d|, |o| and bound read
+// from the owner lane), the open (chunk, ray) pairs are gathered one per lane in ray order, and a
+// test pass tests each lane's chunk against its pair's ray (fetched from the owner lane by
+// ds_bpermute).  A ray's best (t, position) is kept as one 64-bit key — the f32 bits of t (t > 0,
+// so they order as t) above the position — in its LDS slot, lowered with ds_min_u64; its bound
+// after each pass is min(prior, that t).  Per ray this is chunk_leaf's argument unchanged: every
+// entry able to report a hit at t <= the ray's bound at check time is tested, the bound never
+// drops below the leaf's final answer, so each ray ends with the smallest (t, position) over its
+// leaf's hitting entries whenever that beats its prior; and each served lane then takes the leaf
+// exactly as chunk_turn does.
+constexpr int kMultiRays = 16;
+// The walk for the lanes of `same` (wave-uniform, at most kMultiRays lanes; every lane of the wave
+// runs), each with its own ray r and closest t so far `prior` (+inf for none), over the leaf whose
+// records start at rec0; keys: kMultiRays LDS slots of this wave.  Each lane of `same` ends with
+// its (bt, bk): the smallest (t, position) over the leaf's entries able to beat prior (bk =
+// 0x7fffffff: none) — what chunk_leaf gives that ray.
+template <bool FAST_RCP>
+__device__ __forceinline__ void chunk_leaf_multi(const SceneView& sc, const Ray& r, uint64_t same, int rec0, float prior,
+                                                 uint64_t* keys, float& bt_out, int& bk_out) {
+    constexpr uint64_t kNoKey = ~0ull;
+    const int lane = (int)(threadIdx.x & 63u);
+    const bool served = ((same >> lane) & 1ull) != 0;
+    const int slot = (int)__popcll(same & ((1ull << lane) - 1ull));  // this lane's slot, when served
+    if (served) keys[slot] = kNoKey;
+    // this lane's ray constants, read by the checks from the owner lane
+    const float idl = 1.0f / sqrtf(dot(r.d, r.d));
+    const float on = sqrtf(dot(r.o, r.o));
+    float bnd = prior;  // this lane's ray's bound
+    auto rl = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
+    auto bp = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(l << 2, __builtin_bit_cast(int, v))); };
+    const int c0 = sc.tris[rec0].lbvh - 1, c1 = sc.tris[rec0 + 1].lbvh;
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(sc.lnodes);
+    int mine = 0;    // the gathered pair of this lane: its chunk (first slot | count << 24) ...
+    int mray = 0;    // ... and the lane that owns its ray
+    int filled = 0;  // lanes holding a gathered pair (wave-uniform)
+    auto test_pairs = [&]() {
+        const int first = mine & 0xffffff, cnt_l = lane < filled ? (mine >> 24) : 0;
+        Ray q;  // the pair's ray, from its owner lane
+        q.o = mk(bp(r.o.x, mray), bp(r.o.y, mray), bp(r.o.z, mray));
+        q.d = mk(bp(r.d.x, mray), bp(r.d.y, mray), bp(r.d.z, mray));
+        q.inv = mk(bp(r.inv.x, mray), bp(r.inv.y, mray), bp(r.inv.z, mray));
+        float bt = __builtin_inff();
+        int bk = 0x7fffffff;
+#pragma unroll 2
+        for (int e = 0; e < 8; ++e) {
+            if (e < cnt_l) {
+                const Tri* rec = sc.ltris + first + e;
+                const int k = rec->lbvh;
+                float t;
+                const bool hit = tri_hit<FAST_RCP>(load_tri(rec, 0), q, t);
+                if (hit & ((t < bt) | ((t == bt) & (k < bk)))) { bt = t; bk = k; }
+            }
+        }
+        if (bk != 0x7fffffff) {  // t > 1e-8: its f32 bits order as t does
+            const int os = (int)__popcll(same & ((1ull << mray) - 1ull));
+            atomicMin(reinterpret_cast<unsigned long long*>(keys + os),
+                      ((unsigned long long)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk);
+        }
+        filled = 0;
+        if (served) {  // the next checks against each ray's best so far
+            const uint64_t k = keys[slot];
+            if (k != kNoKey) bnd = fminf(prior, __builtin_bit_cast(float, (uint32_t)(k >> 32)));
+        }
+    };
+    const int cl = max(c0, c1 - 1);  // a valid chunk for lanes past the end (their check is off)
+    int pgot = 0, pray = 0, plo = 0, phi = 0;  // a gathered run, merged later (chunk_leaf)
+    auto merge = [&]() {
+        const bool in = lane >= plo && lane < phi;
+        mine = in ? pgot : mine;
+        mray = in ? pray : mray;
+        phi = plo;
+    };
+    for (int cb = c0; cb < c1; cb += 64) {
+        const int c = cb + lane, cn = min(c, cl);
+        const float4 a = nodes[4 * cn], b = nodes[4 * cn + 1], cc = nodes[4 * cn + 2], e = nodes[4 * cn + 3];
+        const int info = __builtin_bit_cast(int, e.w);
+        for (uint64_t m = same; m; m &= m - 1) {  // wave-uniform: every ray of the walk
+            const int o = (int)__builtin_ctzll(m);
+            Ray qr;
+            qr.o = mk(rl(r.o.x, o), rl(r.o.y, o), rl(r.o.z, o));
+            qr.d = mk(rl(r.d.x, o), rl(r.d.y, o), rl(r.d.z, o));
+            qr.inv = mk(rl(r.inv.x, o), rl(r.inv.y, o), rl(r.inv.z, o));
+            const bool open = (c < c1) & !chunk_skip(a, b, cc, e, qr, rl(idl, o), rl(on, o), rl(bnd, o));
+            const uint64_t mo = __ballot(open);
+            const int cnt_o = (int)__popcll(mo);
+            if (!cnt_o) continue;
+            merge();
+            if (filled + cnt_o > 64) test_pairs();
+            const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mo, 0u));
+            const int dest = open ? filled + below : (filled + cnt_o + (lane - below)) & 63;
+            pgot = __builtin_amdgcn_ds_permute(dest << 2, info);
+            pray = o;
+            plo = filled;
+            phi = filled + cnt_o;
+            filled += cnt_o;
+        }
+    }
+    merge();
+    if (filled) test_pairs();
+    const uint64_t k = served ? keys[slot] : kNoKey;
+    bt_out = __builtin_bit_cast(float, (uint32_t)(k >> 32));
+    bk_out = k == kNoKey ? 0x7fffffff : (int)(uint32_t)k;
+}
+template <bool COUNT, bool FAST_RCP, class ST>
+__device__ __forceinline__ void chunk_turn_multi(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked,
+                                                 const ST& stack, Counters& cnt) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const int f = (int)__builtin_ctzll(parked);
+    int my0 = 0, myn = 0;
+    big_seg(s, my0, myn);
+    const int rec0 = __builtin_amdgcn_readlane(my0, f), n = __builtin_amdgcn_readlane(myn, f);
+    // the rays of this walk: parked lanes at f's leaf, the first kMultiRays of them (f included)
+    uint64_t same = __ballot((((parked >> lane) & 1ull) != 0) && my0 == rec0);
+    while (__popcll(same) > kMultiRays) same &= ~(1ull << (63 - __builtin_clzll(same)));
+    float bt;
+    int bk;
+    chunk_leaf_multi<FAST_RCP>(sc, r, same, rec0, s.best_t < 0.0f ? __builtin_inff() : s.best_t, sc.lkeys, bt, bk);
+    if ((same >> lane) & 1ull) {
+        const bool take = (bk != 0x7fffffff) & ((s.best_t < 0.0f) | (bt < s.best_t));
+        s.best_t = take ? bt : s.best_t;
+        s.best = take ? rec0 + bk : s.best;
+        if (COUNT) cnt.tri_tests += n;
+        s.k += n;
+        s.fl &= ~TF_PARK;
+        if (s.k == s.nt) {
+            s.fl &= ~TF_LEAF;
+            lean_decide(s, stack);
+        } else if (big_at(sc, s)) {
+            s.fl |= TF_PARK;  // its right leaf is big too
+        }
+    }
+}
+
 // Each iteration runs ONE unit type for the whole wave — a leaf turn (up to K triangle tests)
 // when leaf lanes >= node_bias * node lanes, else a node turn — keeping each lane's unit order.
 template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, class ST>
@@ -658,9 +795,10 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
             int my0 = 0, myn = 0;  // the first parked lane's leaf (the other lanes' fields may not be a leaf's)
             big_seg(s, my0, myn);
             if (CHUNKS && sc.lnodes && __ballot(1) == ~0ull &&
-                sc.tris[__builtin_amdgcn_readlane(my0, (int)__builtin_ctzll(parked))].lbvh > 0)
-                chunk_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);  // its leaf has chunks
-            else
+                sc.tris[__builtin_amdgcn_readlane(my0, (int)__builtin_ctzll(parked))].lbvh > 0) {  // its leaf has chunks
+                if (sc.lkeys) chunk_turn_multi<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
+                else chunk_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
+            } else
                 big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
             return true;
         }

@@ -286,13 +286,16 @@ hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, h
 // from 10^-3 .. 20 units away; 2 grazing: along the entry's plane, tilted by 10^-7 .. 10^-1 rad,
 // so the test's rounding is at its largest; 3 leaving a surface as the path tracer's bounces do
 // (the point offset by 1e-4 along the normal, directions uniform).  Row i of out: the loop's
-// result (position taken or -1, t bits), chunk_leaf's, its entry tests and open chunks.
+// result (position taken or -1, t bits), chunk_leaf's, its entry tests and open chunks.  mode + 4:
+// chunk_leaf_multi instead (the walk several rays share; tests and chunks not counted).
 __device__ __forceinline__ uint32_t st_hash(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
     return x;
 }
-__global__ __launch_bounds__(256) void k_selftest_leaf(SceneView sc, int rec0, int n, int mode, uint32_t seed,
+__global__ __launch_bounds__(256) void k_selftest_leaf(SceneView sc, int rec0, int n, int mode_in, uint32_t seed,
                                                        uint32_t nrays, int32_t* __restrict__ out) {
+    const int mode = mode_in & 3;
+    const bool multi = (mode_in & 4) != 0;
     // every lane runs (chunk_leaf needs the whole wave); lanes past nrays store nothing
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t st = st_hash(seed * 0x9e3779b9u + i * 0x85ebca6bu + (uint32_t)mode);
@@ -342,7 +345,16 @@ __global__ __launch_bounds__(256) void k_selftest_leaf(SceneView sc, int rec0, i
     float wt = 0.0f;
     int wk = 0x7fffffff, tests = 0, chunks = 0;
     const int lane = (int)(threadIdx.x & 63u);
-    for (int f = 0; f < 64; ++f) {
+    if (multi) {  // chunk_leaf_multi: four walks of 16 interleaved lanes each (lanes g, g + 4, ...)
+        __shared__ uint64_t keys[4][kMultiRays];
+        for (int g = 0; g < 4; ++g) {
+            float bt;
+            int bk;
+            chunk_leaf_multi<false>(sc, r, 0x1111111111111111ull << g, rec0, pb, keys[threadIdx.x / 64u], bt, bk);
+            if ((lane & 3) == g) { wt = bt; wk = bk; }
+        }
+    }
+    for (int f = 0; f < (multi ? 0 : 64); ++f) {
         auto bc = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), f)); };
         Ray q;
         q.o = mk(bc(r.o.x), bc(r.o.y), bc(r.o.z));

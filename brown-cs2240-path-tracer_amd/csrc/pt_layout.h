@@ -143,6 +143,9 @@ struct SceneView {
     // in its leaf (ltris: one load per test, no index indirection)
     const LNode* lnodes;
     const Tri* ltris;
+    // the traversal kernel's per-wave LDS slots for chunk_turn_multi (kMultiRays keys; set by
+    // k_wf_trace for its big-leaf instances, nullptr elsewhere)
+    uint64_t* lkeys;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

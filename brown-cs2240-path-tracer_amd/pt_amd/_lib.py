@@ -275,7 +275,7 @@ class Scene:
 
     def selftest_leaf(self, leaf: int, mode: int, seed: int, nrays: int) -> np.ndarray:
         """pt_selftest_leaf: [nrays, 6] int32 — the sequential loop's (position or -1, t bits), the
-        walk's, the walk's entry tests and nodes."""
+        walk's, the walk's entry tests and nodes (mode + 4: the shared multi-ray walk, no counts)."""
         out = np.zeros((nrays, 6), np.int32)
         _check(self._lib.pt_selftest_leaf(self._h, leaf, mode, seed, nrays, _ptr(out)))
         return out

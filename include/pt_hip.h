@@ -275,7 +275,8 @@ int pt_scene_leaf_bvh(const pt_scene* scene, int leaf, int32_t* first_record, in
  * against chunked leaf `leaf` by the reference's sequential loop over all entries and by the
  * chunk scheme the traversal uses, with the same closest-t-so-far.  out (host, nrays x 6): loop
  * (position taken or -1, t bits), chunks (position or -1, t bits), entries tested and chunks
- * opened.  Blocking. */
+ * opened.  mode + 4: the same families through the walk that several rays parked at one leaf share
+ * (chunk_leaf_multi), out columns 4-5 zero.  Blocking. */
 int pt_selftest_leaf(pt_scene* scene, int leaf, int mode, uint32_t seed, uint32_t nrays, int32_t* out);
 
 #ifdef __cplusplus

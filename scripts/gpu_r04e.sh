@@ -33,3 +33,7 @@ for sc in "--scene MedievalBoat --res 960 --spp 2 --depth 16" "--scene CornellBo
   rc=$?; echo "park diag rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 grep -v amdgpu.ids $P
+# cooperative turns for Glossy's medium leaves (largest 61 entries: never cooperative at the
+# default threshold 128)
+timeout -k 10 300 python3 scripts/env_ab.py --scene CornellBox-Glossy --spp 16 --depth 16 --reps 3 big_leaf=128 big_leaf=48 big_leaf=32 big_leaf=20 > gpurun_out/profiles/r04e_ab_glossy_bigleaf.jsonl 2>gpurun_out/ab.err
+rc=$?; echo "glossy big_leaf rc=$rc"; cat gpurun_out/profiles/r04e_ab_glossy_bigleaf.jsonl; [ $rc -eq 0 ] || exit $rc

@@ -1,7 +1,9 @@
 """Leaf chunks (csrc/pt_leafbvh.cpp, pt_device.h chunk_leaf): a big leaf's entries tested chunk by
 chunk, skipping chunks that provably hold no hit below the bound, must end exactly where the
 reference's sequential strict-< loop over all the leaf's entries ends — same entry, same t bits —
-for every ray and closest-t-so-far.  pt_selftest_leaf runs both on the device for four ray
+for every ray and closest-t-so-far — walked for one ray at a time (chunk_leaf) and by the walk that
+the rays parked at one leaf share (chunk_leaf_multi, 16 interleaved lanes per walk).
+pt_selftest_leaf runs them on the device for four ray
 families, including rays grazing the entries' planes (where the triangle test's rounding, which
 the skip rule bounds, is largest) and rays leaving the surfaces as the path tracer's bounces do.  Renders through the walk are checked against the oracle by
 test_gpu_parity.py (the leaf variants, the boat frames) and test_gpu_config_bands.py (the boat
@@ -21,13 +23,14 @@ def _check(s, label, nrays=NRAYS):
     assert leaves, f"{label}: no leaf BVH"
     stats = []
     for li, (rec0, n, nodes) in enumerate(leaves):
-        for mode in range(4):
+        for mode in range(8):  # + 4: the walk several parked rays share (chunk_leaf_multi)
             out = s.selftest_leaf(li, mode, 1234 + 17 * li, nrays)
             bad = np.flatnonzero(np.any(out[:, :2] != out[:, 2:4], axis=1))
             assert bad.size == 0, (f"{label} leaf {li} ({n} entries) mode {mode}: {bad.size} rays differ, first "
                                    f"{out[bad[:4]].tolist()}")
-            hits = int((out[:, 0] >= 0).sum())
-            stats.append((li, n, nodes, mode, hits, float(out[:, 4].mean()), float(out[:, 5].mean())))
+            if mode < 4:
+                hits = int((out[:, 0] >= 0).sum())
+                stats.append((li, n, nodes, mode, hits, float(out[:, 4].mean()), float(out[:, 5].mean())))
     for li, n, nchunks, mode, hits, tests, opened in stats if len(stats) <= 64 else []:
         steps = -(-nchunks // 64) + 8 * -(-opened // 64)
         print(f"{label} leaf {li}: {n} entries {nchunks} chunks mode {mode}: {hits}/{nrays} taken, "
