@@ -920,7 +920,7 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         const long big = o.num("big_leaf", kBigLeafDefault);
         view.big_leaf = (big > 0 && s->info.max_leaf >= (uint32_t)big) ? (int32_t)big : 0;
         // leaf BVHs (built at pt_scene_create, option leaf_bvh): lanes park at every leaf that has
-        // chunks and test them chunk by chunk (chunk_turn); option leaf_walk=0 keeps them out (A/B)
+        // chunks and test them chunk by chunk (chunk_turn_multi); option leaf_walk=0 keeps them out (A/B)
         if (big > 0 && s->leaf_min > 0 && o.flag("leaf_walk", 1) != 0)
             view.big_leaf = view.big_leaf > 0 ? std::min<int32_t>(view.big_leaf, s->leaf_min) : s->leaf_min;
         else

@@ -545,7 +545,9 @@ __device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const
 // so the loads of a lane's tests are independent of each other and of the tests.  Every entry
 // that could report a hit at t <= the bound is tested, so the wave's smallest (t, position) —
 // returned in every lane — is the sequential strict-< loop's outcome whenever the loop would take
-// one (t < prior).  tests / chunks: work counters (selftest only).
+// one (t < prior).  tests / chunks: work counters (selftest only).  The traversal walks with
+// chunk_leaf_multi (below: the same argument for several rays at once); this single-ray walk is
+// its reference in pt_selftest_leaf, which checks both against the sequential loop.
 template <bool FAST_RCP, bool STATS = false>
 __device__ __forceinline__ void chunk_leaf(const SceneView& sc, const Ray& q, int rec0, float prior, float& bt_out,
                                            int& bk_out, int* tests = nullptr, int* chunks = nullptr) {
@@ -561,8 +563,9 @@ __device__ __forceinline__ void chunk_leaf(const SceneView& sc, const Ray& q, in
     int filled = 0;  // lanes holding a gathered chunk (wave-uniform)
     auto test_gathered = [&]() {
         const int first = mine & 0xffffff, cnt = lane < filled ? (mine >> 24) : 0;
-        // two records in flight at a time: all eight would hold 96 VGPRs and cost the trace
-        // kernel its occupancy (62 -> 94 VGPRs measured)
+        // the records' loads stay inside the per-entry branch: loading two entries together (or
+        // the next while this one is tested) costs the trace kernel 14 VGPRs and a wave per SIMD,
+        // measured slower on the boat (profiles/r04g_ab_chunkwalk.log, r04h_ab_chunkwalk.log)
 #pragma unroll 2
         for (int e = 0; e < 8; ++e) {
             if (e < cnt) {
@@ -610,45 +613,10 @@ __device__ __forceinline__ void chunk_leaf(const SceneView& sc, const Ray& q, in
     bt_out = bt;
     bk_out = bk;
 }
-// The first parked lane f whose big leaf has chunks: chunk_leaf for f's ray, then big_turn's
-// bookkeeping (the leaf counts as n reference tests).  Needs every lane of the wave running (the
-// wavefront kernels; the megakernel reaches here only through the same step with all lanes on).
-template <bool COUNT, bool FAST_RCP, class ST>
-__device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, TravLean& s, uint64_t parked, const ST& stack,
-                                           Counters& cnt) {
-    const int f = (int)__builtin_ctzll(parked);
-    int my0 = 0, myn = 0;
-    big_seg(s, my0, myn);
-    const int rec0 = __builtin_amdgcn_readlane(my0, f), n = __builtin_amdgcn_readlane(myn, f);
-    auto bc = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), f)); };
-    Ray q;
-    q.o = mk(bc(r.o.x), bc(r.o.y), bc(r.o.z));
-    q.d = mk(bc(r.d.x), bc(r.d.y), bc(r.d.z));
-    q.inv = mk(bc(r.inv.x), bc(r.inv.y), bc(r.inv.z));
-    const float pb = bc(s.best_t);
-    float bt;
-    int bk;
-    chunk_leaf<FAST_RCP>(sc, q, rec0, pb < 0.0f ? __builtin_inff() : pb, bt, bk);
-    const int lane = (int)(threadIdx.x & 63u);
-    if (lane == f) {
-        const bool take = (bk != 0x7fffffff) & ((s.best_t < 0.0f) | (bt < s.best_t));
-        s.best_t = take ? bt : s.best_t;
-        s.best = take ? rec0 + bk : s.best;
-        if (COUNT) cnt.tri_tests += n;
-        s.k += n;
-        s.fl &= ~TF_PARK;
-        if (s.k == s.nt) {
-            s.fl &= ~TF_LEAF;
-            lean_decide(s, stack);
-        } else if (big_at(sc, s)) {
-            s.fl |= TF_PARK;  // its right leaf is big too
-        }
-    }
-}
-
 // Several rays at one big leaf (the wavefront kernel's chunk walk; verdict r03 item 3 step 3):
 // when a turn starts, ~11 lanes of a wave on average are parked at the SAME big leaf of the boat
-// (profiles/r04e_park_diag.log) and chunk_turn served them one walk each.  Here up to kMultiRays
+// (profiles/r04e_park_diag.log) and a turn served them one walk each (chunk_leaf for the first
+// parked lane's ray, round 3).  Here up to kMultiRays
 // of them (the first parked lane f and the lanes parked at f's leaf) share ONE walk: each block of
 // 64 chunks is loaded once and checked against every ray (its o, d, 1/d, |d|, |o| and bound read
 // from the owner lane), the open (chunk, ray) pairs are gathered one per lane in ray order, and a
@@ -659,7 +627,7 @@ __device__ __forceinline__ void chunk_turn(const SceneView& sc, const Ray& r, Tr
 // entry able to report a hit at t <= the ray's bound at check time is tested, the bound never
 // drops below the leaf's final answer, so each ray ends with the smallest (t, position) over its
 // leaf's hitting entries whenever that beats its prior; and each served lane then takes the leaf
-// exactly as chunk_turn does.
+// exactly as the single-ray turn did.
 constexpr int kMultiRays = 16;
 // The walk for the lanes of `same` (wave-uniform, at most kMultiRays lanes; every lane of the wave
 // runs), each with its own ray r and closest t so far `prior` (+inf for none), over the leaf whose
@@ -796,8 +764,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
             big_seg(s, my0, myn);
             if (CHUNKS && sc.lnodes && __ballot(1) == ~0ull &&
                 sc.tris[__builtin_amdgcn_readlane(my0, (int)__builtin_ctzll(parked))].lbvh > 0) {  // its leaf has chunks
-                if (sc.lkeys) chunk_turn_multi<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
-                else chunk_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
+                chunk_turn_multi<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);  // sc.lkeys: k_wf_trace's BIG instances
             } else
                 big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
             return true;
@@ -908,7 +875,7 @@ struct TravSel { using type = TravState; };
 template <int TRAV>
 struct TravSel<TRAV, true> { using type = TravLean; };
 
-// CHUNKS: big leaves with leaf chunks take chunk_turn (the wavefront traversal kernel; the
+// CHUNKS: big leaves with leaf chunks take chunk_turn_multi (the wavefront traversal kernel; the
 // megakernel keeps the cooperative turn and its registers)
 template <int TRAV, bool COUNT, bool CHUNKS = false, class ST>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,

@@ -280,7 +280,7 @@ hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, h
 
 // Leaf chunk stress (pt_selftest_leaf): rays against the leaf whose records start at rec0, tested
 // once by the reference's sequential loop over all n entries (each lane its own ray) and once by
-// chunk_leaf (the wave on each lane's ray in turn, as chunk_turn runs it), both against the same
+// chunk_leaf (the wave on each lane's ray in turn, as round 3's single-ray turn ran it), both against the same
 // closest t so far (prior; none for half the rays).  Ray families (mode): 0 origins
 // within 5 units of a random point of an entry, directions uniform; 1 aimed at such a point
 // from 10^-3 .. 20 units away; 2 grazing: along the entry's plane, tilted by 10^-7 .. 10^-1 rad,
