@@ -1325,7 +1325,11 @@ extern "C" int pt_render_multi(pt_scene* const* scenes, int n, const float meta[
         for (int h = 0; h < g; ++h)
             if (!scenes[g] || scenes[g] == scenes[h]) return fail(PT_ERR_INVALID, "null or repeated scene");
     if (!scenes[0]) return fail(PT_ERR_INVALID, "null scene");
-    if (n == 1) return pt_render(scenes[0], meta, frame0, nframes, frame_stride, max_depth, mode, accum, counters);
+    const Opts o = opts_snapshot();
+    // one device is pt_render itself — unless option reduce=rccl asks for the RCCL branch anyway
+    // (a one-rank communicator: how a one-GPU machine runs that code, tests/test_gpu_multi.py)
+    if (n == 1 && !o.is("reduce", "rccl"))
+        return pt_render(scenes[0], meta, frame0, nframes, frame_stride, max_depth, mode, accum, counters);
     FrameParams fp{};
     int rc = make_params(meta, max_depth, fp);
     if (rc != PT_OK) return rc;
@@ -1335,7 +1339,6 @@ extern "C" int pt_render_multi(pt_scene* const* scenes, int n, const float meta[
     bool distinct = true;
     for (int g = 0; g < n; ++g)
         for (int h = 0; h < g; ++h) distinct &= scenes[g]->device != scenes[h]->device;
-    const Opts o = opts_snapshot();
     const bool want_rccl = !o.is("reduce", "ordered");
     if (o.is("reduce", "rccl") && (!distinct || !rccl_api().ok))
         return fail(PT_ERR_INVALID, "option reduce=rccl needs distinct devices and librccl.so.1");

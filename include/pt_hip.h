@@ -178,7 +178,8 @@ const char* pt_build_id(void);
  * librccl.so.1 loads) = ONE ncclReduce(sum, f32) to device 0 over a communicator made once per
  * device list (ncclCommInitAll, single process) — the summation order is RCCL's; "ordered" (and
  * always with repeated devices) = peer copies added on device 0 in device order,
- * deterministic.  n == 1 is exactly pt_render.  counters: nullable, summed over devices.
+ * deterministic.  n == 1 is exactly pt_render (with option reduce=rccl: the render and a one-rank
+ * RCCL communicator's reduce, the same bits).  counters: nullable, summed over devices.
  * Blocking; the scenes must not be in use by other calls meanwhile. */
 int pt_render_multi(pt_scene* const* scenes, int n, const float meta[48], uint32_t frame0, uint32_t nframes,
                     uint32_t frame_stride, int max_depth, int mode, float* accum, pt_counters* counters);

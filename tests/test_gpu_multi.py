@@ -4,8 +4,9 @@ scene per device, partial f32 accumulators reduced onto the first scene's device
 The box has one GPU, so the multi-device orchestration runs with repeated devices (several scenes
 on device 0: one host thread each, then the ORDERED reduction: partials added in device order).
 That reduction is deterministic, so it is pinned bit for bit against the oracle's per-shard
-renders summed in the same order; n = 1 is pt_render exactly.  The RCCL reduction (distinct
-devices) changes only the summation order of the same partials; the driver's 8-GPU node runs it.
+renders summed in the same order; n = 1 is pt_render exactly, and through a one-rank RCCL
+communicator (option reduce=rccl) too.  The RCCL reduction over distinct devices changes only the
+summation order of the same partials; the driver's 8-GPU node runs it.
 """
 import numpy as np
 import pytest
@@ -35,6 +36,25 @@ def test_single_device_list_is_pt_render(packed, env):
         a, ca = pt_amd.render_multi([s], meta, 0, 20, 1, 8, accum=init.copy(), counters=True)
         b, cb = s.render(meta, 0, 20, 1, 8, accum=init.copy(), counters=True)
     assert np.array_equal(bits(a), bits(b)) and ca == cb
+
+
+@pytest.mark.timeout(240, method="thread")  # a stuck collective ends the run with its stacks, not a hang
+def test_rccl_one_rank_is_pt_render(packed, env):
+    """The RCCL branch on the one-GPU box: option reduce=rccl sends a one-device list through it —
+    librccl loaded, ncclCommInitAll over one device, the ncclReduce (a copy onto itself), the
+    communicator released — and the bits are pt_render's."""
+    p = packed["CornellBox"]
+    meta = p.meta_for(128, 128)
+    init = np.random.default_rng(5).uniform(0, 1, (128, 128, 3)).astype(np.float32)
+    env.set("PT_REDUCE", "rccl")
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        try:
+            a, ca = pt_amd.render_multi([s], meta, 0, 9, 1, 8, accum=init.copy(), counters=True)
+            a2, _ = pt_amd.render_multi([s], meta, 0, 9, 1, 8, accum=init.copy(), counters=True)  # cached communicator
+        finally:
+            pt_amd.release_communicators()
+        b, cb = s.render(meta, 0, 9, 1, 8, accum=init.copy(), counters=True)
+    assert np.array_equal(bits(a), bits(b)) and np.array_equal(bits(a2), bits(b)) and ca == cb
 
 
 @pytest.mark.parametrize("n,mode", [(2, pt_amd.MODE_AUTO), (3, pt_amd.MODE_MEGAKERNEL), (4, pt_amd.MODE_WAVEFRONT)])
