@@ -210,7 +210,8 @@ def native_multi(args):
                                   f"round-robin over {n} devices in one process (pt_render_multi), host accumulator "
                                   f"(PCIe upload + read-back in the step)",
                       "mode": args.mode, "samples_per_step": total,
-                      "reduce": (args.reduce or "rccl") if n > 1 else "none"}}
+                      "reduce": (args.reduce or "rccl") if n > 1 else
+                      ("rccl (one-rank communicator)" if args.reduce == "rccl" else "none")}}
     print(json.dumps(out), flush=True)
 
 
