@@ -3,7 +3,8 @@
 BVH: per ray, the reference walk's node steps and leaf-pair test counts (f64 restatement of the
 ray/box and ray/triangle tests, random rays inside the scene box), then a 64-lane wave with refill
 running lean<K> turns under a node-bias policy; prints the modelled cost (VALU instructions) and
-lane use, with and without dealing a leaf turn's tests over all lanes.
+lane use, with and without dealing a leaf turn's tests over all lanes, and with
+runs of 8 entries dealt one per lane (lean_leaf_pool, round 4).
 usage: wave_model.py SCENE NRAYS"""
 import math
 import os
@@ -64,6 +65,7 @@ for k in range(NR):
         if tr: st.append(rp)
     seqs.append(seq)
 CN, CT, OV = 50.0, 35.0, 16.0
+OVR = 40.0  # per run of 8 (lean_leaf_pool): owner fetches, gather, key atomic
 def simulate(K, bias, redistribute):
     pool=list(range(len(seqs))); lanes=[None]*64; cost=0.0; useful=0.0
     def refill():
@@ -79,7 +81,12 @@ def simulate(K, bias, redistribute):
         nL=st.count('L'); nN=st.count('N')
         if nL and nL >= bias*nN:
             rem=[seqs[l[0]][l[1]][1]-l[2] if s=='L' else 0 for l,s in zip(lanes,st)]
-            if redistribute:
+            if redistribute == 'runs':  # lean_leaf_pool: runs of 8 entries dealt one per lane
+                tot=sum(rem); items=sum(math.ceil(x/8) for x in rem); steps=math.ceil(items/64)
+                cost+=steps*(8*CT+OVR); useful+=tot*CT
+                for i,s in enumerate(st):
+                    if s=='L': lanes[i][2]=seqs[lanes[i][0]][lanes[i][1]][1]
+            elif redistribute:
                 tot=sum(rem); steps=math.ceil(tot/64); cost+=steps*(CT+OV); useful+=tot*CT
                 for i,s in enumerate(st):
                     if s=='L': lanes[i][2]=seqs[lanes[i][0]][lanes[i][1]][1]
@@ -98,5 +105,6 @@ def simulate(K, bias, redistribute):
             if l[1]>=len(u): lanes[i]=None
         refill()
     return cost, useful/(64*cost)
-for K,bias,red in [(16,8,False),(16,2,False),(16,1,False),(8,8,False),(16,8,True),(16,2,True),(16,1,True)]:
+for K,bias,red in [(16,4,False),(16,8,False),(16,2,False),(16,1,False),(8,8,False),(16,8,True),(16,2,True),(16,1,True),
+                   (16,4,'runs'),(16,2,'runs'),(16,1,'runs')]:
     c,u=simulate(K,bias,red); print(name,'K',K,'bias',bias,'redist',red,'cost',round(c),'util',round(u,3))
