@@ -751,6 +751,101 @@ __device__ __forceinline__ void chunk_turn_multi(const SceneView& sc, const Ray&
     }
 }
 
+// A leaf turn with the pair's remaining entries pooled over the whole wave (the wavefront
+// traversal kernel, every lane running).  lean_leaf_loop has each leaf lane test its own pair K
+// entries per turn while the lanes in node state — and those whose pair ends sooner — idle: lane
+// use ~0.53 on Glossy (PMC; scripts/wave_model.py models the same).  Here every leaf lane's
+// remaining entries [k, lim) are cut into runs of kPoolRun positions, the runs of all leaf lanes —
+// and the lanes in node state test too — are dealt one per lane (ds_permute, as chunk_leaf
+// gathers chunks) and each lane tests its run against the
+// run owner's ray (fetched by ds_bpermute), keeping the smallest (t, position); the owner's best
+// is a 64-bit key — the f32 bits of t > 0 order as t — lowered with ds_min_u64 in its LDS slot.
+// The pair's smallest (t, position) is what the reference's strict-< loop over the entries in
+// order ends with among them; it replaces the lane's closest hit only if strictly closer, as that
+// loop's first test of it would.  Returns decide for this lane, as lean_leaf_loop does.  Runs of 4
+// (in process against lean16, bit-identical, profiles/r04s_ab_pool.log): Glossy +17 %, synthetic
+// 1k +10 %, 12.5k +5 %, 100k +9 %, 1M +22 %, the boat +9 %; runs of 8 and 16 in between.
+constexpr int kPoolRun = 4;
+template <bool COUNT, bool FAST_RCP, bool BIG>
+__device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r, TravLean& s, bool in_leaf, Counters& cnt) {
+    constexpr uint64_t kNoKey = ~0ull;
+    const int lane = (int)(threadIdx.x & 63u);
+    if constexpr (BIG) {  // park at a big leaf: now (no tests this turn)
+        if (in_leaf && big_at(sc, s)) { s.fl |= TF_PARK; in_leaf = false; }
+    }
+    // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
+    const int lim = (BIG && s.k < s.na && s.nt - s.na >= sc.big_leaf) ? s.na : s.nt;
+    const int n = in_leaf ? lim - s.k : 0;
+    const int runs = (n + kPoolRun - 1) / kPoolRun;
+    uint64_t* keys = sc.lkeys;
+    keys[lane] = kNoKey;
+    auto bpi = [](int v, int l) { return __builtin_amdgcn_ds_bpermute(l << 2, v); };
+    auto bpf = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(l << 2, __builtin_bit_cast(int, v))); };
+    int mine = 0;    // this lane's run: owner lane | run index << 6
+    int filled = 0;  // lanes holding a run (wave-uniform)
+    auto test_runs = [&]() {
+        const int o = mine & 63, j = mine >> 6;
+        const bool has = lane < filled;
+        // the run owner's pair and ray
+        const int k0 = bpi(s.k, o), lo = bpi(lim, o), na = bpi(s.na, o), la = bpi(s.la, o), lb = bpi(s.lb, o);
+        Ray q;
+        q.o = mk(bpf(r.o.x, o), bpf(r.o.y, o), bpf(r.o.z, o));
+        q.d = mk(bpf(r.d.x, o), bpf(r.d.y, o), bpf(r.d.z, o));
+        const int p0 = k0 + j * kPoolRun, p1 = has ? min(p0 + kPoolRun, lo) : p0;
+        float bt = __builtin_inff();
+        int bk = 0x7fffffff;
+#pragma unroll 2
+        for (int e = 0; e < kPoolRun; ++e) {
+            const int pos = p0 + e;
+            if (pos < p1) {
+                const int rec = pos < na ? la + pos : lb + (pos - na);
+                float t;
+                if (tri_hit<FAST_RCP>(sc.tris, rec, q, t) & (t < bt)) { bt = t; bk = pos; }  // positions ascend: the first of equal t
+            }
+        }
+        if (bk != 0x7fffffff)
+            atomicMin(reinterpret_cast<unsigned long long*>(keys + o),
+                      ((unsigned long long)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk);
+        filled = 0;
+    };
+    int pgot = 0, plo = 0, phi = 0;  // a gathered round, merged later (chunk_leaf)
+    auto merge = [&]() {
+        mine = (lane >= plo && lane < phi) ? pgot : mine;
+        phi = plo;
+    };
+    for (int j = 0;; ++j) {  // round j: every leaf lane with more than j runs contributes its run j
+        const bool give = runs > j;
+        const uint64_t m = __ballot(give);
+        if (!m) break;
+        const int c = (int)__popcll(m);
+        merge();
+        if (filled + c > 64) test_runs();
+        const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const int dest = give ? filled + below : (filled + c + (lane - below)) & 63;
+        pgot = __builtin_amdgcn_ds_permute(dest << 2, lane | (j << 6));
+        plo = filled;
+        phi = filled + c;
+        filled += c;
+    }
+    merge();
+    if (filled) test_runs();
+    bool decide = false;
+    if (in_leaf) {
+        const uint64_t k = keys[lane];
+        const float bt = __builtin_bit_cast(float, (uint32_t)(k >> 32));
+        const int pos = (int)(uint32_t)k;
+        const bool take = (k != kNoKey) & ((s.best_t < 0.0f) | (bt < s.best_t));
+        s.best_t = take ? bt : s.best_t;
+        s.best = take ? (pos < s.na ? s.la + pos : s.lb + (pos - s.na)) : s.best;
+        if (COUNT) cnt.tri_tests += n;
+        s.k = lim;
+        decide = s.k == s.nt;
+        s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
+        if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
+    }
+    return decide;
+}
+
 // Each iteration runs ONE unit type for the whole wave — a leaf turn (up to K triangle tests)
 // when leaf lanes >= node_bias * node lanes, else a node turn — keeping each lane's unit order.
 template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, class ST>
@@ -775,7 +870,10 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     if ((want_leaf | want_node) == 0) return false;
     bool decide = false;
     if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
-        if (state == TF_LEAF) decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);
+        if (CHUNKS && sc.lkeys && __ballot(1) == ~0ull)  // the wavefront kernel: the leaf entries pooled
+            decide = lean_leaf_pool<COUNT, FAST_RCP, BIG>(sc, r, s, state == TF_LEAF, cnt);
+        else if (state == TF_LEAF)
+            decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);
     } else if (state == 0) {
         decide = lean_node_unit<COUNT>(sc, r, s, cnt);
     }

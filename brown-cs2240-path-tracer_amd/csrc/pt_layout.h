@@ -143,8 +143,8 @@ struct SceneView {
     // in its leaf (ltris: one load per test, no index indirection)
     const LNode* lnodes;
     const Tri* ltris;
-    // the traversal kernel's per-wave LDS slots for chunk_turn_multi (kMultiRays keys; set by
-    // k_wf_trace for its big-leaf instances, nullptr elsewhere)
+    // the traversal kernel's per-wave LDS keys (64: lean_leaf_pool's per-lane bests, the first
+    // kMultiRays of them chunk_turn_multi's; set by k_wf_trace, nullptr in the other kernels)
     uint64_t* lkeys;
 };
 
