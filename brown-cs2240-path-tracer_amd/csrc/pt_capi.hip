@@ -76,7 +76,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
-    {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},
+    {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
     {"reduce", OPT_ENUM, "rccl|ordered"},
 };
@@ -926,6 +926,10 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         else
             view.lnodes = nullptr;
     }
+    // pooled leaf turns (pt_device.h lean_leaf_pool) where leaves are long enough to fill runs: the
+    // reference trees (Glossy +17 %, 1M synthetic +22 %, in process); on the SAH trees (leaves <= 8)
+    // Glossy measured -3.6 % (profiles/r04t_configs.jsonl), so there the lanes walk their own pairs
+    view.leaf_pool = o.has("leaf_pool") ? (o.flag("leaf_pool", 1) != 0) : (s->info.max_leaf >= 16);
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);

@@ -870,7 +870,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     if ((want_leaf | want_node) == 0) return false;
     bool decide = false;
     if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
-        if (CHUNKS && sc.lkeys && __ballot(1) == ~0ull)  // the wavefront kernel: the leaf entries pooled
+        if (CHUNKS && sc.leaf_pool && sc.lkeys && __ballot(1) == ~0ull)  // the wavefront kernel: the leaf entries pooled
             decide = lean_leaf_pool<COUNT, FAST_RCP, BIG>(sc, r, s, state == TF_LEAF, cnt);
         else if (state == TF_LEAF)
             decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);

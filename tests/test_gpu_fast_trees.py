@@ -5,7 +5,8 @@
   MedievalBoat 1920x1080 (depth 16, 4 frames);
 * the Cornell-sized synthetic scenes of the BVH sweep (scripts/synth_scene.py, seed 1234,
   BASELINE.json north_star) on the reference's tree: 1,000 and 12,500 triangles (1024^2,
-  depth 8, 8 frames, three bands), 100,000 (one band, 8 frames) and 1,000,000 (one band, 2 frames: the reference builder's
+  depth 8, 8 frames, three bands), 100,000 (one band, 8 frames; with and without the traversal
+  kernel's pooled leaf turns) and 1,000,000 (one band, 2 frames: the reference builder's
   depth cap of 16 keeps even this tree at <= 32,767 internal nodes), plus 12,500 on the SAH tree.
 The bands are rows that see light (the light at rows ~190-210; the random triangles shade the
 rest of the box more and more as N grows).
@@ -86,9 +87,13 @@ def test_synthetic_12500_sah_rows_bitexact(synth_packed):
     _trace_kernel_ran(profs)
 
 
-def test_synthetic_100k_band_bitexact(synth_packed):
-    _, profs = _render_bands(synth_packed(100000), 1024, 1024, 8, 8, [(192, 208)])
+def test_synthetic_100k_band_bitexact(synth_packed, ptopts):
+    p = synth_packed(100000)
+    img, profs = _render_bands(p, 1024, 1024, 8, 8, [(192, 208)])
     _trace_kernel_ran(profs)
+    ptopts.set("leaf_pool", "0")  # the same render with each lane walking its own leaf pairs
+    img2, _ = _render_bands(p, 1024, 1024, 8, 8, [(192, 208)])
+    assert_same_bits(img2, img, "leaf_pool=0 vs default (pooled leaf turns)")
 
 
 def test_synthetic_1m_band_bitexact(synth_packed):

@@ -101,6 +101,11 @@ KERNELS = {
     "wavefront_sort512_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "512", "PT_MAILBOX": "0"},
     "wavefront_sort64_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_SORT": "64", "PT_MAILBOX": "0",
                                           "PT_WF_TRACE_BLOCKS": "1"},
+    # the traversal kernel's leaf turns pooled over the wave (lean_leaf_pool; auto on the reference
+    # trees) and not (each lane walks its own pair, lean_leaf_loop), and pooled on one block
+    "wavefront_nopool_nomailbox": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "0", "PT_MAILBOX": "0"},
+    "wavefront_pool_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "1", "PT_MAILBOX": "0",
+                                        "PT_WF_TRACE_BLOCKS": "1"},
     # the traversal kernel on one block with the big-leaf turns forced onto small leaves
     "wavefront_big4_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_MAILBOX": "0",
                               "PT_WF_TRACE_BLOCKS": "1"},
@@ -110,7 +115,7 @@ KERNELS = {
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
-            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING")
+            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL")
 
 
 @pytest.fixture(params=list(KERNELS))
