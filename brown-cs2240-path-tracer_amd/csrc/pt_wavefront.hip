@@ -175,7 +175,11 @@ static_assert(win_tab(kHitRingMax) >= kHitRingMax / kWinRays + 2, "wtab must nam
 static_assert(win_tab(kHitRing) >= kHitRing / kWinRays + 2, "wtab must name every window the ring can hold");
 // per wave: the window's rays, the hit ring, the window ids, and 64 keys — one per lane for
 // lean_leaf_pool's pooled leaf turns, the first kMultiRays for chunk_turn_multi's shared walks
-__host__ __device__ constexpr uint32_t stage_bytes(uint32_t ring) { return kWinRays * 32 + ring * 8 + win_tab(ring) * 4 + 64 * 8; }
+__host__ __device__ constexpr uint32_t stage_bytes(uint32_t ring) { return kWinRays * 32 + ring * 8 + win_tab(ring) * 4; }
+// after the waves' stages, when the scene needs them (pooled leaf turns or leaf chunks: keys_on),
+// 64 keys per wave — one per lane for lean_leaf_pool, the first kMultiRays for chunk_turn_multi
+constexpr uint32_t kKeyBytes = 64 * 8;
+__host__ __device__ inline bool keys_on(const SceneView& sc) { return sc.leaf_pool != 0 || sc.lnodes != nullptr; }
 // the traversal flavours that have a 256-entry-ring instance (the defaults: lean16 + fast rcp, with
 // and without big-leaf turns); the others always use 128
 constexpr bool has_big_ring(int trav) { return trav == 17 || trav == 177; }
@@ -207,7 +211,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     float4* wray = reinterpret_cast<float4*>(stage);               // [kWinRays][2]
     int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [RING]
     uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32 + RING * 8);  // [kWinTab] window ids
-    sc.lkeys = reinterpret_cast<uint64_t*>(stage + kWinRays * 32 + RING * 8 + kWinTab * 4);  // [64] keys
+    char* key_base = stage_base + (blockDim.x / 64u) * stage_bytes(nring);
+    const uint32_t key_bytes = keys_on(sc) ? (blockDim.x / 64u) * kKeyBytes : 0u;
+    sc.lkeys = key_bytes ? reinterpret_cast<uint64_t*>(key_base + (threadIdx.x / 64u) * kKeyBytes) : nullptr;
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip
     // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     if (sparse > 0)
         while (wr > 1 && (uint64_t)count * (uint32_t)sparse < (uint64_t)nwaves * wr) wr >>= 1;
     const uint32_t nwin = (count + wr - 1) / wr;
-    if (LDS) stage_scene_lds(sc, stage_base + (blockDim.x / 64u) * stage_bytes(nring));
+    if (LDS) stage_scene_lds(sc, key_base + key_bytes);
     const uint32_t lane = lane_id();
     constexpr uint32_t kNone = 0xffffffffu;
     uint32_t nstatic = 0;
@@ -863,7 +869,7 @@ template <bool LDS, int TRAV, bool COUNT>
 static size_t trace_lds(const SceneView& sc, uint32_t ring = kHitRing) {
     const size_t span = LDS ? sc.span_bytes : 0;
     if (TRAV >= 300) return (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * ((size_t)kBfSlots * 64 * 4) + span;
-    return (size_t)sc.max_stack * 4 * kTraceBlock + (kTraceBlock / 64) * stage_bytes(ring) + span;
+    return (size_t)sc.max_stack * 4 * kTraceBlock + (kTraceBlock / 64) * (stage_bytes(ring) + (keys_on(sc) ? kKeyBytes : 0)) + span;
 }
 // resident blocks of `kernel` per CU at `lds` bytes of dynamic LDS, times the CUs: the persistent
 // grid of the trace and step kernels (cached per kernel instance and LDS size)
