@@ -100,7 +100,7 @@ def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int
     key = f"{W}x{H}x{spp}x{depth}x{world}"
     cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix) and field in v}
     # the timed instances: COUNT=false (template argument 4 of k_wf_step_bf<EXT, LDS, rcp, COUNT,
-    # GEN> and of k_wf_trace<LDS, TRAV, COUNT, RING> counted from 1 as 3; round 3's profiles name
+    # GEN> and of k_wf_trace<LDS, TRAV, COUNT, RING, PRUN> counted from 1 as 3; round 3's profiles name
     # a sixth k_wf_step_bf argument, the removed opt-in CULL, after COUNT); averaged per launch,
     # weighted by their dispatch counts when the summary has them (extension, shadow and the one
     # camera GEN launch per batch), else the plain mean of the instances (GEN left out)

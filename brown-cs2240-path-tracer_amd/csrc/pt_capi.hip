@@ -76,7 +76,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
-    {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},
+    {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},   {"pool_run", OPT_ENUM, "2|4"},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
     {"reduce", OPT_ENUM, "rccl|ordered"},
 };
@@ -928,8 +928,15 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     }
     // pooled leaf turns (pt_device.h lean_leaf_pool) where leaves are long enough to fill runs: the
     // reference trees (Glossy +17 %, 1M synthetic +22 %, in process); on the SAH trees (leaves <= 8)
-    // Glossy measured -3.6 % (profiles/r04t_configs.jsonl), so there the lanes walk their own pairs
-    view.leaf_pool = o.has("leaf_pool") ? (o.flag("leaf_pool", 1) != 0) : (s->info.max_leaf >= 16);
+    // Glossy measured -3.6 % (profiles/r04t_configs.jsonl), so there the lanes walk their own pairs.
+    // The run length: 2 where the leaves reference >= 128 Ki triangles (their records outgrow an
+    // XCD's 4 MB L2: 100k +12 %, 1M +26 % against runs of 4), else 4 (Glossy, the boat: 1-1.5 %
+    // faster than 2; profiles/r04aa_ab_run.log); option pool_run=2|4 sets it
+    {
+        const bool pool = o.has("leaf_pool") ? (o.flag("leaf_pool", 1) != 0) : (s->info.max_leaf >= 16);
+        const long run = o.num("pool_run", s->info.leaf_refs >= (1u << 17) ? 2 : 4);
+        view.leaf_pool = pool ? (int32_t)run : 0;
+    }
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);

@@ -755,7 +755,7 @@ __device__ __forceinline__ void chunk_turn_multi(const SceneView& sc, const Ray&
 // traversal kernel, every lane running).  lean_leaf_loop has each leaf lane test its own pair K
 // entries per turn while the lanes in node state — and those whose pair ends sooner — idle: lane
 // use ~0.53 on Glossy (PMC; scripts/wave_model.py models the same).  Here every leaf lane's
-// remaining entries [k, lim) are cut into runs of kPoolRun positions, the runs of all leaf lanes —
+// remaining entries [k, lim) are cut into runs of RUN positions, the runs of all leaf lanes —
 // and the lanes in node state test too — are dealt one per lane (ds_permute, as chunk_leaf
 // gathers chunks) and each lane tests its run against the
 // run owner's ray (fetched by ds_bpermute), keeping the smallest (t, position); the owner's best
@@ -764,9 +764,15 @@ __device__ __forceinline__ void chunk_turn_multi(const SceneView& sc, const Ray&
 // order ends with among them; it replaces the lane's closest hit only if strictly closer, as that
 // loop's first test of it would.  Returns decide for this lane, as lean_leaf_loop does.  Runs of 4
 // (in process against lean16, bit-identical, profiles/r04s_ab_pool.log): Glossy +17 %, synthetic
-// 1k +10 %, 12.5k +5 %, 100k +9 %, 1M +22 %, the boat +9 %; runs of 8 and 16 in between.
-constexpr int kPoolRun = 4;
-template <bool COUNT, bool FAST_RCP, bool BIG>
+// 1k +10 %, 12.5k +5 %, 100k +9 %, 1M +22 %, the boat +9 %; runs of 8 and 16 in between.  The run
+// length RUN is sc.leaf_pool (2 or 4, set per scene by pt_capi.hip; a k_wf_trace template argument): runs of 2 against 4
+// (profiles/r04aa_ab_run.log) are +12 % on 100k and +26 % on 1M — trees whose triangles outgrow
+// the L2, where shorter runs put more independent triangle loads in flight — and -1 to -1.5 % on
+// Glossy and the boat.  RUN is a template argument: a run-time trip count kept only a third of the
+// gain (profiles/r04ab_ab_runtime_run.log: 100k +3 %, 1M +12 %; r04ad_ab_runtime_run.log: the
+// same with two entries per iteration), and both runs inlined into one kernel cost Glossy 1.5 %
+// (r04ac, r04ad: ablib/tmpl), so each run length is its own k_wf_trace instance.
+template <int RUN, bool COUNT, bool FAST_RCP, bool BIG>
 __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r, TravLean& s, bool in_leaf, Counters& cnt) {
     constexpr uint64_t kNoKey = ~0ull;
     const int lane = (int)(threadIdx.x & 63u);
@@ -776,7 +782,8 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
     // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
     const int lim = (BIG && s.k < s.na && s.nt - s.na >= sc.big_leaf) ? s.na : s.nt;
     const int n = in_leaf ? lim - s.k : 0;
-    const int runs = (n + kPoolRun - 1) / kPoolRun;
+    static_assert(RUN == 2 || RUN == 4, "pooled runs of 2 or 4 entries");
+    const int runs = (n + RUN - 1) / RUN;
     uint64_t* keys = sc.lkeys;
     keys[lane] = kNoKey;
     auto bpi = [](int v, int l) { return __builtin_amdgcn_ds_bpermute(l << 2, v); };
@@ -791,11 +798,11 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
         Ray q;
         q.o = mk(bpf(r.o.x, o), bpf(r.o.y, o), bpf(r.o.z, o));
         q.d = mk(bpf(r.d.x, o), bpf(r.d.y, o), bpf(r.d.z, o));
-        const int p0 = k0 + j * kPoolRun, p1 = has ? min(p0 + kPoolRun, lo) : p0;
+        const int p0 = k0 + j * RUN, p1 = has ? min(p0 + RUN, lo) : p0;
         float bt = __builtin_inff();
         int bk = 0x7fffffff;
 #pragma unroll 2
-        for (int e = 0; e < kPoolRun; ++e) {
+        for (int e = 0; e < RUN; ++e) {
             const int pos = p0 + e;
             if (pos < p1) {
                 const int rec = pos < na ? la + pos : lb + (pos - na);
@@ -848,7 +855,8 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
 
 // Each iteration runs ONE unit type for the whole wave — a leaf turn (up to K triangle tests)
 // when leaf lanes >= node_bias * node lanes, else a node turn — keeping each lane's unit order.
-template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, class ST>
+// PRUN: the pooled leaf turns' run length (lean_leaf_pool)
+template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, int PRUN = 4, class ST>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, const ST& stack,
                                                Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE | (BIG ? TF_PARK : 0));
@@ -871,7 +879,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     bool decide = false;
     if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
         if (CHUNKS && sc.leaf_pool && sc.lkeys && __ballot(1) == ~0ull)  // the wavefront kernel: the leaf entries pooled
-            decide = lean_leaf_pool<COUNT, FAST_RCP, BIG>(sc, r, s, state == TF_LEAF, cnt);
+            decide = lean_leaf_pool<PRUN, COUNT, FAST_RCP, BIG>(sc, r, s, state == TF_LEAF, cnt);
         else if (state == TF_LEAF)
             decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);
     } else if (state == 0) {
@@ -975,7 +983,7 @@ struct TravSel<TRAV, true> { using type = TravLean; };
 
 // CHUNKS: big leaves with leaf chunks take chunk_turn_multi (the wavefront traversal kernel; the
 // megakernel keeps the cooperative turn and its registers)
-template <int TRAV, bool COUNT, bool CHUNKS = false, class ST>
+template <int TRAV, bool COUNT, bool CHUNKS = false, int PRUN = 4, class ST>
 __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, typename TravSel<TRAV>::type& s,
                                              const ST& stack, Counters& cnt) {
     if constexpr (TRAV >= 100 && TRAV < 160) {  // mailboxed lean<K> (SceneView::mailbox scenes); + 10: fast reciprocal
@@ -985,7 +993,7 @@ __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, 
     else if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 160: big-leaf cooperation
         constexpr int B = TRAV % 10;
         constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
-        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, TRAV >= 160, CHUNKS>(sc, r, s, stack, cnt);
+        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, TRAV >= 160, CHUNKS, PRUN>(sc, r, s, stack, cnt);
     }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, cnt);
     else return trav_step_pred<COUNT>(sc, r, s, stack, cnt);

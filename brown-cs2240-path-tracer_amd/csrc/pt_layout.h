@@ -144,7 +144,8 @@ struct SceneView {
     const LNode* lnodes;
     const Tri* ltris;
     // leaf turns of the traversal kernel pool the leaf lanes' entries over the wave (lean_leaf_pool):
-    // trees with leaves of >= 16 entries (the reference builder's); option leaf_pool
+    // trees with leaves of >= 16 entries (the reference builder's); option leaf_pool.  The value is
+    // the run length (2 or 4; 0: off), option pool_run
     int32_t leaf_pool;
     // the traversal kernel's per-wave LDS keys (64: lean_leaf_pool's per-lane bests, the first
     // kMultiRays of them chunk_turn_multi's; set by k_wf_trace, nullptr in the other kernels)

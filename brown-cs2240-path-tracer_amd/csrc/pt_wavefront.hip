@@ -200,7 +200,7 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 // busy (the last depths), windows of wr / 2 .. 1 entries spread the queue over more waves, so each
 // wave's traversal is the slowest of fewer rays.  A window still takes kWinRays sequence numbers
 // (ring and flush bookkeeping unchanged); only its queue span is wr.
-template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing>
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4>
 __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
                                                           uint32_t watchdog, int sparse) {
     constexpr uint32_t nring = RING, kWinTab = win_tab(RING);
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
             if (nv == 0 && cur == jl * kWinRays + wv && flushed >= (jl + 1) * kWinRays) break;  // all done
             continue;  // ring full with nothing in flight: the flush above frees it
         }
-        trav_advance<TRAV, COUNT, true>(sc, r, s, stack, c);
+        trav_advance<TRAV, COUNT, true, PRUN>(sc, r, s, stack, c);
         if (has && trav_finished(s)) {
             ring[sq & (nring - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;
@@ -848,21 +848,25 @@ __global__ __launch_bounds__(256) void k_wf_accum(const float* __restrict__ rad,
     } while (0)
 // TRAV >= 300: the brute-force + replay kernel (k_wf_trace_bf; + 10: fast reciprocal); >= 400: fused
 // with the shading (k_wf_step_bf)
-template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing>
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4>
 constexpr const void* trace_kernel() {
     if constexpr (TRAV >= 400) return (const void*)k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>;
     else if constexpr (TRAV >= 300) return (const void*)k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
-    else return (const void*)k_wf_trace<LDS, TRAV, COUNT, RING>;
+    else return (const void*)k_wf_trace<LDS, TRAV, COUNT, RING, PRUN>;
 }
-// the k_wf_trace instances with a 256-entry ring: the default flavours, uncounted
+// the k_wf_trace instances with a 256-entry ring and with pooled runs of 2 (SceneView::leaf_pool
+// == 2): the default flavours, uncounted (the others pool runs of 4: the same bits and counts)
 template <int TRAV, bool COUNT>
 constexpr bool has_variants() { return TRAV < 300 && has_big_ring(TRAV) && !COUNT; }
 template <bool LDS, int TRAV, bool COUNT>
-static const void* trace_instance(uint32_t ring) {
+static const void* trace_instance(uint32_t ring, bool run2) {
     if constexpr (has_variants<TRAV, COUNT>()) {
-        if (ring == kHitRingMax) return trace_kernel<LDS, TRAV, COUNT, kHitRingMax>();
+        if (ring == kHitRingMax)
+            return run2 ? trace_kernel<LDS, TRAV, COUNT, kHitRingMax, 2>() : trace_kernel<LDS, TRAV, COUNT, kHitRingMax>();
+        if (run2) return trace_kernel<LDS, TRAV, COUNT, kHitRing, 2>();
     }
     (void)ring;
+    (void)run2;
     return trace_kernel<LDS, TRAV, COUNT>();
 }
 template <bool LDS, int TRAV, bool COUNT>
@@ -939,16 +943,17 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     // k_wf_trace's instance: the 256-entry hit ring when its extra 8 KB per block cost no block per
     // CU (option trace_ring: 128 / 256 forces one)
     uint32_t nring = kHitRing;
+    const bool run2 = sc.leaf_pool == 2;  // pooled runs of 2 (the has_variants instances)
     if constexpr (has_variants<TRAV, COUNT>()) {
         const size_t l1 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRing), l2 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRingMax);
         const bool fits = l2 <= max_block_lds() &&
                           (ws.trace_ring == (int)kHitRingMax ||
-                           (ws.trace_ring <= 0 && occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRingMax), l2) >=
-                                                      occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRing), l1)));
+                           (ws.trace_ring <= 0 && occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRingMax, run2), l2) >=
+                                                      occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(kHitRing, run2), l1)));
         if (fits) nring = kHitRingMax;
     }
     const size_t lds = trace_lds<LDS, TRAV, COUNT>(sc, nring);
-    int tblocks = occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(nring), lds);
+    int tblocks = occupancy_blocks(trace_instance<LDS, TRAV, COUNT>(nring, run2), lds);
     if (ws.trace_blocks > 0) tblocks = std::min(tblocks, ws.trace_blocks);  // option wf_trace_blocks (tests)
     const int iters = 2 * (fp.max_depth + 1);
     // option trace_watchdog: tests of the failure report
@@ -1025,13 +1030,15 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
                           dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
             } else {
-#define PT_TRACE(RG) PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, RG>), dim3(tblocks), \
-                               dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, watchdog, sparse)
+#define PT_TRACE(RG, PR) PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, RG, PR>), dim3(tblocks), \
+                                   dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, watchdog, sparse)
                 if constexpr (has_variants<TRAV, COUNT>()) {
-                    if (nring == kHitRingMax) PT_TRACE(kHitRingMax);
-                    else PT_TRACE(kHitRing);
+                    if (nring == kHitRingMax && run2) PT_TRACE(kHitRingMax, 2);
+                    else if (nring == kHitRingMax) PT_TRACE(kHitRingMax, 4);
+                    else if (run2) PT_TRACE(kHitRing, 2);
+                    else PT_TRACE(kHitRing, 4);
                 } else {
-                    PT_TRACE(kHitRing);
+                    PT_TRACE(kHitRing, 4);
                 }
 #undef PT_TRACE
             }

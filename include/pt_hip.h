@@ -153,6 +153,7 @@ int pt_set_hw_queues(int n);
  *   "trace_ring" "trace_watchdog"                                           integers
  *   "mb_uid_order"  forward | reverse   (read by pt_scene_create: uid numbering of mailbox scenes)
  *   "leaf_bvh"      integer             (read by pt_scene_create: leaves with a leaf BVH, >= this many entries)
+ *   "pool_run"      2 | 4               (entries per run of the pooled leaf turns; default per scene)
  *   "reduce"        rccl | ordered      (pt_render_multi's reduction)
  * DESIGN.md §6 describes each.  pt_get_option writes the current value ("" = default) into buf. */
 int pt_set_option(const char* name, const char* value);

@@ -22,7 +22,7 @@ def uncounted(name: str, kernel: str) -> bool:
     args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")]
     if name.startswith("k_wf_step_bf<"):  # <EXT, LDS, rcp, COUNT, GEN>
         return len(args) >= 4 and args[3] == "false"
-    if name.startswith("k_wf_trace<"):  # <LDS, TRAV, COUNT, RING>
+    if name.startswith("k_wf_trace<"):  # <LDS, TRAV, COUNT, RING, PRUN>
         return len(args) >= 3 and args[2] == "false"
     return bool(args) and args[-1] == "false"
 

@@ -109,6 +109,12 @@ def test_layout_options():
         assert pt_amd.get_option("wf_paths") == str(8 << 20)
         with pytest.raises(pt_amd.PtError):
             pt_amd.set_option("wf_paths", "lots")
+        for run in (2, 4):  # pooled leaf turns: runs of 2 or 4 entries
+            pt_amd.set_option("pool_run", run)
+            assert pt_amd.get_option("pool_run") == str(run)
+        for bad in ("0", "1", "3", "8", "-2"):
+            with pytest.raises(pt_amd.PtError):
+                pt_amd.set_option("pool_run", bad)
     finally:
         pt_amd.reset_options()
 

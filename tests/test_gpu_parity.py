@@ -106,6 +106,9 @@ KERNELS = {
     "wavefront_nopool_nomailbox": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "0", "PT_MAILBOX": "0"},
     "wavefront_pool_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "1", "PT_MAILBOX": "0",
                                         "PT_WF_TRACE_BLOCKS": "1"},
+    # runs of 2 entries (the default where leaves reference >= 128 Ki triangles)
+    "wavefront_pool_run2_nomailbox": {"PT_KERNEL": "wavefront", "PT_POOL_RUN": "2", "PT_MAILBOX": "0"},
+    "wavefront_pool_run2_1block": {"PT_KERNEL": "wavefront", "PT_POOL_RUN": "2", "PT_WF_TRACE_BLOCKS": "1"},
     # the traversal kernel on one block with the big-leaf turns forced onto small leaves
     "wavefront_big4_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_MAILBOX": "0",
                               "PT_WF_TRACE_BLOCKS": "1"},
@@ -115,7 +118,8 @@ KERNELS = {
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
-            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL")
+            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
+            "PT_POOL_RUN")
 
 
 @pytest.fixture(params=list(KERNELS))

@@ -1,5 +1,5 @@
 """The pooled leaf turn (pt_device.h lean_leaf_pool, round 4): a leaf lane's remaining entries
-[k, lim) of its leaf pair are cut into runs of kPoolRun positions, the runs are tested by other
+[k, lim) of its leaf pair are cut into runs of sc.leaf_pool positions (option pool_run: 2 or 4), the runs are tested by other
 lanes in any order, each run keeps its smallest (t, position), the owner's key is the minimum of
 the runs' (t, position) keys, and the result replaces the lane's closest hit only if strictly
 closer.  Claim: that is exactly where the reference's leaf loop ends — entries in order, each hit
@@ -10,7 +10,7 @@ import random
 
 import pytest
 
-RUN = 4  # pt_device.h kPoolRun
+RUNS = (1, 2, 4, 8, 16)  # option pool_run takes 2 or 4; the claim holds for any run length
 
 
 def reference_loop(ts, prior_t, prior_rec, k0):
@@ -23,8 +23,8 @@ def reference_loop(ts, prior_t, prior_rec, k0):
     return best_t, best
 
 
-def pooled(ts, prior_t, prior_rec, k0, rng):
-    runs = [(p, min(p + RUN, len(ts))) for p in range(k0, len(ts), RUN)]
+def pooled(ts, prior_t, prior_rec, k0, rng, run):
+    runs = [(p, min(p + run, len(ts))) for p in range(k0, len(ts), run)]
     rng.shuffle(runs)  # any lane, any order
     key = None
     for p0, p1 in runs:
@@ -40,8 +40,9 @@ def pooled(ts, prior_t, prior_rec, k0, rng):
     return prior_t, prior_rec
 
 
-@pytest.mark.parametrize("seed", range(100))
-def test_pooled_turn_equals_the_reference_loop(seed):
+@pytest.mark.parametrize("run", RUNS)
+@pytest.mark.parametrize("seed", range(40))
+def test_pooled_turn_equals_the_reference_loop(seed, run):
     rng = random.Random(seed)
     for _ in range(200):
         n = rng.randint(1, 70)
@@ -50,7 +51,7 @@ def test_pooled_turn_equals_the_reference_loop(seed):
         k0 = rng.randint(0, n - 1)
         prior_t = rng.choice([-1.0] + tvals)
         prior_rec = -1 if prior_t < 0 else 10_000
-        assert pooled(ts, prior_t, prior_rec, k0, rng) == reference_loop(ts, prior_t, prior_rec, k0)
+        assert pooled(ts, prior_t, prior_rec, k0, rng, run) == reference_loop(ts, prior_t, prior_rec, k0)
 
 
 def test_the_model_has_teeth():
