@@ -1088,8 +1088,10 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;
     // turn policy of the lean16 traversal: 4 since the queues are grouped by coherence keys (in
-    // process: Glossy +2.5 %, boat +1 %, 1M synthetic +1.8 % over 8; 1 = majority: -13 % in round 1)
-    if (sc.node_bias <= 0) sc.node_bias = 4;
+    // process: Glossy +2.5 %, boat +1 %, 1M synthetic +1.8 % over 8; 1 = majority: -13 % in round 1);
+    // 1 where the leaf turns pool runs of 2 (100k +5.2 %, 1M +5.3 % over 4, both orders:
+    // profiles/r04ai_node_bias.log; with runs of 4 the bias is within noise, r04z_ab_node_bias.log)
+    if (sc.node_bias <= 0) sc.node_bias = sc.leaf_pool == 2 ? 1 : 4;
     const bool lds = lo.lds && scene_fits_lds(sc);
     // lean16 with the fast reciprocal by default (measured best on gfx950, scripts/perf_variants.py);
     // the wavefront always uses a flattened traversal; lean flavours take the fast reciprocal
