@@ -106,7 +106,7 @@ KERNELS = {
     "wavefront_nopool_nomailbox": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "0", "PT_MAILBOX": "0"},
     "wavefront_pool_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "1", "PT_MAILBOX": "0",
                                         "PT_WF_TRACE_BLOCKS": "1"},
-    # runs of 2 entries (the default where leaves reference >= 128 Ki triangles)
+    # runs of 2 entries (the default where leaves reference >= 32 Ki triangles and no leaf is big)
     "wavefront_pool_run2_nomailbox": {"PT_KERNEL": "wavefront", "PT_POOL_RUN": "2", "PT_MAILBOX": "0"},
     "wavefront_pool_run2_1block": {"PT_KERNEL": "wavefront", "PT_POOL_RUN": "2", "PT_WF_TRACE_BLOCKS": "1"},
     # the traversal kernel on one block with the big-leaf turns forced onto small leaves
