@@ -926,16 +926,18 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         else
             view.lnodes = nullptr;
     }
-    // pooled leaf turns (pt_device.h lean_leaf_pool) where leaves are long enough to fill runs: the
-    // reference trees (Glossy +17 %, 1M synthetic +22 %, in process); on the SAH trees (leaves <= 8)
-    // Glossy measured -3.6 % (profiles/r04t_configs.jsonl), so there the lanes walk their own pairs.
-    // The run length: 2 where the leaves reference >= 32 Ki triangles and no leaf is big (100k
-    // +12 %, 1M +26 % against runs of 4: profiles/r04aa_ab_run.log; 12.5k +3.7 % with node bias
-    // 1-2: r04ak_run2_bias.log), else 4 (Glossy 5 Ki references, 1k, and the boat — 52 Ki
-    // references, but big leaves walked in chunks — are 1-2 % faster with 4); option pool_run=2|4
+    // pooled leaf turns (pt_device.h lean_leaf_pool) on every tree (option leaf_pool=0: each lane
+    // walks its own pairs).  The run length: 2 on trees of short leaves (< 16 entries: the SAH
+    // builder's; Glossy +2.9 %, the boat +16.5 %, 100k +26 %, 1M +29 % over unpooled:
+    // profiles/r04am_sah_pool.log — runs of 4 there cost Glossy 3.6 %, r04t_configs.jsonl) and
+    // where the leaves reference >= 32 Ki triangles and no leaf is big (100k +12 %, 1M +26 % against
+    // runs of 4: r04aa_ab_run.log; 12.5k +3.7 % with node bias 1-2: r04ak_run2_bias.log), else 4
+    // (Glossy 5 Ki references, 1k, and the boat — 52 Ki references, but big leaves walked in
+    // chunks — are 1-2 % faster with 4); option pool_run=2|4
     {
-        const bool pool = o.has("leaf_pool") ? (o.flag("leaf_pool", 1) != 0) : (s->info.max_leaf >= 16);
-        const long run = o.num("pool_run", (s->info.leaf_refs >= (1u << 15) && view.big_leaf == 0) ? 2 : 4);
+        const bool pool = o.flag("leaf_pool", 1) != 0;
+        const bool run2 = s->info.max_leaf < 16 || (s->info.leaf_refs >= (1u << 15) && view.big_leaf == 0);
+        const long run = o.num("pool_run", run2 ? 2 : 4);
         view.leaf_pool = pool ? (int32_t)run : 0;
     }
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)

@@ -71,7 +71,7 @@ def test_sah_glossy_1024_depth16_rows_bitexact(sah_packed):
 def test_sah_boat_1080p_depth16_rows_bitexact(sah_packed):
     p = sah_packed["MedievalBoat"]
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        assert s.info["max_leaf"] <= 8  # no big leaves on the SAH tree: plain lean16 turns
+        assert s.info["max_leaf"] <= 8  # no big leaves on the SAH tree: lean16 turns, leaf entries pooled in runs of 2
     _, profs = _render_bands(p, 1920, 1080, 4, 16, [(680, 696), (560, 576)])
     _trace_kernel_ran(profs)
 
