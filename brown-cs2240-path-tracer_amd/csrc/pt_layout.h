@@ -143,9 +143,9 @@ struct SceneView {
     // in its leaf (ltris: one load per test, no index indirection)
     const LNode* lnodes;
     const Tri* ltris;
-    // leaf turns of the traversal kernel pool the leaf lanes' entries over the wave (lean_leaf_pool):
-    // trees with leaves of >= 16 entries (the reference builder's); option leaf_pool.  The value is
-    // the run length (2 or 4; 0: off), option pool_run
+    // leaf turns of the traversal kernel pool the leaf lanes' entries over the wave (lean_leaf_pool;
+    // every tree by default, option leaf_pool).  The value is the run length (2 or 4; 0: off),
+    // chosen per scene by pt_capi.hip, option pool_run
     int32_t leaf_pool;
     // the traversal kernel's per-wave LDS keys (64: lean_leaf_pool's per-lane bests, the first
     // kMultiRays of them chunk_turn_multi's; set by k_wf_trace, nullptr in the other kernels)

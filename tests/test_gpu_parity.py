@@ -101,8 +101,7 @@ KERNELS = {
     "wavefront_sort512_nomailbox": {"PT_KERNEL": "wavefront", "PT_SORT": "512", "PT_MAILBOX": "0"},
     "wavefront_sort64_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_SORT": "64", "PT_MAILBOX": "0",
                                           "PT_WF_TRACE_BLOCKS": "1"},
-    # the traversal kernel's leaf turns pooled over the wave (lean_leaf_pool; auto on the reference
-    # trees) and not (each lane walks its own pair, lean_leaf_loop), and pooled on one block
+    # the traversal kernel's leaf turns pooled over the wave (lean_leaf_pool; on by default) and not (each lane walks its own pair, lean_leaf_loop), and pooled on one block
     "wavefront_nopool_nomailbox": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "0", "PT_MAILBOX": "0"},
     "wavefront_pool_nomailbox_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_POOL": "1", "PT_MAILBOX": "0",
                                         "PT_WF_TRACE_BLOCKS": "1"},
