@@ -41,6 +41,7 @@ PKG = os.path.join(ROOT, "brown-cs2240-path-tracer_amd")
 sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector), spec
 
 
 def pack_scene(scene: str, out_dir: str, W: int, H: int, spp: int, synthetic: int = 0, bvh: str = "reference",
@@ -83,8 +84,8 @@ def cpu_baseline(tri, bvh, meta, depth, target_s=12.0):
     dt = time.perf_counter() - t
     return {"value": round(c["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"oracle/pt_oracle.c (CPU restatement of the reference WGSL; no CPU WebGPU adapter exists "
-                      f"here), {W}x{n_rows} rows x {nframes} frames of the same workload (depth {depth}), "
-                      f"{threads} OpenMP threads, {c['samples']} samples in {dt:.2f} s"}
+                      f"here) built gcc {oracle.lib_flags()} -fopenmp, {W}x{n_rows} rows x {nframes} frames of the "
+                      f"same workload (depth {depth}), {threads} OpenMP threads, {c['samples']} samples in {dt:.2f} s"}
 
 
 def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int, field: str = "hbm_bytes_per_launch"):
@@ -296,12 +297,21 @@ def main():
         frame0, nframes, fstride = frames_for_rank(args.share_rank, args.share_of, args.spp)
     stream = torch.cuda.Stream(device=dev)
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+    # the step ends with the accumulator on the host ("from the first kernel launch to
+    # the accumulator on the host"; the reference copies it to a MAP_READ buffer each frame,
+    # program-raymarch.ts:262-293): rank 0 copies the reduced accumulator to pinned host memory
+    host_acc = torch.empty((H, W, 3), dtype=torch.float32, pin_memory=True) if rank == 0 else None
+
+    def to_host():
+        if host_acc is not None:
+            host_acc.copy_(acc, non_blocking=True)
 
     def step():
         with torch.cuda.stream(stream):
             acc.zero_()
             scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
             reduce_accum(acc, dist)
+            to_host()
 
     # work counters for the roofline's algorithmic bytes (separate pass, not timed)
     cnt = torch.zeros(6, dtype=torch.int64, device=dev)
@@ -339,6 +349,7 @@ def main():
             scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
             ev1.record(stream)
             reduce_accum(acc, dist)
+            to_host()
     stream.synchronize()
     render_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
     if world > 1:
@@ -376,6 +387,11 @@ def main():
     else:  # --no-kernel-timing (diagnostic)
         kernel, launches_per_render, k_ms, busy_ms, bytes_per_launch, achieved = "n/a", 0, 0.0, 0.0, 0.0, 0.0
     pipeline = b_alg / (r_ms * 1e-3) / 1e9
+    # SURVEY.md §8d's secondary figure, the algorithmic VALU work, from the same counters (the
+    # reference's own units: every triangle test and node step its traversal makes, and the path
+    # logic per bounce): 40 flop per triangle test + 2 x 24 per node step + 150 per extension query
+    flop_per_render = 40.0 * c[4] + 48.0 * c[3] + 150.0 * q_ext
+    valu_tflops = flop_per_render / max(samples_c, 1) * value * 1e6 / 1e12  # at the step's samples/s
 
     if rank == 0:
         prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<",)}
@@ -409,6 +425,8 @@ def main():
                                                                          f", {backend} sum-reduce through host memory (rehearsal)")
                                                                         if world > 1 else ""),
                        "mode": args.mode, "bvh": args.bvh, "samples_per_step": total_samples,
+                       "timed_to": "accumulator on the host (rank 0: pinned device-to-host copy after the "
+                                   "reduce, inside each timed step)",
                        "ranks": ranks_seen, "backend": backend if world > 1 else None,
                        "options": dict(kv.partition("=")[::2] for kv in args.opt) or None,
                        "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size),
@@ -434,6 +452,13 @@ def main():
                                          "HIP-event intervals on every part stream)",
                          "launches_per_step": launches_per_render, "bytes_per_launch": round(bytes_per_launch),
                          "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3),
+                         "valu_alg_frac": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
+                         "valu_alg": {"flop_per_sample": round(flop_per_render / max(samples_c, 1), 1),
+                                      "achieved": round(valu_tflops, 2), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                      "frac": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
+                                      "def": "(40 x triangle tests + 48 x node steps + 150 x extension queries) of "
+                                             "the reference's traversal, from the GPU's work counters (SURVEY.md 8d "
+                                             "secondary), per sample x samples/s of the step / the f32 vector peak"},
                          "pipeline": {"bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
                                       "achieved": round(pipeline, 2), "frac": round(pipeline / HBM_PEAK_GBS, 4)},
                          # not a utilisation (it can exceed 1): VALU wave-instructions priced at the

@@ -286,8 +286,11 @@ struct SahBuilder {
 // 12,500-triangle sweep scenes rendered black).  A leaf child of the root is tested whenever the
 // ray meets its box (intersection-logic.wgsl:47-176: no pruning for leaf children), so the
 // triangles of the flagged materials (the emitters, program-raymarch.wgsl:136's sum(Ke) > 0) go
-// into the root's left child — one leaf when they are at most kSahMaxLeaf, else their own SAH
-// subtree — and the rest of the scene into its right child.
+// into the root's left child as ONE leaf, however many they are, and the rest of the scene into its
+// right child.  (Round 4 gave more than kSahMaxLeaf emitters an SAH subtree of their own, whose
+// internal nodes the pruning can still skip: a finely meshed light could be hidden, advisor r04.
+// A big emitter leaf costs the rays that meet its box more tests; leaves of >= big_leaf entries
+// take the traversal's big-leaf path.)
 extern "C" int pt_bvh_build_sah2(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count,
                                  const uint8_t* isolate_material, size_t material_count, float* bvh_out,
                                  size_t bvh_cap, size_t* bvh_len) {
@@ -330,13 +333,9 @@ extern "C" int pt_bvh_build_sah2(const double* vertices, size_t vertex_count, co
         top.r = std::make_unique<BNode>();
         top.l->objs = std::move(lit);
         top.r->objs = std::move(rest);
-        if ((int)top.l->objs.size() <= kSahMaxLeaf) {  // one leaf under the root
-            top.l->leaf = true;
-            top.l->box = empty_box();
-            for (int32_t o : top.l->objs) grow(top.l->box, tb[o]);
-        } else {
-            sb.build(*top.l, 2);
-        }
+        top.l->leaf = true;  // one leaf under the root: never pruned
+        top.l->box = empty_box();
+        for (int32_t o : top.l->objs) grow(top.l->box, tb[o]);
         sb.build(*top.r, 2);
     } else {
         top.objs.resize(tri_count);

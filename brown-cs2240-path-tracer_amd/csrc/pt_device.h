@@ -462,6 +462,16 @@ __device__ __forceinline__ void big_turn(const SceneView& sc, const Ray& r, Trav
     }
 }
 
+// The per-wave LDS key slots (lean_leaf_pool, chunk_leaf_multi) are written by one lane, lowered by
+// other lanes' ds_min_u64 and read back by the first: a wave barrier plus a wavefront-scope fence
+// orders those accesses under the memory model too, not only by wave64 lockstep and in-order LDS
+// (advisor r04; neither emits an instruction on gfx950).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Cross-lane minima by DPP (gfx9 lane moves inside the VALU: no LDS round trip, unlike the
 // ds_bpermute a __shfl_xor becomes).  dpp_mov: lanes the move does not write keep `old`.
 template <int CTRL, int ROW_MASK>
@@ -642,6 +652,7 @@ __device__ __forceinline__ void chunk_leaf_multi(const SceneView& sc, const Ray&
     const bool served = ((same >> lane) & 1ull) != 0;
     const int slot = (int)__popcll(same & ((1ull << lane) - 1ull));  // this lane's slot, when served
     if (served) keys[slot] = kNoKey;
+    wave_lds_sync();
     // this lane's ray constants, read by the checks from the owner lane
     const float idl = 1.0f / sqrtf(dot(r.d, r.d));
     const float on = sqrtf(dot(r.o, r.o));
@@ -677,6 +688,7 @@ __device__ __forceinline__ void chunk_leaf_multi(const SceneView& sc, const Ray&
                       ((unsigned long long)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk);
         }
         filled = 0;
+        wave_lds_sync();
         if (served) {  // the next checks against each ray's best so far
             const uint64_t k = keys[slot];
             if (k != kNoKey) bnd = fminf(prior, __builtin_bit_cast(float, (uint32_t)(k >> 32)));
@@ -717,6 +729,7 @@ __device__ __forceinline__ void chunk_leaf_multi(const SceneView& sc, const Ray&
     }
     merge();
     if (filled) test_pairs();
+    wave_lds_sync();
     const uint64_t k = served ? keys[slot] : kNoKey;
     bt_out = __builtin_bit_cast(float, (uint32_t)(k >> 32));
     bk_out = k == kNoKey ? 0x7fffffff : (int)(uint32_t)k;
@@ -786,6 +799,7 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
     const int runs = (n + RUN - 1) / RUN;
     uint64_t* keys = sc.lkeys;
     keys[lane] = kNoKey;
+    wave_lds_sync();
     auto bpi = [](int v, int l) { return __builtin_amdgcn_ds_bpermute(l << 2, v); };
     auto bpf = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(l << 2, __builtin_bit_cast(int, v))); };
     int mine = 0;    // this lane's run: owner lane | run index << 6
@@ -807,7 +821,9 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
             if (pos < p1) {
                 const int rec = pos < na ? la + pos : lb + (pos - na);
                 float t;
-                if (tri_hit<FAST_RCP>(sc.tris, rec, q, t) & (t < bt)) { bt = t; bk = pos; }  // positions ascend: the first of equal t
+                // positions ascend: the first of equal t; a first hit is taken whatever its t (a t
+                // of +inf, reachable only through overflow, is a hit the reference keeps too)
+                if (tri_hit<FAST_RCP>(sc.tris, rec, q, t) & ((t < bt) | (bk == 0x7fffffff))) { bt = t; bk = pos; }
             }
         }
         if (bk != 0x7fffffff)
@@ -836,6 +852,7 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
     }
     merge();
     if (filled) test_runs();
+    wave_lds_sync();
     bool decide = false;
     if (in_leaf) {
         const uint64_t k = keys[lane];

@@ -179,7 +179,14 @@ __host__ __device__ constexpr uint32_t stage_bytes(uint32_t ring) { return kWinR
 // after the waves' stages, when the scene needs them (pooled leaf turns or leaf chunks: keys_on),
 // 64 keys per wave — one per lane for lean_leaf_pool, the first kMultiRays for chunk_turn_multi
 constexpr uint32_t kKeyBytes = 64 * 8;
-__host__ __device__ inline bool keys_on(const SceneView& sc) { return sc.leaf_pool != 0 || sc.lnodes != nullptr; }
+// Only the lean flavours pool leaf turns or walk chunks (trav_step_lean; not the mailboxed 1xx nor
+// the flattened 1 / 2), so only their instances reserve the keys (advisor r04: every instance did)
+template <int TRAV>
+__host__ __device__ constexpr bool lean_flavour() { return TRAV >= 3 && !(TRAV >= 100 && TRAV < 160) && TRAV < 300; }
+template <int TRAV>
+__host__ __device__ inline bool keys_on(const SceneView& sc) {
+    return lean_flavour<TRAV>() && (sc.leaf_pool != 0 || sc.lnodes != nullptr);
+}
 // the traversal flavours that have a 256-entry-ring instance (the defaults: lean16 + fast rcp, with
 // and without big-leaf turns); the others always use 128
 constexpr bool has_big_ring(int trav) { return trav == 17 || trav == 177; }
@@ -212,7 +219,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     int2* ring = reinterpret_cast<int2*>(stage + kWinRays * 32);   // [RING]
     uint32_t* wtab = reinterpret_cast<uint32_t*>(stage + kWinRays * 32 + RING * 8);  // [kWinTab] window ids
     char* key_base = stage_base + (blockDim.x / 64u) * stage_bytes(nring);
-    const uint32_t key_bytes = keys_on(sc) ? (blockDim.x / 64u) * kKeyBytes : 0u;
+    const uint32_t key_bytes = keys_on<TRAV>(sc) ? (blockDim.x / 64u) * kKeyBytes : 0u;
     sc.lkeys = key_bytes ? reinterpret_cast<uint64_t*>(key_base + (threadIdx.x / 64u) * kKeyBytes) : nullptr;
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip
@@ -873,7 +880,7 @@ template <bool LDS, int TRAV, bool COUNT>
 static size_t trace_lds(const SceneView& sc, uint32_t ring = kHitRing) {
     const size_t span = LDS ? sc.span_bytes : 0;
     if (TRAV >= 300) return (size_t)sc.max_stack * kTraceBlock * 4 + (kTraceBlock / 64) * ((size_t)kBfSlots * 64 * 4) + span;
-    return (size_t)sc.max_stack * 4 * kTraceBlock + (kTraceBlock / 64) * (stage_bytes(ring) + (keys_on(sc) ? kKeyBytes : 0)) + span;
+    return (size_t)sc.max_stack * 4 * kTraceBlock + (kTraceBlock / 64) * (stage_bytes(ring) + (keys_on<TRAV>(sc) ? kKeyBytes : 0)) + span;
 }
 // resident blocks of `kernel` per CU at `lds` bytes of dynamic LDS, times the CUs: the persistent
 // grid of the trace and step kernels (cached per kernel instance and LDS size)
@@ -932,7 +939,7 @@ template <bool LDS, int TRAV, bool COUNT>
 static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, const WfBuffers& wb, uint32_t frame0,
                               uint32_t nframes, uint32_t stride, bool accum, float* out, Counters* cnt,
                               hipStream_t stream, const WfStreams& ws) {
-    const SceneView sc = bf_view<TRAV, COUNT>(sc_in);
+    SceneView sc = bf_view<TRAV, COUNT>(sc_in);
     const uint32_t npix = fp.width * fp.height;
     // the batch in ws.nparts parts on as many streams when a part holds at least a frame: one
     // part's kernel fills the others' launch tails and boundaries (and, with separate trace and
@@ -944,6 +951,13 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     // CU (option trace_ring: 128 / 256 forces one)
     uint32_t nring = kHitRing;
     const bool run2 = sc.leaf_pool == 2;  // pooled runs of 2 (the has_variants instances)
+    // turn policy of the lean traversal: 4 since the queues are grouped by coherence keys (in process:
+    // Glossy +2.5 %, boat +1 %, 1M synthetic +1.8 % over 8; 1 = majority: -13 % in round 1); 1 for the
+    // instances that pool runs of 2 (100k +5.2 %, 1M +5.3 % over 4, both orders:
+    // profiles/r04ai_node_bias.log; with runs of 4 the bias is within noise, r04z_ab_node_bias.log).
+    // Chosen from the instance launched (advisor r04: the counted and non-default flavours pool runs
+    // of 4 whatever sc.leaf_pool says)
+    if (sc.node_bias <= 0) sc.node_bias = (run2 && has_variants<TRAV, COUNT>()) ? 1 : 4;
     if constexpr (has_variants<TRAV, COUNT>()) {
         const size_t l1 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRing), l2 = trace_lds<LDS, TRAV, COUNT>(sc, kHitRingMax);
         const bool fits = l2 <= max_block_lds() &&
@@ -1086,12 +1100,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
     if (!accum) { nframes = 1; stride = 1; }
-    SceneView sc = scene;
-    // turn policy of the lean16 traversal: 4 since the queues are grouped by coherence keys (in
-    // process: Glossy +2.5 %, boat +1 %, 1M synthetic +1.8 % over 8; 1 = majority: -13 % in round 1);
-    // 1 where the leaf turns pool runs of 2 (100k +5.2 %, 1M +5.3 % over 4, both orders:
-    // profiles/r04ai_node_bias.log; with runs of 4 the bias is within noise, r04z_ab_node_bias.log)
-    if (sc.node_bias <= 0) sc.node_bias = sc.leaf_pool == 2 ? 1 : 4;
+    SceneView sc = scene;  // node_bias <= 0: chosen per instance in wf_render_t
     const bool lds = lo.lds && scene_fits_lds(sc);
     // lean16 with the fast reciprocal by default (measured best on gfx950, scripts/perf_variants.py);
     // the wavefront always uses a flattened traversal; lean flavours take the fast reciprocal

@@ -225,10 +225,11 @@ int pt_bvh_build_sah(const double* vertices, size_t vertex_count, const int32_t*
                      size_t bvh_cap, size_t* bvh_len);
 
 /* pt_bvh_build_sah with the triangles of flagged materials (isolate_material[m] != 0 for material
- * id m < material_count; hosts flag the emitters, sum(Ke) > 0) in the root's left child — one leaf
- * of at most 8 entries, which the traversal tests whenever a ray meets its box, so the
- * exit-distance pruning of intersection-logic.wgsl:178-181 cannot hide the lights — and the rest
- * of the scene in its right child.  material_count = 0: exactly pt_bvh_build_sah. */
+ * id m < material_count; hosts flag the emitters, sum(Ke) > 0) in the root's left child — ONE leaf
+ * however many they are, which the traversal tests whenever a ray meets its box (leaf children are
+ * never pruned), so the exit-distance pruning of intersection-logic.wgsl:178-181 cannot hide the
+ * lights — and the rest of the scene in its right child.  material_count = 0: exactly
+ * pt_bvh_build_sah. */
 int pt_bvh_build_sah2(const double* vertices, size_t vertex_count, const int32_t* tris, size_t tri_count,
                       const uint8_t* isolate_material, size_t material_count, float* bvh_out, size_t bvh_cap,
                       size_t* bvh_len);

@@ -14,7 +14,29 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "libpt_oracle.so")
+_LIB_V4_PATH = os.path.join(_HERE, "_build", "libpt_oracle_v4.so")
+FLAGS = {_LIB_PATH: "-O3 -march=x86-64-v3 -ffp-contract=off", _LIB_V4_PATH: "-O3 -march=x86-64-v4 -ffp-contract=off"}
 _lib = None
+_lib_path = None
+
+
+def _has_avx512() -> bool:
+    """x86-64-v4's AVX-512 subsets (F, BW, CD, DQ, VL) on this host's CPU."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    fl = set(line.split(":", 1)[1].split())
+                    return {"avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"} <= fl
+    except OSError:
+        pass
+    return False
+
+
+def lib_flags() -> str:
+    """Compiler flags of the oracle build lib() loaded (bench.py's cpu_baseline reports them)."""
+    lib()
+    return FLAGS[_lib_path]
 
 
 class Counters(ctypes.Structure):
@@ -30,11 +52,12 @@ def build():
 
 
 def lib():
-    global _lib
+    global _lib, _lib_path
     if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+        if not os.path.exists(_LIB_PATH) or not os.path.exists(_LIB_V4_PATH):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
+        _lib_path = _LIB_V4_PATH if _has_avx512() and os.environ.get("PT_ORACLE_V3") != "1" else _LIB_PATH
+        L = ctypes.CDLL(_lib_path)
         f, u32, i32, p = ctypes.c_float, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
         for n in ("po_sinf", "po_cosf", "po_tanf", "po_acosf", "po_log2f", "po_exp2f"):
             getattr(L, n).restype = f; getattr(L, n).argtypes = [f]

@@ -302,7 +302,15 @@ static inline v3 vert(const scene_t *s, int32_t v_start, int32_t i) {
     return V3(P(s, v_start + i), P(s, v_start + i + 1), P(s, v_start + i + 2));
 }
 
+/* diagnostic hooks (scripts/leaf_visit_stats.c defines them; empty in the oracle build) */
+#ifndef PO_LEAF_HOOK
+#define PO_LEAF_HOOK(s, ray, lp)
+#endif
+#ifndef PO_INTERSECT_HOOK
+#define PO_INTERSECT_HOOK(s, ray, closest_t)
+#endif
 static void test_leaf(const scene_t *s, const ray_t *ray, int32_t lp, isect_t *closest, float *closest_t, po_counters *c) {
+    PO_LEAF_HOOK(s, ray, lp);
     float num_triangles = B(s, lp + 4);
     int32_t o_start = lp + 5 + 12;
     int32_t o_end = o_start + (int32_t)num_triangles;
@@ -364,6 +372,7 @@ static isect_t intersect(const scene_t *s, const ray_t *ray, po_counters *c) {
             else { stack[SI(sp + 1)] = (int32_t)B(s, ptr + 2); sp += 2; stack[SI(sp)] = (int32_t)B(s, ptr + 3); }
         }
     }
+    PO_INTERSECT_HOOK(s, ray, closest_t);
     return closest;
 }
 

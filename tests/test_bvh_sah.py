@@ -6,7 +6,8 @@ straddle a split; this builder puts each in one leaf), but it must still be a va
 reference's packed layout (src/packer.ts:83-137) for the unchanged traversal
 (src/wgsl-util/intersection-logic.wgsl:1-215) to find every closest hit the oracle finds:
   * every input triangle record (i0, i1, i2, material) in exactly one leaf;
-  * leaves of at most kSahMaxLeaf = 8 entries, except at the depth cap (kSahMaxDepth = 28, root 1);
+  * leaves of at most kSahMaxLeaf = 8 entries, except at the depth cap (kSahMaxDepth = 28, root 1)
+    and the emitter leaf of pt_bvh_build_sah2 (all flagged triangles in one leaf under the root);
   * every child box (the parent's [o+5..10] / [o+11..16]) contains the f32 vertices of every
     triangle below that child, and the outer bounds [0..5] contain all of them;
   * every non-empty child box has a positive extent on every axis (ray-bbox-intersection.wgsl's
@@ -61,16 +62,17 @@ def walk_packed(bvh):
     return leaves, inner
 
 
-def check_sah(verts64, recs, bvh):
+def check_sah(verts64, recs, bvh, emitter_leaf=False):
     leaves, inner = walk_packed(bvh)
+    first_leaf_free = emitter_leaf and bvh[int(bvh[6 + 2])] == 1.0  # the root's left child, a leaf
     v32 = verts64.astype(np.float32)
     got = np.concatenate([e for e, _, _, _ in leaves])
     # every triangle record in exactly one leaf
     key = lambda a: np.sort(a.view([("", a.dtype)] * 4).reshape(-1))  # noqa: E731
     assert got.shape == recs.shape
     assert np.array_equal(key(np.ascontiguousarray(got)), key(np.ascontiguousarray(recs.astype(np.int64))))
-    for e, lo, hi, depth in leaves:
-        assert len(e) <= K_MAX_LEAF or depth >= K_MAX_DEPTH, (len(e), depth)
+    for i, (e, lo, hi, depth) in enumerate(leaves):
+        assert len(e) <= K_MAX_LEAF or depth >= K_MAX_DEPTH or (i == 0 and first_leaf_free), (len(e), depth)
         if len(e):
             p = v32[e[:, :3].reshape(-1) - 1]
             assert np.all(p >= lo) and np.all(p <= hi), "a leaf's box must contain its triangles"
@@ -113,13 +115,14 @@ def emitter_flags(xml_path, assets):
 
 
 def check_isolated(verts, recs, flags):
-    """pt_bvh_build_sah2: the emitters' triangles in the root's left child — one leaf when they are
-    at most 8 — the rest on the right; still a valid SAH tree over all triangles."""
+    """pt_bvh_build_sah2: the emitters' triangles in the root's left child as ONE leaf however many
+    they are (a leaf child of the root is never pruned, intersection-logic.wgsl:47-176), the rest on
+    the right; still a valid SAH tree over all triangles."""
     bvh = pt_amd.bvh_build(verts, recs, sah=True, isolate=flags)
-    check_sah(verts, recs, bvh)
+    check_sah(verts, recs, bvh, emitter_leaf=True)
     lit = recs[flags[recs[:, 3]] != 0]
     left = int(bvh[6 + 2])
-    if 0 < len(lit) <= K_MAX_LEAF:
+    if 0 < len(lit) < len(recs):
         assert bvh[left] == 1.0, "the emitters form one leaf under the root"
         got = bvh[left + 17: left + 17 + int(bvh[left + 4])].reshape(-1, 4).astype(np.int64)
         assert sorted(map(tuple, got)) == sorted(map(tuple, lit.astype(np.int64)))
@@ -145,6 +148,28 @@ def test_sah_emitters_under_the_root_synthetic(n, tmp_path):
     assets = os.path.join(str(tmp_path), "scene_assets")
     verts, recs = scene_inputs(xml, assets)
     check_isolated(verts, recs, emitter_flags(xml, assets))
+
+
+def test_sah_many_emitters_one_leaf():
+    """A finely meshed area light (a quad split into 2 x 12 x 12 = 288 emissive triangles) above a
+    floor of 200 triangles: all 288 in the one leaf under the root (advisor r04: round 4 built them
+    an SAH subtree, whose internal nodes the exit-distance pruning can skip)."""
+    g = 12
+    xs = np.linspace(-0.25, 0.25, g + 1)
+    lv = np.array([[x, 1.98, z] for z in xs for x in xs], np.float64)
+    idx = lambda i, j: i * (g + 1) + j + 1  # noqa: E731
+    light = [[idx(i, j), idx(i, j + 1), idx(i + 1, j), 1] for i in range(g) for j in range(g)]
+    light += [[idx(i, j + 1), idx(i + 1, j + 1), idx(i + 1, j), 1] for i in range(g) for j in range(g)]
+    rng = np.random.default_rng(3)
+    fl = rng.uniform(-1, 1, (200, 3, 3)) * [1, 0.01, 1]
+    verts = np.concatenate([lv, fl.reshape(-1, 3)])
+    base = len(lv)
+    floor = [[base + 3 * k + 1, base + 3 * k + 2, base + 3 * k + 3, 0] for k in range(200)]
+    recs = np.array(light + floor, np.int32)
+    flags = np.array([0, 1], np.uint8)
+    bvh = check_isolated(verts, recs, flags)
+    left = int(bvh[6 + 2])
+    assert int(bvh[left + 4]) // 4 == 288
 
 
 def test_node_sah_pack_isolates_emitters(tmp_path):

@@ -50,12 +50,12 @@ def sah_packed(tmp_path_factory):
 def synth_packed(tmp_path_factory):
     cache = {}
 
-    def get(n, bvh="reference"):
-        if (n, bvh) not in cache:
+    def get(n, bvh="reference", light_grid=1):
+        if (n, bvh, light_grid) not in cache:
             root = tmp_path_factory.mktemp(f"synth{n}")
-            xml = synth_scene.write(n, str(root))
-            cache[(n, bvh)] = pack_with_node(xml, str(root / "packed"), "--native-bvh", "--bvh", bvh)
-        return cache[(n, bvh)]
+            xml = synth_scene.write(n, str(root), light_grid)
+            cache[(n, bvh, light_grid)] = pack_with_node(xml, str(root / "packed"), "--native-bvh", "--bvh", bvh)
+        return cache[(n, bvh, light_grid)]
     return get
 
 
@@ -101,4 +101,18 @@ def test_synthetic_1m_band_bitexact(synth_packed):
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         assert s.info["nodes"] <= 32767 and s.info["max_stack"] <= 17  # bvh.ts's depth cap of 16
     _, profs = _render_bands(p, 1024, 1024, 2, 8, [(256, 272)])
+    _trace_kernel_ran(profs)
+
+
+@pytest.mark.parametrize("bvh", ["sah", "reference"])
+def test_many_emitters_rows_bitexact(synth_packed, bvh):
+    """A finely meshed light (synth_scene LIGHT_GRID 12: 288 emissive triangles) over the 1,000-triangle
+    synthetic scene: on the fast tree all 288 sit in ONE leaf under the root, which the pruning never
+    skips (advisor r04: round 4 gave them an SAH subtree), and the bands through the light and the box
+    must see it, bit-exact against the oracle on both trees."""
+    p = synth_packed(1000, bvh, 12)
+    if bvh == "sah":
+        left = int(p.bvh_data[6 + 2])
+        assert p.bvh_data[left] == 1.0 and int(p.bvh_data[left + 4]) // 4 == 288
+    _, profs = _render_bands(p, 1024, 1024, 4, 8, SYNTH_BANDS)
     _trace_kernel_ran(profs)
