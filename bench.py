@@ -374,7 +374,9 @@ def main():
         launches_per_render = prof[kernel]["launches"] / args.steps
         k_ms = prof[kernel]["avg_ms"]
         busy_ms = prof[kernel]["busy_ms"] / args.steps  # union of the launches' intervals, per step
-        if kernel == "k_wf_trace":
+        if kernel in ("k_wf_trace", "k_wf_leafpass"):
+            # the traversal's model: a ray record read and a hit record written per query (the big-leaf
+            # pass reads the same records and writes a key per query that meets a big leaf's boxes)
             bytes_per_launch = 48.0 * (q_ext + q_sh) / launches_per_render
         elif kernel == "k_wf_step":  # fused trace + shade: the path model minus camera rays and accumulation
             bytes_per_launch = (48.0 * (q_ext + q_sh) + 96.0 * q_ext) / launches_per_render
@@ -394,7 +396,8 @@ def main():
     valu_tflops = flop_per_render / max(samples_c, 1) * value * 1e6 / 1e12  # at the step's samples/s
 
     if rank == 0:
-        prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<",)}
+        prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<",),
+                    "k_wf_leafpass": ("k_wf_leafpass<",)}
         pre = prefixes.get(kernel, (kernel + "<",))
         # the committed PMC / trace figures describe the full configuration (not a rank's share)
         full = args.share_of <= 1

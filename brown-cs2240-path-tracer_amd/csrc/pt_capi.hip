@@ -75,6 +75,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
+    {"leaf_pre", OPT_BOOL, nullptr},     {"leaf_blocks", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
     {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},   {"pool_run", OPT_ENUM, "2|4"},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
@@ -148,6 +149,8 @@ struct HostLayout {
     std::vector<Tri> ltris;       // per chunk slot: its entry's record, lbvh = the entry's position in its leaf
     std::vector<std::array<int32_t, 3>> lleaves;
     int32_t leaf_min = 0;         // leaves of at least this many entries have one (option leaf_bvh; 0: none)
+    std::vector<PreLeaf> pre;     // the kMaxPre largest leaves with their paths (SceneView::pre), largest first
+    std::vector<int32_t> leaf_sizes;  // every non-empty leaf's entries, largest first
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -358,6 +361,43 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             if (L.lleaves.empty()) L.leaf_min = 0;
         }
     }
+    // Leaves that k_wf_leafpass can resolve before the traversal: the kMaxPre largest, each with its
+    // path of child boxes from the root (node << 1 | side per step; PreLeaf)
+    {
+        std::vector<PreLeaf> all;
+        // iterative pre-order walk keeping the path: (node, depth) frames, path[depth] = the step in
+        std::vector<std::pair<int32_t, std::vector<int32_t>>> st;
+        st.push_back({0, {}});
+        bool deep = false;
+        while (!st.empty()) {
+            auto fr = std::move(st.back());
+            st.pop_back();
+            const Node& nd = L.nodes[(size_t)fr.first];
+            for (int side = 1; side >= 0; --side) {
+                const int32_t cnt = side ? nd.rcnt : nd.lcnt, ref = side ? nd.rref : nd.lref;
+                std::vector<int32_t> p2 = fr.second;
+                p2.push_back(fr.first << 1 | side);
+                if (cnt >= 0) {
+                    if (cnt == 0) continue;
+                    L.leaf_sizes.push_back(cnt);
+                    if ((int)p2.size() > kMaxPrePath) { deep = true; continue; }
+                    PreLeaf pl{};
+                    pl.rec0 = ref;
+                    pl.n = cnt;
+                    pl.npath = (int32_t)p2.size();
+                    for (size_t k = 0; k < p2.size(); ++k) pl.path[k] = p2[k];
+                    all.push_back(pl);
+                } else if (ref >= 0 && (size_t)ref < L.nodes.size()) {
+                    st.push_back({ref, std::move(p2)});
+                }
+            }
+        }
+        std::sort(L.leaf_sizes.begin(), L.leaf_sizes.end(), std::greater<int32_t>());
+        std::sort(all.begin(), all.end(), [](const PreLeaf& a, const PreLeaf& b) { return a.n > b.n || (a.n == b.n && a.rec0 < b.rec0); });
+        if (!deep) {  // (a leaf below kMaxPrePath steps could be among the largest: no table then)
+            for (size_t k = 0; k < all.size() && k < (size_t)kMaxPre; ++k) L.pre.push_back(all[k]);
+        }
+    }
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
     // a reflection/refraction of unit vectors; non-finite ones give no hit on either path)
     double emax = 0.0;
@@ -470,6 +510,13 @@ struct pt_scene {
     size_t peer_cap = 0;
     int32_t leaf_min = 0;  // leaf BVHs: leaves of at least this many entries have one (0: none)
     std::vector<std::array<int32_t, 3>> lleaves;  // (first record, entries, nodes) per leaf BVH
+    // big leaves resolved before the traversal (k_wf_leafpass): the table (device copy in d_mem at
+    // d_pre), every leaf's size (largest first), and the result keys (ensure_pres)
+    std::vector<PreLeaf> pre;
+    std::vector<int32_t> leaf_sizes;
+    const PreLeaf* d_pre = nullptr;
+    uint64_t* d_pres = nullptr;
+    size_t pres_cap = 0;  // keys
 };
 
 // Set once any call of this library has touched the HIP runtime (pt_set_hw_queues is then too late).
@@ -622,7 +669,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
     const size_t o_lnode = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
-    const size_t total = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
+    const size_t o_pre = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
+    const size_t total = align_up(o_pre + std::max<size_t>(1, L.pre.size()) * sizeof(PreLeaf), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -637,7 +685,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_bfmap, L.bfmap.data(), L.bfmap.size() * sizeof(int32_t)) != hipSuccess ||
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
-        up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess) {
+        up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess ||
+        up(o_pre, L.pre.data(), L.pre.size() * sizeof(PreLeaf)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -666,6 +715,9 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.ltris = L.lnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_lidx);
     s->leaf_min = L.leaf_min;
     s->lleaves = L.lleaves;
+    s->pre = L.pre;
+    s->leaf_sizes = L.leaf_sizes;
+    s->d_pre = L.pre.empty() ? nullptr : reinterpret_cast<const PreLeaf*>(base + o_pre);
     s->view.mb_base = L.mb_base;
     s->view.bfnode = L.bfnode.empty() ? nullptr : reinterpret_cast<const BfNode*>(base + o_bfnode);
     s->view.bfmap = L.bfmap.empty() ? nullptr : reinterpret_cast<const int32_t*>(base + o_bfmap);
@@ -691,6 +743,7 @@ void pt_scene_destroy(pt_scene* s) {
     }
     if (s->ws.fork) hipEventDestroy(s->ws.fork);
     if (s->d_rad) hipFree(s->d_rad);
+    if (s->d_pres) hipFree(s->d_pres);
     if (s->d_peer) hipFree(s->d_peer);
     if (s->d_rgba) hipFree(s->d_rgba);
     if (s->h_ctl) hipHostFree(s->h_ctl);
@@ -780,6 +833,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);
+    lo.leaf_blocks = (int)o.num("leaf_blocks", 0);
     if (o.has("trav")) {
         static const char* const names[] = {"nested", "flat1", "pred", "lean", "lean2", "lean4", "lean8", "lean16", "lean32"};
         for (int k = 0; k < 9; ++k)
@@ -807,6 +861,22 @@ int ensure_rad(pt_scene* s, uint64_t paths) {
     s->rad_cap = paths;
     s->wf.rad = s->d_rad;
     s->wf.rad_cap = paths;
+    return PT_OK;
+}
+
+// keys of the pre-resolved big leaves: npre per queue entry of the wavefront buffers
+int ensure_pres(pt_scene* s, int npre) {
+    const size_t need = (size_t)npre * s->wf.qcap;
+    if (s->d_pres && s->pres_cap >= need) { s->wf.pres = s->d_pres; s->wf.pres_stride = s->wf.qcap; return PT_OK; }
+    if (s->d_pres) { hipDeviceSynchronize(); hipFree(s->d_pres); s->d_pres = nullptr; s->pres_cap = 0; }
+    if (hipMalloc(&s->d_pres, need * sizeof(uint64_t)) != hipSuccess) {
+        s->d_pres = nullptr;
+        (void)hipGetLastError();
+        return fail(PT_ERR_NOMEM, "hipMalloc pre-resolved leaf keys");
+    }
+    s->pres_cap = need;
+    s->wf.pres = s->d_pres;
+    s->wf.pres_stride = s->wf.qcap;
     return PT_OK;
 }
 
@@ -943,6 +1013,23 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);
+    // big leaves resolved before the traversal (k_wf_leafpass, pt_leafpass.hip; option leaf_pre=0:
+    // the cooperative turns and chunk walks inside k_wf_trace): the leaves of >= big_leaf entries, at
+    // most kMaxPre of them — with more, the threshold rises above the (kMaxPre + 1)-th largest and
+    // the rest are ordinary leaves of the pooled turns
+    view.npre = 0;
+    view.pre = nullptr;
+    if (lo.wavefront && view.big_leaf > 0 && o.flag("leaf_pre", 1) != 0 && !s->pre.empty()) {
+        int32_t T = view.big_leaf;
+        if (s->leaf_sizes.size() > (size_t)kMaxPre && s->leaf_sizes[kMaxPre] >= T) T = s->leaf_sizes[kMaxPre] + 1;
+        int np = 0;
+        while (np < (int)s->pre.size() && s->pre[(size_t)np].n >= T) ++np;
+        if (np > 0) {
+            view.big_leaf = T;
+            view.npre = np;
+            view.pre = s->d_pre;
+        }
+    }
     if ((rc = take_watchdog(s)) != PT_OK) return rc;  // an earlier asynchronous render failed
     if (lo.wavefront) {
         // the target in whole pairs of frames (a batch's two parts take whole frames each): 4096^2
@@ -967,6 +1054,11 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         if (rc2 != PT_OK) return rc2;
         rc2 = ensure_rad(s, s->wf.capacity);
         if (rc2 != PT_OK) return rc2;
+        if (view.npre > 0) {
+            if ((rc2 = ensure_pres(s, view.npre)) != PT_OK) return rc2;
+        } else {
+            s->wf.pres = nullptr;
+        }
         HIP_TRY(launch_wavefront(lo, view, fp, s->wf, frame0, nframes, stride, accum, d_cnt != nullptr, d_out, d_cnt,
                                  stream, s->ws));
         HIP_TRY(hipMemcpyAsync(s->h_ctl, s->wf.ctl, 4 * kMaxParts * WF_CTL_WORDS, hipMemcpyDeviceToHost, stream));

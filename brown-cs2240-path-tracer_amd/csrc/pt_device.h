@@ -298,9 +298,10 @@ struct TravLean {
     int node, sp, k, na, nt, la, lb, fl, best;
     float ld, rd, best_t;
     uint64_t tested, rem;  // mailbox flavours only: uids tested by this query / left in this pair
+    uint32_t qi;           // pre-resolved big leaves only: the query's queue entry (SceneView::pres)
 };
 __device__ __forceinline__ void trav_init(TravLean& s, bool active) {
-    s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1;
+    s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1; s.qi = 0;
     s.fl = active ? 0 : TF_DONE;
     s.ld = 0.0f; s.rd = 0.0f; s.best_t = -1.0f;
     s.tested = 0; s.rem = 0;
@@ -764,6 +765,37 @@ __device__ __forceinline__ void chunk_turn_multi(const SceneView& sc, const Ray&
     }
 }
 
+// Big leaves resolved before the traversal (k_wf_leafpass, pt_leafpass.hip): the parked lanes
+// — every one, whatever its leaf — take their leaf's precomputed key, the smallest (t, position)
+// over ALL the leaf's entries that report a hit (~0: none), and apply it as the reference's
+// strict-< loop over the leaf ends: that loop, started at the closest t so far, keeps the first
+// entry of the smallest t when that t is below it, and nothing otherwise — which needs no test of
+// the leaf here (the same argument as the cooperative turns; intersection-logic.wgsl:47-176).
+template <bool COUNT, class ST>
+__device__ __forceinline__ void pre_turn(const SceneView& sc, TravLean& s, uint64_t parked, const ST& stack, Counters& cnt) {
+    const int lane = (int)(threadIdx.x & 63u);
+    if ((parked >> lane) & 1ull) {
+        int rec0 = 0, n = 0;
+        big_seg(s, rec0, n);
+        int b = 0;  // the slot of this lane's leaf: the leaves >= big_leaf are exactly sc.pre[0, npre)
+        for (int j = 1; j < sc.npre; ++j) b = sc.pre[j].rec0 == rec0 ? j : b;
+        const uint64_t key = sc.pres[(size_t)b * sc.pres_stride + s.qi];
+        const float bt = __builtin_bit_cast(float, (uint32_t)(key >> 32));
+        const bool take = (key != ~0ull) & ((s.best_t < 0.0f) | (bt < s.best_t));
+        s.best_t = take ? bt : s.best_t;
+        s.best = take ? rec0 + (int)(uint32_t)key : s.best;
+        if (COUNT) cnt.tri_tests += n;
+        s.k += n;
+        s.fl &= ~TF_PARK;
+        if (s.k == s.nt) {
+            s.fl &= ~TF_LEAF;
+            lean_decide(s, stack);
+        } else if (big_at(sc, s)) {
+            s.fl |= TF_PARK;  // its right leaf is big too
+        }
+    }
+}
+
 // A leaf turn with the pair's remaining entries pooled over the whole wave (the wavefront
 // traversal kernel, every lane running).  lean_leaf_loop has each leaf lane test its own pair K
 // entries per turn while the lanes in node state — and those whose pair ends sooner — idle: lane
@@ -873,11 +905,19 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
 // Each iteration runs ONE unit type for the whole wave — a leaf turn (up to K triangle tests)
 // when leaf lanes >= node_bias * node lanes, else a node turn — keeping each lane's unit order.
 // PRUN: the pooled leaf turns' run length (lean_leaf_pool)
-template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, int PRUN = 4, class ST>
+// PRE: the big leaves were resolved before the traversal (pre_turn; TRAV 26x / 27x)
+template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, int PRUN = 4, bool PRE = false,
+          class ST>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, const ST& stack,
                                                Counters& cnt) {
     const int state = s.fl & (TF_LEAF | TF_DONE | (BIG ? TF_PARK : 0));
-    if constexpr (BIG) {  // a parked lane's big leaf goes first: the wave tests it for that ray
+    if constexpr (BIG && PRE) {  // parked lanes take their leaves' precomputed results
+        const uint64_t parked = __ballot((state & TF_PARK) != 0);
+        if (parked) {  // wave-uniform
+            pre_turn<COUNT>(sc, s, parked, stack, cnt);
+            return true;
+        }
+    } else if constexpr (BIG) {  // a parked lane's big leaf goes first: the wave tests it for that ray
         const uint64_t parked = __ballot((state & TF_PARK) != 0);
         if (parked) {  // wave-uniform
             int my0 = 0, myn = 0;  // the first parked lane's leaf (the other lanes' fields may not be a leaf's)
@@ -992,7 +1032,8 @@ __device__ __forceinline__ bool trav_step_mb(const SceneView& sc, const Ray& r, 
 // Traversal flavours (LaunchOpts.trav): 0 nested loops (trace), 1 flattened with per-lane
 // branches (trav_step), 2 flattened and predicated (trav_step_pred), 3 lean (trav_step_lean),
 // 4 lean with two triangle tests per leaf turn, 5 with four, 6 with eight, 7 with sixteen; +10: the lean
-// flavours with 1/det from rcp_rn (scenes with SceneView::fast_rcp); +100: mailboxed lean flavours.
+// flavours with 1/det from rcp_rn (scenes with SceneView::fast_rcp); +100: mailboxed lean flavours;
+// +160: big leaves (cooperative turns / chunk walks); +260: big leaves resolved before the traversal.
 template <int TRAV, bool LEAN = (TRAV >= 3)>
 struct TravSel { using type = TravState; };
 template <int TRAV>
@@ -1007,10 +1048,11 @@ __device__ __forceinline__ bool trav_advance(const SceneView& sc, const Ray& r, 
         constexpr int K = 1 << (TRAV % 10 - 3);
         return trav_step_mb<K, COUNT, ((TRAV / 10) & 1) != 0>(sc, r, s, stack, cnt);
     }
-    else if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 160: big-leaf cooperation
+    else if constexpr (TRAV >= 3) {  // TRAV + 10: fast reciprocal; + 160: big-leaf cooperation; + 260: pre-resolved
         constexpr int B = TRAV % 10;
         constexpr int K = 1 << (B - 3);  // lean, lean2, lean4, lean8, lean16, lean32
-        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, TRAV >= 160, CHUNKS, PRUN>(sc, r, s, stack, cnt);
+        return trav_step_lean<K, COUNT, ((TRAV / 10) & 1) != 0, TRAV >= 160, CHUNKS, PRUN, (TRAV >= 260)>(sc, r, s, stack,
+                                                                                                           cnt);
     }
     else if constexpr (TRAV == 1) return trav_step<COUNT>(sc, r, s, stack, cnt);
     else return trav_step_pred<COUNT>(sc, r, s, stack, cnt);

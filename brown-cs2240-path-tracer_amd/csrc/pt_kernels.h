@@ -18,12 +18,12 @@ namespace pt {
 // calling thread, every launch is bracketed by two HIP events on its stream.
 enum KernelId : int {
     KID_MEGA = 0, KID_REGEN, KID_WF_GENERATE, KID_WF_TRACE, KID_WF_SHADE_EXT, KID_WF_SHADE_SHADOW, KID_WF_ACCUM,
-    KID_TONEMAP, KID_WF_STEP, KID_COUNT
+    KID_TONEMAP, KID_WF_STEP, KID_WF_LEAF, KID_COUNT
 };
 inline const char* kernel_name(int k) {
     static const char* const n[KID_COUNT] = {"k_mega",         "k_regen",           "k_wf_generate", "k_wf_trace",
                                              "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum",    "k_tonemap",
-                                             "k_wf_step"};
+                                             "k_wf_step",      "k_wf_leafpass"};
     return (k >= 0 && k < KID_COUNT) ? n[k] : "?";
 }
 struct KernelProfiler {
@@ -72,6 +72,7 @@ struct LaunchOpts {
     int region_perm = -1;  // k_wf_step_bf: camera batches dealt to regions by a permutation (WfBuffers::rq); -1 default
     int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
+    int leaf_blocks = 0;   // k_wf_leafpass grid (A/B): 0 = occupancy-derived
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -114,6 +115,11 @@ struct WfBuffers {
     // batches)
     uint32_t rq, rqi;
     uint64_t rad_cap;   // paths whose radiance `rad` holds (>= capacity)
+    // big leaves resolved before the traversal (k_wf_leafpass): per leaf b and queue entry i the
+    // key (f32 bits of t << 32 | position; ~0: no hit) at pres[b * pres_stride + i] (pres_stride = the
+    // whole buffer's qcap: a part's pres is offset like its queues); nullptr when the scene has none
+    uint64_t* pres;
+    uint32_t pres_stride;
 };
 constexpr uint32_t kRegions = 512;
 // queue slack (entries per part = 64 * this): regions of R <= kRegions hold ceil(batches / R)
@@ -138,6 +144,7 @@ struct WfStreams {
     int trace_ring = 0;    // LaunchOpts::trace_ring
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
+    int leaf_blocks = 0;   // LaunchOpts::leaf_blocks
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
@@ -153,6 +160,11 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
 hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t* rgba, hipStream_t stream);
 // dst[i] += src[i] for i < n (f32; both on the stream's device; pt_image.hip)
 hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t stream);
+
+// k_wf_leafpass (pt_leafpass.hip): every big leaf of sc.pre resolved for the entries of queue in_q
+// whose rays enter its path's boxes, into wb.pres; blocks: the persistent grid (0: occupancy)
+hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks,
+                           hipStream_t stream);
 
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);

@@ -80,6 +80,17 @@ struct alignas(16) LNode {
 };
 static_assert(sizeof(LNode) == 64, "leaf BVH node is 4 x 16 B");
 
+// A big leaf resolved before the traversal (pt_leafpass.hip, k_wf_leafpass): its records, and the
+// path from the root to it as (node << 1 | side) per step — the child boxes every visit of the leaf
+// must enter (ray_box > 0: a leaf child is tested whenever its parent is visited and its box is hit,
+// intersection-logic.wgsl:47-176, and a node is visited only if each box on its path was entered).
+constexpr int kMaxPre = 8;        // big leaves resolved per scene (the largest ones)
+constexpr int kMaxPrePath = 40;   // > the deepest tree the builders make (reference 16 + 1, SAH 28 + 1)
+struct alignas(16) PreLeaf {
+    int32_t rec0, n, npath, pad;
+    int32_t path[kMaxPrePath];
+};
+
 struct alignas(16) Material {
     float Ns, Ni, illum, phong;  // phong = (Ns + 2) / (2 pi), f32, as program-raymarch.wgsl:271
     float Kd[3], kd_pi0;         // kd_pi* = Kd / pi per channel, f32 (program-raymarch.wgsl:165,279)
@@ -150,6 +161,14 @@ struct SceneView {
     // the traversal kernel's per-wave LDS keys (64: lean_leaf_pool's per-lane bests, the first
     // kMultiRays of them chunk_turn_multi's; set by k_wf_trace, nullptr in the other kernels)
     uint64_t* lkeys;
+    // big leaves resolved before the traversal (k_wf_leafpass; the wavefront's TRAV 26x/27x
+    // instances): the npre leaves of pre (device table, the largest first) are exactly the leaves of
+    // at least big_leaf entries; pres[b * pres_stride + i] is queue entry i's (t, position) key for
+    // leaf b (set by k_wf_trace from its part's WfBuffers; nullptr elsewhere)
+    const PreLeaf* pre;
+    int32_t npre;
+    uint32_t pres_stride;
+    const uint64_t* pres;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

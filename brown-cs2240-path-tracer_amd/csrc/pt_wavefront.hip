@@ -189,7 +189,7 @@ __host__ __device__ inline bool keys_on(const SceneView& sc) {
 }
 // the traversal flavours that have a 256-entry-ring instance (the defaults: lean16 + fast rcp, with
 // and without big-leaf turns); the others always use 128
-constexpr bool has_big_ring(int trav) { return trav == 17 || trav == 177; }
+constexpr bool has_big_ring(int trav) { return trav == 17 || trav == 177 || trav == 277; }
 constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scene
 // LDS of k_wf_trace per block: the lanes' traversal stacks (max_stack entries of 4 B) and per wave
 // stage_bytes(ring)
@@ -221,6 +221,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     char* key_base = stage_base + (blockDim.x / 64u) * stage_bytes(nring);
     const uint32_t key_bytes = keys_on<TRAV>(sc) ? (blockDim.x / 64u) * kKeyBytes : 0u;
     sc.lkeys = key_bytes ? reinterpret_cast<uint64_t*>(key_base + (threadIdx.x / 64u) * kKeyBytes) : nullptr;
+    sc.pres = wb.pres;  // this part's pre-resolved big leaves (TRAV 26x / 27x; k_wf_leafpass)
+    sc.pres_stride = wb.pres_stride;
     if (blockIdx.x == 0 && threadIdx.x == 0) wb.ctl[in_q ? WF_COUNT0 : WF_COUNT1] = 0;  // shade's output count
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];  // gave up: skip
     // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
@@ -241,6 +243,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     auto wcount = [&](uint32_t wid) { return min(wr, count - wid * wr); };
     const uint32_t w0 = fetch();
     if (w0 == kNone) return;  // wave-uniform: nothing for this wave
+    uint32_t wcur = w0, wnx = kNone;  // ids of window jl (handed out now) and of the one in flight
     // lanes 0..31 load the first halves of a window's ray records, lanes 32..63 the second
     const uint32_t wl = lane & (kWinRays - 1), half = lane / kWinRays;
     const float4* q = in_q ? wb.shd.ray : wb.ext.ray;
@@ -253,6 +256,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
     float4 na = make_float4(0, 0, 0, 0);
     {
         const uint32_t w1 = fetch();
+        wnx = w1;
         if (w1 != kNone) {
             nv = wcount(w1);
             if (lane == 0) wtab[1] = w1;
@@ -304,7 +308,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
                 wv = nv;
                 cur = jl * kWinRays;
                 nv = 0;
+                wcur = wnx;
                 const uint32_t wn = fetch();
+                wnx = wn;
                 if (wn != kNone) {
                     nv = wcount(wn);
                     if (lane == 0) wtab[(jl + 1) % kWinTab] = wn;
@@ -319,6 +325,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
                     r = unpack_ray(wray[2 * o], wray[2 * o + 1], p);
                     sq = k;
                     trav_init(s, true);
+                    if constexpr (TRAV >= 260 && TRAV < 300) s.qi = wcur * wr + o;  // its queue entry
                     has = true;
                 }
                 cur = min(cur + (uint32_t)__popcll(need), wend);
@@ -917,6 +924,7 @@ static WfBuffers wb_part(const WfBuffers& wb, int h, int nparts, size_t rad_off)
     const size_t e = (size_t)h * (wb.qcap / nparts);
     for (WfQueue* q : {&v.ext, &v.shd}) { q->ray += 2 * e; q->q2 += e; q->q3 += e; }
     v.sp0 += e; v.sp1 += e; v.sp2 += e; v.hitq += e;
+    if (v.pres) v.pres += e;  // per leaf b at b * pres_stride (the whole buffer's stride)
     v.rad += rad_off;
     v.ctl += h * WF_CTL_WORDS;
     v.rcnt += h * 3 * kRegions;
@@ -1044,6 +1052,8 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>), dim3(tblocks),
                           dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
             } else {
+                if constexpr (TRAV >= 260 && TRAV < 300)  // the big leaves first (k_wf_leafpass)
+                    HIP_RETURN_IF(launch_leafpass(sc, w, in_q, ((TRAV / 10) & 1) != 0, ws.leaf_blocks, st));
 #define PT_TRACE(RG, PR) PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, RG, PR>), dim3(tblocks), \
                                    dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, watchdog, sparse)
                 if constexpr (has_variants<TRAV, COUNT>()) {
@@ -1099,6 +1109,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.trace_ring = lo.trace_ring;
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
+    ws.leaf_blocks = lo.leaf_blocks;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;  // node_bias <= 0: chosen per instance in wf_render_t
     const bool lds = lo.lds && scene_fits_lds(sc);
@@ -1112,11 +1123,14 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     // brute force + replay (k_wf_trace_bf) by default for mailbox scenes; an explicit trav option
     // or bf=0 keeps the traversal kernels
     const bool bf = lo.bf != 0 && lo.mailbox != 0 && sc.mailbox && lo.trav < 0;
-    // big-leaf cooperation (+160) for lean<4..16> on scenes with leaves of >= big_leaf entries
+    // big-leaf cooperation (+160) for lean<4..16> on scenes with leaves of >= big_leaf entries; those
+    // leaves resolved before the traversal instead (+260, k_wf_leafpass) when the scene's table of
+    // pre-resolved leaves holds them (render_impl: option leaf_pre, default on) and the buffers exist
     const bool big = !bf && !mb && sc.big_leaf > 0 && base >= 5 && base <= 7;
+    const bool pre = big && sc.npre > 0 && sc.pre && wb.pres;
     const int trav = bf ? (lo.fuse == 0 ? 300 : 400) + (fast ? 10 : 0)
                    : mb ? 100 + base + (fast ? 10 : 0)
-                        : base + ((base >= 3 && fast) ? 10 : 0) + (big ? 160 : 0);
+                        : base + ((base >= 3 && fast) ? 10 : 0) + (big ? (pre ? 260 : 160) : 0);
 #define WF(L, T)                                                                                               \
     if (trav == T) {                                                                                           \
         if (count) return wf_render_t<L, T, true>(sc, fp, wb, frame0, nframes, stride, accum, out, cnt, stream, ws); \
@@ -1128,12 +1142,14 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
         WF(true, 300) WF(true, 310) WF(true, 400) WF(true, 410)
         WF(true, 105) WF(true, 106) WF(true, 107) WF(true, 115) WF(true, 116) WF(true, 117) WF(true, 118)
         WF(true, 165) WF(true, 166) WF(true, 167) WF(true, 175) WF(true, 176) WF(true, 177)
+        WF(true, 265) WF(true, 266) WF(true, 267) WF(true, 275) WF(true, 276) WF(true, 277)
     } else {
         WF(false, 1) WF(false, 2) WF(false, 3) WF(false, 4) WF(false, 5) WF(false, 6) WF(false, 7) WF(false, 8)
         WF(false, 13) WF(false, 14) WF(false, 15) WF(false, 16) WF(false, 17) WF(false, 18)
         WF(false, 300) WF(false, 310) WF(false, 400) WF(false, 410)
         WF(false, 105) WF(false, 106) WF(false, 107) WF(false, 115) WF(false, 116) WF(false, 117) WF(false, 118)
         WF(false, 165) WF(false, 166) WF(false, 167) WF(false, 175) WF(false, 176) WF(false, 177)
+        WF(false, 265) WF(false, 266) WF(false, 267) WF(false, 275) WF(false, 276) WF(false, 277)
     }
 #undef WF
     return hipErrorInvalidValue;

@@ -12,7 +12,7 @@ _LIB_FILE = os.path.join(_PKG_ROOT, "lib", "libpt_hip.so")
 ABI_VERSION = 3  # include/pt_hip.h PT_ABI_VERSION
 _CSRC = os.path.join(_PKG_ROOT, "csrc")
 # csrc/Makefile BUILD_SRCS: the sources whose SHA-256 the library carries as pt_build_id()
-_BUILD_SRCS = ["pt_kernels.hip", "pt_wavefront.hip", "pt_image.hip", "pt_capi.hip", "pt_math.h", "pt_layout.h",
+_BUILD_SRCS = ["pt_kernels.hip", "pt_wavefront.hip", "pt_leafpass.hip", "pt_image.hip", "pt_capi.hip", "pt_math.h", "pt_layout.h",
                "pt_device.h", "pt_path.h", "pt_kernels.h", "../../include/pt_hip.h", "pt_bvh.cpp", "pt_leafbvh.h",
                "pt_leafbvh.cpp", "Makefile"]
 MODE_AUTO, MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1, 2

@@ -76,10 +76,22 @@ def test_config3_1024_depth16_rows_bitexact(packed, scene):
     assert [p["k_wf_accum"]["launches"] for p in profs] == [1, 2], profs
 
 
-def test_config4_boat_1080p_depth16_rows_bitexact(packed):
-    _, profs = _render_bands(packed["MedievalBoat"], 1920, 1080, 5, 16, [(680, 696), (560, 568)])
+def test_config4_boat_1080p_depth16_rows_bitexact(packed, ptopts):
+    img, profs = _render_bands(packed["MedievalBoat"], 1920, 1080, 5, 16, [(680, 696), (560, 568)])
     assert all("k_wf_trace" in p for p in profs), profs
+    # the big leaves (7,327 entries and the next six) resolved before every traversal launch
+    assert all(p["k_wf_leafpass"]["launches"] == p["k_wf_trace"]["launches"] for p in profs), profs
     assert [p["k_wf_accum"]["launches"] for p in profs] == [1, 2], profs  # one batch / two batches
+    # the same image with the big leaves walked inside the traversal kernel (leaf_pre=0: cooperative
+    # turns and shared chunk walks), the whole image bit for bit
+    ptopts.set("leaf_pre", "0")
+    p = packed["MedievalBoat"]
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        img2 = s.render(p.meta_for(1920, 1080), 0, 5, 1, 16, pt_amd.MODE_AUTO)
+        prof = s.profile_read()
+    assert "k_wf_leafpass" not in prof, prof
+    assert_same_bits(img2, img, "leaf_pre=0 vs the default (big leaves resolved before the traversal)")
 
 
 def test_config5_image_4096_depth8_rows_bitexact(packed):

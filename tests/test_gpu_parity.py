@@ -111,6 +111,16 @@ KERNELS = {
     # the traversal kernel on one block with the big-leaf turns forced onto small leaves
     "wavefront_big4_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_MAILBOX": "0",
                               "PT_WF_TRACE_BLOCKS": "1"},
+    # big leaves resolved before the traversal (k_wf_leafpass; the default wherever the wavefront has
+    # big leaves: the variants above with big_leaf / leaf_bvh forced small run it on the 8 largest
+    # leaves of every scene): on one block (each wave's LDS rings wrap and flush partial batches), and
+    # off — the cooperative turns and chunk walks inside k_wf_trace
+    "wavefront_big8_leafpass_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0",
+                                       "PT_LEAF_BLOCKS": "1"},
+    "wavefront_big8_nopre": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0", "PT_LEAF_PRE": "0"},
+    "wavefront_leaf4_nopre": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PRE": "0"},
+    "wavefront_leaf2_div_nopre_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0",
+                                         "PT_FASTRCP": "0", "PT_LEAF_PRE": "0", "PT_WF_TRACE_BLOCKS": "1"},
 }
 
 
@@ -118,7 +128,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
             "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
-            "PT_POOL_RUN")
+            "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS")
 
 
 @pytest.fixture(params=list(KERNELS))
