@@ -1028,6 +1028,7 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
             view.big_leaf = T;
             view.npre = np;
             view.pre = s->d_pre;
+            for (int b = 0; b < kMaxPre; ++b) view.pre_rec0[b] = b < np ? s->pre[(size_t)b].rec0 : -1;
         }
     }
     if ((rc = take_watchdog(s)) != PT_OK) return rc;  // an earlier asynchronous render failed

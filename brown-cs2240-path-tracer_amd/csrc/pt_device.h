@@ -298,10 +298,11 @@ struct TravLean {
     int node, sp, k, na, nt, la, lb, fl, best;
     float ld, rd, best_t;
     uint64_t tested, rem;  // mailbox flavours only: uids tested by this query / left in this pair
-    uint32_t qi;           // pre-resolved big leaves only: the query's queue entry (SceneView::pres)
+    uint32_t qi;           // pre-resolved big leaves only: the query's queue entry (SceneView::pres) ...
+    uint64_t pkey;         // ... and the key of the first big leaf of its current leaf pair (pre_node_prefetch)
 };
 __device__ __forceinline__ void trav_init(TravLean& s, bool active) {
-    s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1; s.qi = 0;
+    s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1; s.qi = 0; s.pkey = ~0ull;
     s.fl = active ? 0 : TF_DONE;
     s.ld = 0.0f; s.rd = 0.0f; s.best_t = -1.0f;
     s.tested = 0; s.rem = 0;
@@ -313,7 +314,19 @@ __device__ __forceinline__ bool trav_finished(const TravState& s) { return s.don
 // runs two in sequence (same order, each against the closest t so far), which halves the
 // per-iteration overhead (scheduling ballots, decision, loop control) per test.
 // The three pieces of a lean step, for lanes in the matching state.
-template <bool COUNT>
+// the slot of the pre-resolved leaf whose first record is rec0 (SceneView::pre_rec0; slot 0 when none
+// matches — callers ask only for leaves of >= big_leaf entries, which are exactly the table's)
+__device__ __forceinline__ int pre_slot(const SceneView& sc, int rec0) {
+    int b = 0;
+#pragma unroll
+    for (int j = 1; j < kMaxPre; ++j) b = (j < sc.npre && sc.pre_rec0[j] == rec0) ? j : b;
+    return b;
+}
+
+// PRE: a node step whose hit leaf children include a pre-resolved big leaf loads that leaf's key
+// now (the first such leaf of the pair), so it arrives behind the next steps' own loads instead of
+// stalling the wave in pre_turn
+template <bool COUNT, bool PRE = false>
 __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
     const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * s.node;
     float4 a = np[0], b = np[1], c = np[2];
@@ -327,6 +340,10 @@ __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r
     s.nt = s.na + ((ri & rleaf) ? d.w : 0);
     s.la = d.x; s.lb = d.y; s.k = 0;
     s.fl = ((li & !lleaf) ? TF_LINT : 0) | ((ri & !rleaf) ? TF_RINT : 0) | (s.nt > 0 ? TF_LEAF : 0);
+    if constexpr (PRE) {
+        const bool lbig = s.na >= sc.big_leaf, rbig = s.nt - s.na >= sc.big_leaf;
+        if (lbig | rbig) s.pkey = sc.pres[(size_t)pre_slot(sc, lbig ? d.x : d.y) * sc.pres_stride + s.qi];
+    }
     return s.nt == 0;  // no leaf to test: decide now
 }
 
@@ -777,9 +794,10 @@ __device__ __forceinline__ void pre_turn(const SceneView& sc, TravLean& s, uint6
     if ((parked >> lane) & 1ull) {
         int rec0 = 0, n = 0;
         big_seg(s, rec0, n);
-        int b = 0;  // the slot of this lane's leaf: the leaves >= big_leaf are exactly sc.pre[0, npre)
-        for (int j = 1; j < sc.npre; ++j) b = sc.pre[j].rec0 == rec0 ? j : b;
-        const uint64_t key = sc.pres[(size_t)b * sc.pres_stride + s.qi];
+        // the pair's first big leaf: its key came with the node step; a big right leaf after a big
+        // left one is loaded now
+        const bool first = !(s.na >= sc.big_leaf && s.k >= s.na);
+        const uint64_t key = first ? s.pkey : sc.pres[(size_t)pre_slot(sc, rec0) * sc.pres_stride + s.qi];
         const float bt = __builtin_bit_cast(float, (uint32_t)(key >> 32));
         const bool take = (key != ~0ull) & ((s.best_t < 0.0f) | (bt < s.best_t));
         s.best_t = take ? bt : s.best_t;
@@ -940,7 +958,7 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
         else if (state == TF_LEAF)
             decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);
     } else if (state == 0) {
-        decide = lean_node_unit<COUNT>(sc, r, s, cnt);
+        decide = lean_node_unit<COUNT, PRE>(sc, r, s, cnt);
     }
     if (decide) lean_decide(s, stack);
     return true;

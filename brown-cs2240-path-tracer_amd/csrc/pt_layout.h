@@ -169,6 +169,7 @@ struct SceneView {
     int32_t npre;
     uint32_t pres_stride;
     const uint64_t* pres;
+    int32_t pre_rec0[kMaxPre];  // pre[b].rec0 by value (kernel arguments: the traversal's slot lookup in SGPRs)
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

@@ -12,7 +12,7 @@
 // condition of any visit: the same f32 slab test as the traversal, ray-bbox-intersection.wgsl),
 // that smallest (t, position) over ALL of b's entries as a key (f32 bits of t << 32 | position),
 // and k_wf_trace's parked lanes apply it (pt_device.h pre_turn).  Leaf-major and lane = ray: the
-// wave tests entry k of the leaf for 64 rays at once, the record uniform (scalar loads), with the
+// wave tests entry k of the leaf for 64 rays at once, the record uniform (one LDS address), with the
 // test's early out when no lane passes the determinant and u tests (bf_closest's phase 1) — full
 // lanes, no divergence, no per-lane memory traffic in the loop.  The rays that pass a leaf's
 // filter are gathered per wave and leaf in an LDS ring until 64 are waiting.
@@ -34,10 +34,6 @@ __device__ __forceinline__ uint32_t lp_rank_below(uint64_t m) {
 // uniform loads through the scalar cache (constant address space: s_load, no VGPRs)
 typedef const __attribute__((address_space(4))) float* cfloat_p;
 typedef const __attribute__((address_space(4))) int32_t* cint_p;
-__device__ __forceinline__ TriRec rec_scalar(const Tri* tris, int i) {
-    const cfloat_p f = (cfloat_p)(tris + i);
-    return TriRec{make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]), f[8]};
-}
 
 // ray r enters child `side` of node `node` (step = node << 1 | side): the traversal's test of that box
 __device__ __forceinline__ bool enters(const SceneView& sc, int step, const Ray& r) {
@@ -45,58 +41,85 @@ __device__ __forceinline__ bool enters(const SceneView& sc, int step, const Ray&
     return 0.0f < ray_box(r, f[0], f[1], f[2], f[3], f[4], f[5]);
 }
 
-// The leaf (records rec0 .. rec0 + n - 1) for the rays of the wave's lanes (valid: lane holds an
-// entry): each lane ends with the smallest (t, position) over the entries that report a hit — the
-// entries in order, a hit taken when strictly closer (or the first), so the first of equal t.
+// The leaf (records rec0 .. rec0 + n - 1) for up to 64 rays: each ray ends with the smallest
+// (t, position) over the leaf's entries that report a hit, as a key (f32 bits of t << 32 | position;
+// t > 1e-8, so the bits order as t; ~0: none), in every lane that holds it.
+// Lanes: 2^lg rays (ray = lane & (2^lg - 1); rvalid: this lane's ray exists) times S = 64 >> lg
+// segments (seg = lane >> lg): a lane tests entries seg, seg + S, ... of each block, in order, taking a
+// hit when strictly closer than its best (or its first), so its best is the first of its smallest t;
+// the S lanes of a ray then take the minimum key — the first entry of the leaf's smallest t.  A full
+// batch is one ray per lane (S = 1); a few rays — the last depths, a queue too short to fill the
+// chip — spread each ray over S lanes, so a wave walks the leaf in n / S steps.
 // Arithmetic: tri_hit's, operation for operation (the same pt_math.h cross/dot, the det test, u and
 // v as four compares with NaN passing, t > 1e-8), cut after u when no lane can hit.
+// The records pass through the wave's LDS in blocks of kRecBlock (lrec: 3 float4 each, the Tri
+// layout): the wave loads block j + 1 into registers (two coalesced float4 loads per lane) while it
+// tests block j, each record read from LDS at one address for its lanes.  (Scalar loads of each
+// record were one L2 round trip per few entries: 18 % of the VALU bound, profiles/r05b_ab_leafpre.log.)
+constexpr int kRecBlock = 32;  // records per LDS block: 96 float4, 1.5 KB per wave
 template <bool FAST_RCP>
-__device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, int n, const f3 o, const f3 d, bool valid) {
+__device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, int n, const f3 o, const f3 d, bool rvalid,
+                                                 int lg, float4* lrec) {
     const float eps = 1e-8f;
-    const uint64_t vm = __builtin_amdgcn_ballot_w64(valid);
+    const uint32_t lane = threadIdx.x & 63u;
+    const int S = 64 >> lg, seg = (int)(lane >> lg);
+    const float4* __restrict__ g = reinterpret_cast<const float4*>(sc.tris + rec0);
+    const int nf4 = 3 * n;
+    // (loads under ifs: `c ? g[i] : zero` became a load through a select of pointers, the zero in scratch)
+    float4 p0 = make_float4(0, 0, 0, 0), p1 = p0;
+    if ((int)lane < nf4) p0 = g[lane];
+    if (lane < 32u && 64 + (int)lane < nf4) p1 = g[64 + lane];
     float bt = 0.0f;
     int bk = 0x7fffffff;  // none
-    constexpr int G = 4;  // records loaded together: G scalar loads in flight per group
-    for (int k0 = 0; k0 < n; k0 += G) {
-        TriRec tr[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) tr[j] = rec_scalar(sc.tris, rec0 + min(k0 + j, n - 1));
-        // the group's loads issue together: the compiler would sink each into its entry's block (one
-        // round trip per entry); an empty asm that reads every record's SGPRs here keeps them up front
-#pragma unroll
-        for (int j = 0; j < G; ++j)
-            asm volatile("" ::"s"(tr[j].a.x), "s"(tr[j].a.y), "s"(tr[j].a.z), "s"(tr[j].a.w), "s"(tr[j].b.x),
-                         "s"(tr[j].b.y), "s"(tr[j].b.z), "s"(tr[j].b.w), "s"(tr[j].c));
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            if (k0 + j >= n) continue;  // uniform: past the leaf's end (the clamped record)
-            const f3 v0 = mk(tr[j].a.x, tr[j].a.y, tr[j].a.z), e1 = mk(tr[j].a.w, tr[j].b.x, tr[j].b.y),
-                     e2 = mk(tr[j].b.z, tr[j].b.w, tr[j].c);
+    for (int k0 = 0; k0 < n; k0 += kRecBlock) {
+        wave_lds_sync();  // every lane is done reading the previous block
+        lrec[lane] = p0;
+        if (lane < 32u) lrec[64 + lane] = p1;
+        wave_lds_sync();
+        const int nb = 3 * (k0 + kRecBlock);  // the next block, in flight while this one is tested
+        if (nb + (int)lane < nf4) p0 = g[nb + lane];
+        if (lane < 32u && nb + 64 + (int)lane < nf4) p1 = g[nb + 64 + lane];
+        const int m = min(kRecBlock, n - k0);
+        for (int j = 0; j < m; j += S) {  // uniform
+            const int e = j + seg;        // this lane's entry of the block
+            const bool live = rvalid & (e < m);
+            const int ee = min(e, m - 1);
+            const float4 a = lrec[3 * ee], b = lrec[3 * ee + 1];
+            const float c = lrec[3 * ee + 2].x;
+            const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c);
             const f3 rce2 = cross(d, e2);
             const float det = dot(e1, rce2);
             const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
             const f3 sv = o - v0;
             const float u = inv_det * dot(sv, rce2);
             const bool ok_det = !(det > -eps && det < eps), ok_lo = !(u < 0.0f), ok_hi = !(u > 1.0f);
-            if ((vm & __builtin_amdgcn_ballot_w64(ok_det) & __builtin_amdgcn_ballot_w64(ok_lo) &
-                 __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
+            if ((__builtin_amdgcn_ballot_w64(live) & __builtin_amdgcn_ballot_w64(ok_det) &
+                 __builtin_amdgcn_ballot_w64(ok_lo) & __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
                 continue;  // wave-uniform: no lane can report a hit
             const f3 sce1 = cross(sv, e1);
             const float v = inv_det * dot(d, sce1);
             const float t = inv_det * dot(e2, sce1);
-            const bool hit = valid & ok_det & ok_lo & ok_hi & !(v < 0.0f) & !(u + v > 1.0f) & (t > eps);
+            const bool hit = live & ok_det & ok_lo & ok_hi & !(v < 0.0f) & !(u + v > 1.0f) & (t > eps);
             const bool take = hit & ((t < bt) | (bk == 0x7fffffff));
             bt = take ? t : bt;
-            bk = take ? k0 + j : bk;
+            bk = take ? k0 + e : bk;
         }
     }
-    return bk == 0x7fffffff ? ~0ull : ((uint64_t)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk;
+    uint64_t key = bk == 0x7fffffff ? ~0ull : ((uint64_t)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk;
+    for (int off = 1 << lg; off < 64; off <<= 1) {  // uniform: the minimum over the ray's S lanes
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, off, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), off, 64);
+        const uint64_t other = ((uint64_t)hi << 32) | lo;
+        key = other < key ? other : key;
+    }
+    return key;
 }
 
 template <bool FAST_RCP>
 __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, WfBuffers wb, int in_q) {
     __shared__ uint32_t ring[kLeafPassBlock / 64][kMaxPre][kLeafRing];
     __shared__ uint32_t pos[kLeafPassBlock / 64][kMaxPre][2];  // per wave and leaf: head, tail (wave-uniform)
+    __shared__ float4 lrec[kLeafPassBlock / 64][3 * kRecBlock];  // per wave: a block of leaf records
     const uint32_t wv = threadIdx.x / 64u, lane = threadIdx.x & 63u;
     // the queue the next traversal launch reads, as k_wf_trace reads it (a trace that gave up: nothing)
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
@@ -106,25 +129,33 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
     const float4* __restrict__ q = in_q ? wb.shd.ray : wb.ext.ray;
     const uint32_t nwaves = gridDim.x * (kLeafPassBlock / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (kLeafPassBlock / 64) + wv);
-    // resolve the 64 (or `avail`) entries waiting in leaf b's ring from position `tail`
+    // resolve the 64 (or `avail`) entries waiting in leaf b's ring from position `tail`: 2^lg >= avail
+    // rays, each over 64 >> lg lanes
     auto run = [&](int b, uint32_t tail, uint32_t avail) {
         wave_lds_sync();  // the ring's entries were written by other lanes
-        const bool valid = lane < avail;
-        const uint32_t i = valid ? ring[wv][b][(tail + lane) & (kLeafRing - 1)] : 0u;
-        const float4 a = valid ? q[2 * (size_t)i] : make_float4(0, 0, 0, 0);
-        const float4 c = valid ? q[2 * (size_t)i + 1] : make_float4(0, 0, 0, 0);
+        const int lg = avail > 1 ? 32 - __builtin_clz(avail - 1) : 0;  // ceil(log2 avail)
+        const uint32_t ri = lane & ((1u << lg) - 1u);
+        const bool valid = ri < avail;
+        const uint32_t i = valid ? ring[wv][b][(tail + ri) & (kLeafRing - 1)] : 0u;
+        float4 a = make_float4(0, 0, 0, 0), c = a;
+        if (valid) { a = q[2 * (size_t)i]; c = q[2 * (size_t)i + 1]; }
         const cint_p pl = (cint_p)(sc.pre + b);
-        const uint64_t key = resolve_leaf<FAST_RCP>(sc, pl[0], pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid);
-        if (valid) wb.pres[(size_t)b * wb.pres_stride + i] = key;
+        const uint64_t key =
+            resolve_leaf<FAST_RCP>(sc, pl[0], pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec[wv]);
+        if (lane < avail) wb.pres[(size_t)b * wb.pres_stride + i] = key;
     };
-    const uint32_t nwin = (count + 63) / 64;
+    // windows of wr queue entries per wave: 64, or fewer when the queue cannot give every wave a
+    // window of 64 (the last depths): then each wave's rays are few and each is walked by many lanes
+    uint32_t wr = 64;
+    while (wr > 1 && (uint64_t)count < (uint64_t)nwaves * wr) wr >>= 1;
+    const uint32_t nwin = (count + wr - 1) / wr;
     for (uint32_t win = w; win < nwin; win += nwaves) {
-        const uint32_t i = win * 64 + lane;
-        const bool valid = i < count;
+        const uint32_t i = win * wr + lane;
+        const bool valid = lane < wr && i < count;
         Ray r;
         {
-            const float4 a = valid ? q[2 * (size_t)i] : make_float4(0, 0, 0, 1);
-            const float4 c = valid ? q[2 * (size_t)i + 1] : make_float4(0, 0, 0, 0);
+            float4 a = make_float4(0, 0, 0, 1), c = make_float4(0, 0, 0, 0);
+            if (valid) { a = q[2 * (size_t)i]; c = q[2 * (size_t)i + 1]; }
             r.o = mk(a.x, a.y, a.z);
             r.d = mk(a.w, c.x, c.y);
             r.inv = rcp3(r.d);  // = unpack_ray's: the traversal's box tests, bit for bit

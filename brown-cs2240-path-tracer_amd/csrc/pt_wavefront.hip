@@ -207,9 +207,9 @@ constexpr uint32_t kTraceBlock = 512;  // 8 waves share one LDS copy of the scen
 // busy (the last depths), windows of wr / 2 .. 1 entries spread the queue over more waves, so each
 // wave's traversal is the slowest of fewer rays.  A window still takes kWinRays sequence numbers
 // (ring and flush bookkeeping unchanged); only its queue span is wr.
-template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4>
-__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
-                                                          uint32_t watchdog, int sparse) {
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING, int PRUN>
+__device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out, uint32_t watchdog,
+                                              int sparse) {
     constexpr uint32_t nring = RING, kWinTab = win_tab(RING);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const LStack32 stack = LStack32::make(smem, blockDim.x);
@@ -342,6 +342,18 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
         }
     }
     if (COUNT) flush_counters(c, cnt_out);
+}
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4>
+__global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
+                                                          uint32_t watchdog, int sparse) {
+    wf_trace_body<LDS, TRAV, COUNT, RING, PRUN>(sc, wb, in_q, cnt_out, watchdog, sparse);
+}
+// The instances with pre-resolved big leaves (TRAV 26x / 27x): held to 80 VGPRs, 6 waves per SIMD
+// (83 unconstrained: 5 waves)
+template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4>
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_wf_trace_pre(
+    SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out, uint32_t watchdog, int sparse) {
+    wf_trace_body<LDS, TRAV, COUNT, RING, PRUN>(sc, wb, in_q, cnt_out, watchdog, sparse);
 }
 
 // Brute force + replay: the closest-hit kernel for mailbox scenes (SceneView::mailbox: at most
@@ -866,6 +878,7 @@ template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4
 constexpr const void* trace_kernel() {
     if constexpr (TRAV >= 400) return (const void*)k_wf_step_bf<false, LDS, ((TRAV / 10) & 1) != 0, COUNT>;
     else if constexpr (TRAV >= 300) return (const void*)k_wf_trace_bf<LDS, ((TRAV / 10) & 1) != 0, COUNT>;
+    else if constexpr (TRAV >= 260) return (const void*)k_wf_trace_pre<LDS, TRAV, COUNT, RING, PRUN>;
     else return (const void*)k_wf_trace<LDS, TRAV, COUNT, RING, PRUN>;
 }
 // the k_wf_trace instances with a 256-entry ring and with pooled runs of 2 (SceneView::leaf_pool
@@ -1054,8 +1067,15 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
             } else {
                 if constexpr (TRAV >= 260 && TRAV < 300)  // the big leaves first (k_wf_leafpass)
                     HIP_RETURN_IF(launch_leafpass(sc, w, in_q, ((TRAV / 10) & 1) != 0, ws.leaf_blocks, st));
-#define PT_TRACE(RG, PR) PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, RG, PR>), dim3(tblocks), \
-                                   dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, watchdog, sparse)
+#define PT_TRACE(RG, PR)                                                                                        \
+    do {                                                                                                        \
+        if constexpr (TRAV >= 260)                                                                              \
+            PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace_pre<LDS, TRAV, COUNT, RG, PR>), dim3(tblocks), dim3(kTraceBlock), \
+                      lds, st, sc, w, in_q, cnt, watchdog, sparse);                                             \
+        else                                                                                                    \
+            PT_LAUNCH(KID_WF_TRACE, st, (k_wf_trace<LDS, TRAV, COUNT, RG, PR>), dim3(tblocks), dim3(kTraceBlock), \
+                      lds, st, sc, w, in_q, cnt, watchdog, sparse);                                             \
+    } while (0)
                 if constexpr (has_variants<TRAV, COUNT>()) {
                     if (nring == kHitRingMax && run2) PT_TRACE(kHitRingMax, 2);
                     else if (nring == kHitRingMax) PT_TRACE(kHitRingMax, 4);
