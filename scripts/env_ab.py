@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--synthetic", type=int, default=0, help="bench.py's N-triangle synthetic scene instead of --scene")
     ap.add_argument("--bvh", default="reference", help="reference | sah (bench.py --bvh)")
+    ap.add_argument("--all-meshes", action="store_true", help="every primitive of the scene (bench.py --all-meshes)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--profile", action="store_true", help="one more render per variant with per-launch events")
     ap.add_argument("--scene-opt", action="append", default=[],
@@ -37,7 +38,8 @@ def main():
     import bench
     import pt_amd
     with tempfile.TemporaryDirectory() as td:
-        tri, bvh, meta = bench.pack_scene(a.scene, td, a.width, a.height, a.spp, a.synthetic, bvh=a.bvh)
+        tri, bvh, meta = bench.pack_scene(a.scene, td, a.width, a.height, a.spp, a.synthetic, bvh=a.bvh,
+                                          all_meshes=a.all_meshes)
     W, H = int(meta[0]), int(meta[1])
     for kv in a.scene_opt:
         pt_amd.set_option(*kv.split("=", 1))
