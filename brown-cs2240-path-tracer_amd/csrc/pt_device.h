@@ -325,7 +325,7 @@ __device__ __forceinline__ int pre_slot(const SceneView& sc, int rec0) {
 
 // PRE: a node step whose hit leaf children include a pre-resolved big leaf loads that leaf's key
 // now (the first such leaf of the pair), so it arrives behind the next steps' own loads instead of
-// stalling the wave in pre_turn
+// stalling the wave in its leaf turn (pre_apply)
 template <bool COUNT, bool PRE = false>
 __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
     const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * s.node;
@@ -360,9 +360,12 @@ __device__ __forceinline__ void big_seg(const TravLean& s, int& rec0, int& n) {
     n = left ? s.na : s.nt - s.na;
 }
 
-template <int K, bool COUNT, bool FAST_RCP, bool BIG = false>
+template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool PRE = false>
 __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
-    if constexpr (BIG) {  // park at a big leaf: now, or where this turn would enter it
+    if constexpr (PRE) {  // a big leaf at the lane's position: its key (pre_apply)
+        if (pre_apply<COUNT>(sc, s, cnt)) { s.fl &= ~TF_LEAF; return true; }
+        if (big_at(sc, s)) return false;  // a big right leaf next: its key in the next turn
+    } else if constexpr (BIG) {  // park at a big leaf: now, or where this turn would enter it
         if (big_at(sc, s)) { s.fl |= TF_PARK; return false; }
     }
     // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
@@ -388,7 +391,7 @@ __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r
     s.k = max(k0 + 1, min(k0 + K, lim));
     const bool decide = s.k == s.nt;
     s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
-    if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
+    if constexpr (BIG && !PRE) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
     return decide;
 }
 
@@ -782,20 +785,20 @@ __device__ __forceinline__ void chunk_turn_multi(const SceneView& sc, const Ray&
     }
 }
 
-// Big leaves resolved before the traversal (k_wf_leafpass, pt_leafpass.hip): the parked lanes
-// — every one, whatever its leaf — take their leaf's precomputed key, the smallest (t, position)
-// over ALL the leaf's entries that report a hit (~0: none), and apply it as the reference's
-// strict-< loop over the leaf ends: that loop, started at the closest t so far, keeps the first
-// entry of the smallest t when that t is below it, and nothing otherwise — which needs no test of
-// the leaf here (the same argument as the cooperative turns; intersection-logic.wgsl:47-176).
-template <bool COUNT, class ST>
-__device__ __forceinline__ void pre_turn(const SceneView& sc, TravLean& s, uint64_t parked, const ST& stack, Counters& cnt) {
-    const int lane = (int)(threadIdx.x & 63u);
-    if ((parked >> lane) & 1ull) {
+// Big leaves resolved before the traversal (k_wf_leafpass, pt_leafpass.hip): a lane whose next
+// entry starts a big leaf takes that leaf's precomputed key — the smallest (t, position) over ALL
+// the leaf's entries that report a hit (~0: none) — and applies it as the reference's strict-<
+// loop over the leaf ends: that loop, started at the closest t so far, keeps the first entry of the
+// smallest t when that t is below it, and nothing otherwise, so no test of the leaf is needed here
+// (the same argument as the cooperative turns; intersection-logic.wgsl:47-176).  Called by the
+// lane's leaf turn, before its other entries; the key of the pair's first big leaf was loaded at the
+// node step (lean_node_unit), a second one (a big right leaf after a big left one: the lane's next
+// leaf turn) is loaded here.  The lane's position moves past the leaf; true when that ends the pair.
+template <bool COUNT>
+__device__ __forceinline__ bool pre_apply(const SceneView& sc, TravLean& s, Counters& cnt) {
+    if (big_at(sc, s)) {
         int rec0 = 0, n = 0;
         big_seg(s, rec0, n);
-        // the pair's first big leaf: its key came with the node step; a big right leaf after a big
-        // left one is loaded now
         const bool first = !(s.na >= sc.big_leaf && s.k >= s.na);
         const uint64_t key = first ? s.pkey : sc.pres[(size_t)pre_slot(sc, rec0) * sc.pres_stride + s.qi];
         const float bt = __builtin_bit_cast(float, (uint32_t)(key >> 32));
@@ -804,14 +807,8 @@ __device__ __forceinline__ void pre_turn(const SceneView& sc, TravLean& s, uint6
         s.best = take ? rec0 + (int)(uint32_t)key : s.best;
         if (COUNT) cnt.tri_tests += n;
         s.k += n;
-        s.fl &= ~TF_PARK;
-        if (s.k == s.nt) {
-            s.fl &= ~TF_LEAF;
-            lean_decide(s, stack);
-        } else if (big_at(sc, s)) {
-            s.fl |= TF_PARK;  // its right leaf is big too
-        }
     }
+    return s.k == s.nt;
 }
 
 // A leaf turn with the pair's remaining entries pooled over the whole wave (the wavefront
@@ -835,11 +832,17 @@ __device__ __forceinline__ void pre_turn(const SceneView& sc, TravLean& s, uint6
 // gain (profiles/r04ab_ab_runtime_run.log: 100k +3 %, 1M +12 %; r04ad_ab_runtime_run.log: the
 // same with two entries per iteration), and both runs inlined into one kernel cost Glossy 1.5 %
 // (r04ac, r04ad: ablib/tmpl), so each run length is its own k_wf_trace instance.
-template <int RUN, bool COUNT, bool FAST_RCP, bool BIG>
+template <int RUN, bool COUNT, bool FAST_RCP, bool BIG, bool PRE = false>
 __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r, TravLean& s, bool in_leaf, Counters& cnt) {
     constexpr uint64_t kNoKey = ~0ull;
     const int lane = (int)(threadIdx.x & 63u);
-    if constexpr (BIG) {  // park at a big leaf: now (no tests this turn)
+    bool pre_done = false;  // PRE: the pair ended with a big leaf's key
+    if constexpr (PRE) {  // a big leaf at the lane's position: its key first
+        if (in_leaf) {
+            pre_done = pre_apply<COUNT>(sc, s, cnt);
+            in_leaf = !pre_done && !big_at(sc, s);  // a big right leaf next: its key in the next turn
+        }
+    } else if constexpr (BIG) {  // park at a big leaf: now (no tests this turn)
         if (in_leaf && big_at(sc, s)) { s.fl |= TF_PARK; in_leaf = false; }
     }
     // a turn of a lane whose right leaf is big stops at that leaf's start (it parks below)
@@ -915,7 +918,11 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
         s.k = lim;
         decide = s.k == s.nt;
         s.fl = decide ? (s.fl & ~TF_LEAF) : s.fl;
-        if constexpr (BIG) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
+        if constexpr (BIG && !PRE) s.fl |= (!decide && big_at(sc, s)) ? TF_PARK : 0;
+    }
+    if constexpr (PRE) {
+        if (pre_done) s.fl &= ~TF_LEAF;
+        decide |= pre_done;
     }
     return decide;
 }
@@ -923,19 +930,13 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
 // Each iteration runs ONE unit type for the whole wave — a leaf turn (up to K triangle tests)
 // when leaf lanes >= node_bias * node lanes, else a node turn — keeping each lane's unit order.
 // PRUN: the pooled leaf turns' run length (lean_leaf_pool)
-// PRE: the big leaves were resolved before the traversal (pre_turn; TRAV 26x / 27x)
+// PRE: the big leaves were resolved before the traversal (pre_apply; TRAV 26x / 27x)
 template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool CHUNKS = false, int PRUN = 4, bool PRE = false,
           class ST>
 __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r, TravLean& s, const ST& stack,
                                                Counters& cnt) {
-    const int state = s.fl & (TF_LEAF | TF_DONE | (BIG ? TF_PARK : 0));
-    if constexpr (BIG && PRE) {  // parked lanes take their leaves' precomputed results
-        const uint64_t parked = __ballot((state & TF_PARK) != 0);
-        if (parked) {  // wave-uniform
-            pre_turn<COUNT>(sc, s, parked, stack, cnt);
-            return true;
-        }
-    } else if constexpr (BIG) {  // a parked lane's big leaf goes first: the wave tests it for that ray
+    const int state = s.fl & (TF_LEAF | TF_DONE | ((BIG && !PRE) ? TF_PARK : 0));
+    if constexpr (BIG && !PRE) {  // a parked lane's big leaf goes first: the wave tests it for that ray
         const uint64_t parked = __ballot((state & TF_PARK) != 0);
         if (parked) {  // wave-uniform
             int my0 = 0, myn = 0;  // the first parked lane's leaf (the other lanes' fields may not be a leaf's)
@@ -954,9 +955,9 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     bool decide = false;
     if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
         if (CHUNKS && sc.leaf_pool && sc.lkeys && __ballot(1) == ~0ull)  // the wavefront kernel: the leaf entries pooled
-            decide = lean_leaf_pool<PRUN, COUNT, FAST_RCP, BIG>(sc, r, s, state == TF_LEAF, cnt);
+            decide = lean_leaf_pool<PRUN, COUNT, FAST_RCP, BIG, PRE>(sc, r, s, state == TF_LEAF, cnt);
         else if (state == TF_LEAF)
-            decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG>(sc, r, s, cnt);
+            decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG, PRE>(sc, r, s, cnt);
     } else if (state == 0) {
         decide = lean_node_unit<COUNT, PRE>(sc, r, s, cnt);
     }

@@ -11,7 +11,7 @@
 // queue entry whose ray enters all the child boxes on b's path from the root (a necessary
 // condition of any visit: the same f32 slab test as the traversal, ray-bbox-intersection.wgsl),
 // that smallest (t, position) over ALL of b's entries as a key (f32 bits of t << 32 | position),
-// and k_wf_trace's parked lanes apply it (pt_device.h pre_turn).  Leaf-major and lane = ray: the
+// and k_wf_trace's lanes apply it in their leaf turns (pt_device.h pre_apply).  Leaf-major and lane = ray: the
 // wave tests entry k of the leaf for 64 rays at once, the record uniform (one LDS address), with the
 // test's early out when no lane passes the determinant and u tests (bf_closest's phase 1) — full
 // lanes, no divergence, no per-lane memory traffic in the loop.  The rays that pass a leaf's
