@@ -71,6 +71,33 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
     if (lane < 32u && 64 + (int)lane < nf4) p1 = g[64 + lane];
     float bt = 0.0f;
     int bk = 0x7fffffff;  // none
+    // One entry (record words a, b, c) for this lane's ray: tri_hit's arithmetic.  The wave skips
+    // the entry when no lane can report a hit, decided before the reciprocal: a lane cannot when its
+    // determinant fails, or when its u = RN(RN(1 / det) * un) is certainly outside [0, 1] — un and
+    // det of opposite signs with |un| >= 2^-100 |det| (u < 0, far above underflow to -0), or |un| >
+    // RN(|det| (1 + 2^-20)) (|u| > (1 + 2^-21)(1 - 2^-24)^2 > 1).  NaN operands vote "maybe".
+    auto test_entry = [&](const float4 a, const float4 b, const float c, const bool live, const int pos) {
+        const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c);
+        const f3 rce2 = cross(d, e2);
+        const float det = dot(e1, rce2);
+        const f3 sv = o - v0;
+        const float un = dot(sv, rce2);
+        const bool ok_det = !(det > -eps && det < eps);
+        const float ad = fabsf(det), au = fabsf(un);
+        const bool out = ((un * det < 0.0f) & (au >= ad * 0x1p-100f)) | (au > ad * 1.00000095367431640625f);
+        if ((__builtin_amdgcn_ballot_w64(live) & __builtin_amdgcn_ballot_w64(ok_det) &
+             ~__builtin_amdgcn_ballot_w64(out)) == 0)
+            return;  // wave-uniform: no lane can report a hit
+        const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
+        const float u = inv_det * un;
+        const f3 sce1 = cross(sv, e1);
+        const float v = inv_det * dot(d, sce1);
+        const float t = inv_det * dot(e2, sce1);
+        const bool hit = live & ok_det & !(u < 0.0f) & !(u > 1.0f) & !(v < 0.0f) & !(u + v > 1.0f) & (t > eps);
+        const bool take = hit & ((t < bt) | (bk == 0x7fffffff));
+        bt = take ? t : bt;
+        bk = take ? pos : bk;
+    };
     for (int k0 = 0; k0 < n; k0 += kRecBlock) {
         wave_lds_sync();  // every lane is done reading the previous block
         lrec[lane] = p0;
@@ -80,29 +107,15 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
         if (nb + (int)lane < nf4) p0 = g[nb + lane];
         if (lane < 32u && nb + 64 + (int)lane < nf4) p1 = g[nb + 64 + lane];
         const int m = min(kRecBlock, n - k0);
-        for (int j = 0; j < m; j += S) {  // uniform
-            const int e = j + seg;        // this lane's entry of the block
-            const bool live = rvalid & (e < m);
-            const int ee = min(e, m - 1);
-            const float4 a = lrec[3 * ee], b = lrec[3 * ee + 1];
-            const float c = lrec[3 * ee + 2].x;
-            const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c);
-            const f3 rce2 = cross(d, e2);
-            const float det = dot(e1, rce2);
-            const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
-            const f3 sv = o - v0;
-            const float u = inv_det * dot(sv, rce2);
-            const bool ok_det = !(det > -eps && det < eps), ok_lo = !(u < 0.0f), ok_hi = !(u > 1.0f);
-            if ((__builtin_amdgcn_ballot_w64(live) & __builtin_amdgcn_ballot_w64(ok_det) &
-                 __builtin_amdgcn_ballot_w64(ok_lo) & __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
-                continue;  // wave-uniform: no lane can report a hit
-            const f3 sce1 = cross(sv, e1);
-            const float v = inv_det * dot(d, sce1);
-            const float t = inv_det * dot(e2, sce1);
-            const bool hit = live & ok_det & ok_lo & ok_hi & !(v < 0.0f) & !(u + v > 1.0f) & (t > eps);
-            const bool take = hit & ((t < bt) | (bk == 0x7fffffff));
-            bt = take ? t : bt;
-            bk = take ? k0 + e : bk;
+        // two entries per step, both records read from LDS before either is tested (their LDS latency
+        // behind one another's arithmetic)
+        for (int j = 0; j < m; j += 2 * S) {  // uniform
+            const int ea = j + seg, eb = j + S + seg;  // this lane's two entries of the block
+            const int xa = min(ea, m - 1), xb = min(eb, m - 1);
+            const float4 aa = lrec[3 * xa], ab = lrec[3 * xa + 1], ba = lrec[3 * xb], bb = lrec[3 * xb + 1];
+            const float ac = lrec[3 * xa + 2].x, bc = lrec[3 * xb + 2].x;
+            test_entry(aa, ab, ac, rvalid & (ea < m), k0 + ea);
+            if (j + S < m) test_entry(ba, bb, bc, rvalid & (eb < m), k0 + eb);  // uniform
         }
     }
     uint64_t key = bk == 0x7fffffff ? ~0ull : ((uint64_t)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk;

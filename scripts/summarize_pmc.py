@@ -13,7 +13,7 @@ import sys
 
 
 def short(name):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
     for pre in ("void pt::", "pt::"):
         if name.startswith(pre):
             name = name[len(pre):]
