@@ -53,10 +53,15 @@ __device__ __forceinline__ bool enters(const SceneView& sc, int step, const Ray&
 // Arithmetic: tri_hit's, operation for operation (the same pt_math.h cross/dot, the det test, u and
 // v as four compares with NaN passing, t > 1e-8), cut after u when no lane can hit.
 // The records pass through the wave's LDS in blocks of kRecBlock (lrec: 3 float4 each, the Tri
-// layout): the wave loads block j + 1 into registers (two coalesced float4 loads per lane) while it
+// layout): the wave loads block j + 1 into registers (one coalesced float4 load per lane) while it
 // tests block j, each record read from LDS at one address for its lanes.  (Scalar loads of each
 // record were one L2 round trip per few entries: 18 % of the VALU bound, profiles/r05b_ab_leafpre.log.)
-constexpr int kRecBlock = 32;  // records per LDS block: 96 float4, 1.5 KB per wave
+// Measured and not kept (profiles/r05g_ab_leafpass.log, r05h_ab_leafpass.log, same bits): two
+// entries per step with their records read ahead and the skip vote taken before the reciprocal
+// (-2 %); the test without the vote, branch-free (-21 %: the vote skips v and t for about half the
+// entries); a walk of the leaf's chunks that skips the chunks no lane's ray can hit (option
+// leaf_cull, -35 %, profiles/r05e_ab_leafpre.log: a wave's 64 rays keep nearly every chunk open).
+constexpr int kRecBlock = 16;  // records per LDS block: 48 float4, 768 B per wave
 template <bool FAST_RCP>
 __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, int n, const f3 o, const f3 d, bool rvalid,
                                                  int lg, float4* lrec) {
@@ -66,56 +71,40 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
     const float4* __restrict__ g = reinterpret_cast<const float4*>(sc.tris + rec0);
     const int nf4 = 3 * n;
     // (loads under ifs: `c ? g[i] : zero` became a load through a select of pointers, the zero in scratch)
-    float4 p0 = make_float4(0, 0, 0, 0), p1 = p0;
-    if ((int)lane < nf4) p0 = g[lane];
-    if (lane < 32u && 64 + (int)lane < nf4) p1 = g[64 + lane];
+    float4 p0 = make_float4(0, 0, 0, 0);
+    if (lane < 3u * kRecBlock && (int)lane < nf4) p0 = g[lane];
     float bt = 0.0f;
     int bk = 0x7fffffff;  // none
-    // One entry (record words a, b, c) for this lane's ray: tri_hit's arithmetic.  The wave skips
-    // the entry when no lane can report a hit, decided before the reciprocal: a lane cannot when its
-    // determinant fails, or when its u = RN(RN(1 / det) * un) is certainly outside [0, 1] — un and
-    // det of opposite signs with |un| >= 2^-100 |det| (u < 0, far above underflow to -0), or |un| >
-    // RN(|det| (1 + 2^-20)) (|u| > (1 + 2^-21)(1 - 2^-24)^2 > 1).  NaN operands vote "maybe".
-    auto test_entry = [&](const float4 a, const float4 b, const float c, const bool live, const int pos) {
-        const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c);
-        const f3 rce2 = cross(d, e2);
-        const float det = dot(e1, rce2);
-        const f3 sv = o - v0;
-        const float un = dot(sv, rce2);
-        const bool ok_det = !(det > -eps && det < eps);
-        const float ad = fabsf(det), au = fabsf(un);
-        const bool out = ((un * det < 0.0f) & (au >= ad * 0x1p-100f)) | (au > ad * 1.00000095367431640625f);
-        if ((__builtin_amdgcn_ballot_w64(live) & __builtin_amdgcn_ballot_w64(ok_det) &
-             ~__builtin_amdgcn_ballot_w64(out)) == 0)
-            return;  // wave-uniform: no lane can report a hit
-        const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
-        const float u = inv_det * un;
-        const f3 sce1 = cross(sv, e1);
-        const float v = inv_det * dot(d, sce1);
-        const float t = inv_det * dot(e2, sce1);
-        const bool hit = live & ok_det & !(u < 0.0f) & !(u > 1.0f) & !(v < 0.0f) & !(u + v > 1.0f) & (t > eps);
-        const bool take = hit & ((t < bt) | (bk == 0x7fffffff));
-        bt = take ? t : bt;
-        bk = take ? pos : bk;
-    };
     for (int k0 = 0; k0 < n; k0 += kRecBlock) {
         wave_lds_sync();  // every lane is done reading the previous block
-        lrec[lane] = p0;
-        if (lane < 32u) lrec[64 + lane] = p1;
+        if (lane < 3u * kRecBlock) lrec[lane] = p0;
         wave_lds_sync();
         const int nb = 3 * (k0 + kRecBlock);  // the next block, in flight while this one is tested
-        if (nb + (int)lane < nf4) p0 = g[nb + lane];
-        if (lane < 32u && nb + 64 + (int)lane < nf4) p1 = g[nb + 64 + lane];
+        if (lane < 3u * kRecBlock && nb + (int)lane < nf4) p0 = g[nb + lane];
         const int m = min(kRecBlock, n - k0);
-        // two entries per step, both records read from LDS before either is tested (their LDS latency
-        // behind one another's arithmetic)
-        for (int j = 0; j < m; j += 2 * S) {  // uniform
-            const int ea = j + seg, eb = j + S + seg;  // this lane's two entries of the block
-            const int xa = min(ea, m - 1), xb = min(eb, m - 1);
-            const float4 aa = lrec[3 * xa], ab = lrec[3 * xa + 1], ba = lrec[3 * xb], bb = lrec[3 * xb + 1];
-            const float ac = lrec[3 * xa + 2].x, bc = lrec[3 * xb + 2].x;
-            test_entry(aa, ab, ac, rvalid & (ea < m), k0 + ea);
-            if (j + S < m) test_entry(ba, bb, bc, rvalid & (eb < m), k0 + eb);  // uniform
+        for (int j = 0; j < m; j += S) {  // uniform
+            const int e = j + seg;        // this lane's entry of the block
+            const bool live = rvalid & (e < m);
+            const int ee = min(e, m - 1);
+            const float4 a = lrec[3 * ee], b = lrec[3 * ee + 1];
+            const float c = lrec[3 * ee + 2].x;
+            const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c);
+            const f3 rce2 = cross(d, e2);
+            const float det = dot(e1, rce2);
+            const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
+            const f3 sv = o - v0;
+            const float u = inv_det * dot(sv, rce2);
+            const bool ok_det = !(det > -eps && det < eps), ok_lo = !(u < 0.0f), ok_hi = !(u > 1.0f);
+            if ((__builtin_amdgcn_ballot_w64(live) & __builtin_amdgcn_ballot_w64(ok_det) &
+                 __builtin_amdgcn_ballot_w64(ok_lo) & __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
+                continue;  // wave-uniform: no lane can report a hit
+            const f3 sce1 = cross(sv, e1);
+            const float v = inv_det * dot(d, sce1);
+            const float t = inv_det * dot(e2, sce1);
+            const bool hit = live & ok_det & ok_lo & ok_hi & !(v < 0.0f) & !(u + v > 1.0f) & (t > eps);
+            const bool take = hit & ((t < bt) | (bk == 0x7fffffff));
+            bt = take ? t : bt;
+            bk = take ? k0 + e : bk;
         }
     }
     uint64_t key = bk == 0x7fffffff ? ~0ull : ((uint64_t)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk;
@@ -128,110 +117,8 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
     return key;
 }
 
-// The same result, walking the leaf's chunks (pt_leafbvh.cpp; SceneView::lnodes / ltris, option
-// leaf_cull): chunk c (wave-uniform, its node through the scalar cache, loaded one chunk ahead) is
-// checked for every lane's ray against that lane's best so far (chunk_skip, pt_device.h: no entry
-// of a skipped chunk can report a hit at t <= the bound), and its entries are tested only when some
-// lane opens it — by every lane: a lane whose check held no entry able to beat its bound gains
-// nothing it could take.  The records stream through LDS in chunk order (ltris; each carries its
-// position in the leaf, so the keys are the same (t, position)).  Pays where a wave's rays are
-// coherent enough that most chunks are closed for all of them (camera rays).
 template <bool FAST_RCP>
-__device__ __forceinline__ uint64_t resolve_leaf_cull(const SceneView& sc, int rec0, const f3 o, const f3 d, bool rvalid,
-                                                      int lg, float4* lrec) {
-    const float eps = 1e-8f;
-    const uint32_t lane = threadIdx.x & 63u;
-    const int S = 64 >> lg, seg = (int)(lane >> lg);
-    const cint_p tr0 = (cint_p)(sc.tris + rec0);
-    const int c0 = tr0[11] - 1, c1 = tr0[12 + 11];  // Tri::lbvh of the leaf's first two records
-    const cfloat_p nf = (cfloat_p)sc.lnodes;  // chunk nodes, 16 floats each, through the scalar cache
-    auto node4 = [&](int q) { return make_float4(nf[4 * q], nf[4 * q + 1], nf[4 * q + 2], nf[4 * q + 3]); };
-    Ray r;
-    r.o = o;
-    r.d = d;
-    r.inv = rcp3(d);
-    const float idl = 1.0f / sqrtf(dot(d, d));
-    const float on = sqrtf(dot(o, o));
-    // the record stream: block [bs, bs + kRecBlock) of ltris in LDS, [bs + kRecBlock, + 2 kRecBlock) in
-    // registers; every load stays below the leaf's last record f1 (ltris ends there for the last leaf)
-    const float4* __restrict__ g = reinterpret_cast<const float4*>(sc.ltris);
-    const int f0 = __builtin_bit_cast(int, nf[16 * c0 + 15]) & 0xffffff;
-    const int il = __builtin_bit_cast(int, nf[16 * (c1 - 1) + 15]);
-    const int f1 = (il & 0xffffff) + (il >> 24);
-    int bs = f0 - kRecBlock;  // nothing staged yet: the registers hold [f0, f0 + kRecBlock)
-    float4 p0 = make_float4(0, 0, 0, 0), p1 = p0;
-    auto fetch = [&](int base, float4& x0, float4& x1) {  // block at record `base` into registers
-        if (3 * base + (int)lane < 3 * f1) x0 = g[3 * base + lane];
-        if (lane < 32u && 3 * base + 64 + (int)lane < 3 * f1) x1 = g[3 * base + 64 + lane];
-    };
-    fetch(f0, p0, p1);
-    float bt = 0.0f;
-    int bk = 0x7fffffff;  // none
-    float4 na = node4(4 * c0), nb = node4(4 * c0 + 1), nc = node4(4 * c0 + 2), ne = node4(4 * c0 + 3);
-    for (int c = c0; c < c1; ++c) {
-        const float4 a = na, b = nb, cc = nc, e = ne;
-        if (c + 1 < c1) {  // the next chunk's node, in flight while this one is checked
-            na = node4(4 * c + 4); nb = node4(4 * c + 5); nc = node4(4 * c + 6); ne = node4(4 * c + 7);
-        }
-        const float bound = bk == 0x7fffffff ? __builtin_inff() : bt;
-        const bool open = rvalid & !chunk_skip(a, b, cc, e, r, idl, on, bound);
-        if (!__builtin_amdgcn_ballot_w64(open)) continue;  // uniform: closed for every ray
-        const int info = __builtin_bit_cast(int, e.w), first = info & 0xffffff, cnt = info >> 24;
-        for (int j0 = 0; j0 < cnt; j0 += S) {  // uniform
-            const int k = first + j0 + seg;  // this lane's record
-            const int kk = min(k, first + cnt - 1);
-            const int lo = first + j0, hi = min(first + j0 + S, first + cnt);  // this step's records
-            if (lo < bs || hi > bs + kRecBlock) {  // uniform: stage the block that holds them
-                wave_lds_sync();
-                if (lo >= bs + kRecBlock && hi <= bs + 2 * kRecBlock) {  // the prefetched one
-                    bs += kRecBlock;
-                    lrec[lane] = p0;
-                    if (lane < 32u) lrec[64 + lane] = p1;
-                } else {  // further ahead (chunks skipped): load it now
-                    bs = lo;
-                    float4 x0 = make_float4(0, 0, 0, 0), x1 = x0;
-                    fetch(bs, x0, x1);
-                    lrec[lane] = x0;
-                    if (lane < 32u) lrec[64 + lane] = x1;
-                }
-                wave_lds_sync();
-                fetch(bs + kRecBlock, p0, p1);
-            }
-            const int o3 = 3 * (kk - bs);
-            const float4 ra = lrec[o3], rb = lrec[o3 + 1], rc = lrec[o3 + 2];
-            const bool live = rvalid & (k < first + cnt);
-            const f3 v0 = mk(ra.x, ra.y, ra.z), e1 = mk(ra.w, rb.x, rb.y), e2 = mk(rb.z, rb.w, rc.x);
-            const f3 rce2 = cross(d, e2);
-            const float det = dot(e1, rce2);
-            const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
-            const f3 sv = o - v0;
-            const float u = inv_det * dot(sv, rce2);
-            const bool ok_det = !(det > -eps && det < eps), ok_lo = !(u < 0.0f), ok_hi = !(u > 1.0f);
-            if ((__builtin_amdgcn_ballot_w64(live) & __builtin_amdgcn_ballot_w64(ok_det) &
-                 __builtin_amdgcn_ballot_w64(ok_lo) & __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
-                continue;
-            const f3 sce1 = cross(sv, e1);
-            const float v = inv_det * dot(d, sce1);
-            const float t = inv_det * dot(e2, sce1);
-            const int pos = __builtin_bit_cast(int, rc.w);  // Tri::lbvh of an ltris copy: the position in the leaf
-            const bool hit = live & ok_det & ok_lo & ok_hi & !(v < 0.0f) & !(u + v > 1.0f) & (t > eps);
-            const bool take = hit & ((bk == 0x7fffffff) | (t < bt) | ((t == bt) & (pos < bk)));
-            bt = take ? t : bt;
-            bk = take ? pos : bk;
-        }
-    }
-    uint64_t key = bk == 0x7fffffff ? ~0ull : ((uint64_t)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk;
-    for (int off = 1 << lg; off < 64; off <<= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, off, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), off, 64);
-        const uint64_t other = ((uint64_t)hi << 32) | lo;
-        key = other < key ? other : key;
-    }
-    return key;
-}
-
-template <bool FAST_RCP>
-__global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, WfBuffers wb, int in_q, int cull) {
+__global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, WfBuffers wb, int in_q) {
     __shared__ uint32_t ring[kLeafPassBlock / 64][kMaxPre][kLeafRing];
     __shared__ uint32_t pos[kLeafPassBlock / 64][kMaxPre][2];  // per wave and leaf: head, tail (wave-uniform)
     __shared__ float4 lrec[kLeafPassBlock / 64][3 * kRecBlock];  // per wave: a block of leaf records
@@ -255,12 +142,8 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         float4 a = make_float4(0, 0, 0, 0), c = a;
         if (valid) { a = q[2 * (size_t)i]; c = q[2 * (size_t)i + 1]; }
         const cint_p pl = (cint_p)(sc.pre + b);
-        const int rec0 = pl[0];
-        uint64_t key;
-        if (cull && ((cint_p)(sc.tris + rec0))[11] > 0)  // uniform: the leaf has chunks (Tri::lbvh)
-            key = resolve_leaf_cull<FAST_RCP>(sc, rec0, mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec[wv]);
-        else
-            key = resolve_leaf<FAST_RCP>(sc, rec0, pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec[wv]);
+        const uint64_t key =
+            resolve_leaf<FAST_RCP>(sc, pl[0], pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec[wv]);
         if (lane < avail) wb.pres[(size_t)b * wb.pres_stride + i] = key;
     };
     // windows of wr queue entries per wave: 64, or fewer when the queue cannot give every wave a
@@ -327,16 +210,15 @@ int leafpass_blocks(const void* kernel) {
 
 }  // namespace
 
-hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks, int cull,
+hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks,
                            hipStream_t stream) {
-    cull = cull && sc.lnodes && sc.ltris;
     if (sc.npre <= 0 || !sc.pre || !wb.pres) return hipErrorInvalidValue;
     const void* k = fast_rcp ? (const void*)k_wf_leafpass<true> : (const void*)k_wf_leafpass<false>;
     const int nb = blocks > 0 ? blocks : leafpass_blocks(k);
     if (fast_rcp)
-        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<true>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q, cull);
+        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<true>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q);
     else
-        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<false>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q, cull);
+        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<false>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q);
     return hipSuccess;
 }
 
