@@ -141,6 +141,10 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         const uint32_t i = valid ? ring[wv][b][(tail + ri) & (kLeafRing - 1)] : 0u;
         float4 a = make_float4(0, 0, 0, 0), c = a;
         if (valid) { a = q[2 * (size_t)i]; c = q[2 * (size_t)i + 1]; }
+        // the ray arrives here, before resolve_leaf issues its record prefetches: otherwise the
+        // compiler's in-order vmcnt wait for the ray sits inside the entry loop and waits for the
+        // prefetch of the next record block too, every block
+        asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(c.x), "v"(c.y));
         const cint_p pl = (cint_p)(sc.pre + b);
         const uint64_t key =
             resolve_leaf<FAST_RCP>(sc, pl[0], pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec[wv]);
