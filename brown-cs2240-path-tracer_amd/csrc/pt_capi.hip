@@ -75,7 +75,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
-    {"leaf_pre", OPT_BOOL, nullptr},     {"leaf_blocks", OPT_INT, nullptr},
+    {"leaf_pre", OPT_BOOL, nullptr},     {"leaf_blocks", OPT_INT, nullptr},  {"leaf_pairs", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
     {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},   {"pool_run", OPT_ENUM, "2|4"},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
@@ -834,6 +834,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);
     lo.leaf_blocks = (int)o.num("leaf_blocks", 0);
+    lo.leaf_pairs = (int)std::min(2L, o.num("leaf_pairs", 1));
     if (o.has("trav")) {
         static const char* const names[] = {"nested", "flat1", "pred", "lean", "lean2", "lean4", "lean8", "lean16", "lean32"};
         for (int k = 0; k < 9; ++k)

@@ -73,6 +73,7 @@ struct LaunchOpts {
     int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
     int leaf_blocks = 0;   // k_wf_leafpass grid (A/B): 0 = occupancy-derived
+    int leaf_pairs = 1;    // k_wf_leafpass walks chunked leaves by (ray, chunk) pairs (option leaf_pairs)
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -145,6 +146,7 @@ struct WfStreams {
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
     int leaf_blocks = 0;   // LaunchOpts::leaf_blocks
+    int leaf_pairs = 1;    // LaunchOpts::leaf_pairs
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,
@@ -163,7 +165,7 @@ hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t 
 
 // k_wf_leafpass (pt_leafpass.hip): every big leaf of sc.pre resolved for the entries of queue in_q
 // whose rays enter its path's boxes, into wb.pres; blocks: the persistent grid (0: occupancy)
-hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks,
+hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks, int pairs,
                            hipStream_t stream);
 
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);

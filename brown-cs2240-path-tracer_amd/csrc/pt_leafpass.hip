@@ -117,11 +117,120 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
     return key;
 }
 
+// The same key for 64 rays (one per lane) of a leaf with chunks (pt_leafbvh.cpp: SceneView::lnodes,
+// ltris), testing only the entries each ray can hit.  Chunk c's node — wave-uniform, in SGPRs
+// through the scalar cache, the next one in flight — is checked by every lane against its ray
+// and its best so far (chunk_skip, pt_device.h: no entry of a skipped chunk can report a hit at t <=
+// the bound); the (ray, chunk) pairs that stay open are queued in LDS, and every 64 of them a pass
+// tests one pair per lane — the chunk's <= 8 records (ltris, copies in chunk order holding the
+// entry's position in the leaf) against the pair's ray (from the wave's LDS ray table) — and lowers
+// the ray's LDS key (f32 bits of t << 32 | position) with ds_min_u64.  chunk_leaf_multi's argument
+// (round 4): every entry able to report a hit at t <= its ray's bound at check time is tested, and
+// the bound (the ray's best so far, +inf first) never drops below the leaf's final answer, so each
+// ray ends with the smallest (t, position) over the leaf's hitting entries — the key resolve_leaf
+// computes.  Round 4 walked the chunks inside the traversal kernel at 4 waves per SIMD, a chain of
+// L2 round trips; here the checks need no memory and the passes have the kernel's other waves.
+struct PairLds {
+    float* rt;         // [6][64]: the wave's rays (o.xyz, d.xyz)
+    uint32_t* pq;      // [2][kLeafRing]: queued pairs: ray lane, (first record | count << 24)
+    uint64_t* keys;    // [64]: the rays' keys
+};
 template <bool FAST_RCP>
-__global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, WfBuffers wb, int in_q) {
+__device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int rec0, const f3 o, const f3 d, bool rvalid,
+                                                       const PairLds& L) {
+    const float eps = 1e-8f;
+    const uint32_t lane = threadIdx.x & 63u;
+    const cint_p tr0 = (cint_p)(sc.tris + rec0);
+    const int c0 = tr0[11] - 1, c1 = tr0[12 + 11];  // Tri::lbvh of the leaf's first two records
+    L.rt[lane] = o.x; L.rt[64 + lane] = o.y; L.rt[128 + lane] = o.z;
+    L.rt[192 + lane] = d.x; L.rt[256 + lane] = d.y; L.rt[320 + lane] = d.z;
+    L.keys[lane] = ~0ull;
+    wave_lds_sync();
+    Ray r;
+    r.o = o;
+    r.d = d;
+    r.inv = rcp3(d);
+    const float idl = 1.0f / sqrtf(dot(d, d));
+    const float on = sqrtf(dot(o, o));
+    float bound = __builtin_inff();
+    uint32_t head = 0, tail = 0;  // pairs queued / tested (wave-uniform)
+    const float4* __restrict__ lt = reinterpret_cast<const float4*>(sc.ltris);
+    // one pass: lane l tests queued pair tail + l (l < avail)
+    auto pass = [&](uint32_t avail) {
+        wave_lds_sync();
+        const bool has = lane < avail;
+        const uint32_t slot = (tail + lane) & (kLeafRing - 1);
+        const uint32_t ro = has ? L.pq[slot] : 0u, info = has ? L.pq[kLeafRing + slot] : 0u;
+        const int first = (int)(info & 0xffffffu), cnt = (int)(info >> 24);
+        const f3 qo = mk(L.rt[ro], L.rt[64 + ro], L.rt[128 + ro]);
+        const f3 qd = mk(L.rt[192 + ro], L.rt[256 + ro], L.rt[320 + ro]);
+        float bt = 0.0f;
+        int bk = 0x7fffffff;
+#pragma unroll 2
+        for (int e = 0; e < 8; ++e) {
+            if (e < cnt) {
+                const float4* rp = lt + 3 * (size_t)(first + e);
+                const float4 a = rp[0], b = rp[1], c = rp[2];
+                const f3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c.x);
+                const f3 rce2 = cross(qd, e2);
+                const float det = dot(e1, rce2);
+                const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
+                const f3 sv = qo - v0;
+                const float u = inv_det * dot(sv, rce2);
+                const f3 sce1 = cross(sv, e1);
+                const float v = inv_det * dot(qd, sce1);
+                const float t = inv_det * dot(e2, sce1);
+                const int k = __builtin_bit_cast(int, c.w);  // Tri::lbvh of an ltris copy: the position in the leaf
+                const bool hit = !(det > -eps && det < eps) & !(u < 0.0f) & !(u > 1.0f) & !(v < 0.0f) &
+                                 !(u + v > 1.0f) & (t > eps);
+                if (hit & ((bk == 0x7fffffff) | (t < bt) | ((t == bt) & (k < bk)))) { bt = t; bk = k; }
+            }
+        }
+        if (bk != 0x7fffffff)  // t > 1e-8: its f32 bits order as t does
+            atomicMin(reinterpret_cast<unsigned long long*>(L.keys + ro),
+                      ((unsigned long long)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk);
+        wave_lds_sync();
+        const uint64_t mk = L.keys[lane];  // this lane's ray: checks against its best so far
+        if (mk != ~0ull) bound = __builtin_bit_cast(float, (uint32_t)(mk >> 32));
+        tail += avail;
+    };
+    const cfloat_p nf = (cfloat_p)sc.lnodes;  // chunk nodes, 16 floats each, through the scalar cache
+    auto node4 = [&](int q) { return make_float4(nf[4 * q], nf[4 * q + 1], nf[4 * q + 2], nf[4 * q + 3]); };
+    float4 na = node4(4 * c0), nb = node4(4 * c0 + 1), nc = node4(4 * c0 + 2), ne = node4(4 * c0 + 3);
+    for (int c = c0; c < c1; ++c) {
+        const float4 a = na, b = nb, cc = nc, e = ne;
+        if (c + 1 < c1) {  // the next chunk's node, in flight while this one is checked
+            na = node4(4 * c + 4); nb = node4(4 * c + 5); nc = node4(4 * c + 6); ne = node4(4 * c + 7);
+        }
+        const bool open = rvalid & !chunk_skip(a, b, cc, e, r, idl, on, bound);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(open);
+        if (!m) continue;  // uniform
+        if (open) {
+            const uint32_t slot = (head + lp_rank_below(m)) & (kLeafRing - 1);
+            L.pq[slot] = lane;
+            L.pq[kLeafRing + slot] = (uint32_t)__builtin_bit_cast(int, e.w);  // the chunk's first slot | count << 24
+        }
+        head += (uint32_t)__popcll(m);
+        if (head - tail >= 64) pass(64);  // uniform (never more than 127 queued: kLeafRing)
+    }
+    if (head != tail) pass(head - tail);
+    wave_lds_sync();
+    return L.keys[lane];
+}
+
+template <bool FAST_RCP>
+__global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, WfBuffers wb, int in_q, int pairs) {
     __shared__ uint32_t ring[kLeafPassBlock / 64][kMaxPre][kLeafRing];
     __shared__ uint32_t pos[kLeafPassBlock / 64][kMaxPre][2];  // per wave and leaf: head, tail (wave-uniform)
-    __shared__ float4 lrec[kLeafPassBlock / 64][3 * kRecBlock];  // per wave: a block of leaf records
+    // per wave: a block of leaf records (resolve_leaf) or the pair walk's ray table, pair queue and
+    // keys (resolve_leaf_pairs), one region for both
+    constexpr uint32_t kScratch = 6 * 64 * 4 + 2 * kLeafRing * 4 + 64 * 8;  // 3,072 B >= 3 * kRecBlock * 16
+    static_assert(kScratch >= 3 * kRecBlock * 16, "the record block fits the pair walk's region");
+    __shared__ __attribute__((aligned(16))) char scratch[kLeafPassBlock / 64][kScratch];
+    float4* lrec = reinterpret_cast<float4*>(scratch[threadIdx.x / 64u]);
+    const PairLds pl_lds{reinterpret_cast<float*>(scratch[threadIdx.x / 64u]),
+                         reinterpret_cast<uint32_t*>(scratch[threadIdx.x / 64u] + 6 * 64 * 4),
+                         reinterpret_cast<uint64_t*>(scratch[threadIdx.x / 64u] + 6 * 64 * 4 + 2 * kLeafRing * 4)};
     const uint32_t wv = threadIdx.x / 64u, lane = threadIdx.x & 63u;
     // the queue the next traversal launch reads, as k_wf_trace reads it (a trace that gave up: nothing)
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
@@ -135,7 +244,12 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
     // rays, each over 64 >> lg lanes
     auto run = [&](int b, uint32_t tail, uint32_t avail) {
         wave_lds_sync();  // the ring's entries were written by other lanes
-        const int lg = avail > 1 ? 32 - __builtin_clz(avail - 1) : 0;  // ceil(log2 avail)
+        const cint_p pl = (cint_p)(sc.pre + b);
+        const int rec0 = pl[0];
+        // a full batch of a leaf with chunks takes the pair walk, one ray per lane (option
+        // leaf_pairs: 0 never — the whole leaf, rays spread over lanes when few; 2 at every size: tests)
+        const bool use_pairs = pairs && sc.lnodes && ((cint_p)(sc.tris + rec0))[11] > 0 && (pairs == 2 || avail == 64);
+        const int lg = use_pairs ? 6 : (avail > 1 ? 32 - __builtin_clz(avail - 1) : 0);  // ceil(log2 avail)
         const uint32_t ri = lane & ((1u << lg) - 1u);
         const bool valid = ri < avail;
         const uint32_t i = valid ? ring[wv][b][(tail + ri) & (kLeafRing - 1)] : 0u;
@@ -145,9 +259,11 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         // compiler's in-order vmcnt wait for the ray sits inside the entry loop and waits for the
         // prefetch of the next record block too, every block
         asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(c.x), "v"(c.y));
-        const cint_p pl = (cint_p)(sc.pre + b);
-        const uint64_t key =
-            resolve_leaf<FAST_RCP>(sc, pl[0], pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec[wv]);
+        uint64_t key;
+        if (use_pairs)  // uniform
+            key = resolve_leaf_pairs<FAST_RCP>(sc, rec0, mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, pl_lds);
+        else
+            key = resolve_leaf<FAST_RCP>(sc, rec0, pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec);
         if (lane < avail) wb.pres[(size_t)b * wb.pres_stride + i] = key;
     };
     // windows of wr queue entries per wave: 64, or fewer when the queue cannot give every wave a
@@ -214,15 +330,15 @@ int leafpass_blocks(const void* kernel) {
 
 }  // namespace
 
-hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks,
+hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks, int pairs,
                            hipStream_t stream) {
     if (sc.npre <= 0 || !sc.pre || !wb.pres) return hipErrorInvalidValue;
     const void* k = fast_rcp ? (const void*)k_wf_leafpass<true> : (const void*)k_wf_leafpass<false>;
     const int nb = blocks > 0 ? blocks : leafpass_blocks(k);
     if (fast_rcp)
-        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<true>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q);
+        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<true>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q, pairs);
     else
-        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<false>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q);
+        PT_LAUNCH(KID_WF_LEAF, stream, k_wf_leafpass<false>, dim3(nb), dim3(kLeafPassBlock), 0, stream, sc, wb, in_q, pairs);
     return hipSuccess;
 }
 

@@ -1066,7 +1066,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                           dim3(kTraceBlock), lds, st, sc, w, in_q, cnt, bf_slots);
             } else {
                 if constexpr (TRAV >= 260 && TRAV < 300)  // the big leaves first (k_wf_leafpass)
-                    HIP_RETURN_IF(launch_leafpass(sc, w, in_q, ((TRAV / 10) & 1) != 0, ws.leaf_blocks, st));
+                    HIP_RETURN_IF(launch_leafpass(sc, w, in_q, ((TRAV / 10) & 1) != 0, ws.leaf_blocks, ws.leaf_pairs, st));
 #define PT_TRACE(RG, PR)                                                                                        \
     do {                                                                                                        \
         if constexpr (TRAV >= 260)                                                                              \
@@ -1130,6 +1130,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;
     ws.leaf_blocks = lo.leaf_blocks;
+    ws.leaf_pairs = lo.leaf_pairs;
     if (!accum) { nframes = 1; stride = 1; }
     SceneView sc = scene;  // node_bias <= 0: chosen per instance in wf_render_t
     const bool lds = lo.lds && scene_fits_lds(sc);

@@ -92,6 +92,13 @@ def test_config4_boat_1080p_depth16_rows_bitexact(packed, ptopts):
         prof = s.profile_read()
     assert "k_wf_leafpass" not in prof, prof
     assert_same_bits(img2, img, "leaf_pre=0 vs the default (big leaves resolved before the traversal)")
+    # the leaf pass walking every leaf whole (option leaf_pairs=0; the default walks full batches of
+    # the chunked leaves by (ray, chunk) pairs)
+    ptopts.set("leaf_pre", None)
+    ptopts.set("leaf_pairs", "0")
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        img3 = s.render(p.meta_for(1920, 1080), 0, 5, 1, 16, pt_amd.MODE_AUTO)
+    assert_same_bits(img3, img, "leaf_pairs=0 vs the default")
 
 
 def test_config5_image_4096_depth8_rows_bitexact(packed):

@@ -121,9 +121,15 @@ KERNELS = {
     "wavefront_leaf4_nopre": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PRE": "0"},
     "wavefront_leaf2_div_nopre_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0",
                                          "PT_FASTRCP": "0", "PT_LEAF_PRE": "0", "PT_WF_TRACE_BLOCKS": "1"},
-    # the leaf pass with leaf BVHs forced small (the 8 largest leaves of every scene), on one block
+    # the leaf pass with leaf BVHs forced small (the 8 largest leaves of every scene), on one block;
+    # its pair walk of the chunked leaves at every batch size (option leaf_pairs=2; by default only
+    # full batches of 64 rays take it) and never (leaf_pairs=0)
     "wavefront_leaf2_div_leafpass_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0",
                                             "PT_FASTRCP": "0", "PT_LEAF_BLOCKS": "1"},
+    "wavefront_leaf4_pairs_always": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PAIRS": "2"},
+    "wavefront_leaf2_pairs_always_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0",
+                                            "PT_LEAF_PAIRS": "2", "PT_LEAF_BLOCKS": "1"},
+    "wavefront_leaf4_nopairs": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PAIRS": "0"},
 }
 
 
@@ -131,7 +137,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
             "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
-            "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS")
+            "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS")
 
 
 @pytest.fixture(params=list(KERNELS))
