@@ -123,7 +123,7 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
 // and its best so far (chunk_skip, pt_device.h: no entry of a skipped chunk can report a hit at t <=
 // the bound); the (ray, chunk) pairs that stay open are queued in LDS, and every 64 of them a pass
 // tests one pair per lane — the chunk's <= 8 records (ltris, copies in chunk order holding the
-// entry's position in the leaf) against the pair's ray (from the wave's LDS ray table) — and lowers
+// entry's position in the leaf) against the pair's ray (from its lane, ds_bpermute) — and lowers
 // the ray's LDS key (f32 bits of t << 32 | position) with ds_min_u64.  chunk_leaf_multi's argument
 // (round 4): every entry able to report a hit at t <= its ray's bound at check time is tested, and
 // the bound (the ray's best so far, +inf first) never drops below the leaf's final answer, so each
@@ -131,7 +131,6 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
 // computes.  Round 4 walked the chunks inside the traversal kernel at 4 waves per SIMD, a chain of
 // L2 round trips; here the checks need no memory and the passes have the kernel's other waves.
 struct PairLds {
-    float* rt;         // [6][64]: the wave's rays (o.xyz, d.xyz)
     uint32_t* pq;      // [2][kLeafRing]: queued pairs: ray lane, (first record | count << 24)
     uint64_t* keys;    // [64]: the rays' keys
 };
@@ -142,8 +141,6 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
     const uint32_t lane = threadIdx.x & 63u;
     const cint_p tr0 = (cint_p)(sc.tris + rec0);
     const int c0 = tr0[11] - 1, c1 = tr0[12 + 11];  // Tri::lbvh of the leaf's first two records
-    L.rt[lane] = o.x; L.rt[64 + lane] = o.y; L.rt[128 + lane] = o.z;
-    L.rt[192 + lane] = d.x; L.rt[256 + lane] = d.y; L.rt[320 + lane] = d.z;
     L.keys[lane] = ~0ull;
     wave_lds_sync();
     Ray r;
@@ -162,8 +159,9 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         const uint32_t slot = (tail + lane) & (kLeafRing - 1);
         const uint32_t ro = has ? L.pq[slot] : 0u, info = has ? L.pq[kLeafRing + slot] : 0u;
         const int first = (int)(info & 0xffffffu), cnt = (int)(info >> 24);
-        const f3 qo = mk(L.rt[ro], L.rt[64 + ro], L.rt[128 + ro]);
-        const f3 qd = mk(L.rt[192 + ro], L.rt[256 + ro], L.rt[320 + ro]);
+        auto bp = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((int)(ro << 2), __builtin_bit_cast(int, v))); };
+        const f3 qo = mk(bp(o.x), bp(o.y), bp(o.z));  // the pair's ray, from its lane
+        const f3 qd = mk(bp(d.x), bp(d.y), bp(d.z));
         float bt = 0.0f;
         int bk = 0x7fffffff;
 #pragma unroll 2
@@ -224,13 +222,12 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
     __shared__ uint32_t pos[kLeafPassBlock / 64][kMaxPre][2];  // per wave and leaf: head, tail (wave-uniform)
     // per wave: a block of leaf records (resolve_leaf) or the pair walk's ray table, pair queue and
     // keys (resolve_leaf_pairs), one region for both
-    constexpr uint32_t kScratch = 6 * 64 * 4 + 2 * kLeafRing * 4 + 64 * 8;  // 3,072 B >= 3 * kRecBlock * 16
+    constexpr uint32_t kScratch = 2 * kLeafRing * 4 + 64 * 8;  // 1,536 B >= 3 * kRecBlock * 16
     static_assert(kScratch >= 3 * kRecBlock * 16, "the record block fits the pair walk's region");
     __shared__ __attribute__((aligned(16))) char scratch[kLeafPassBlock / 64][kScratch];
     float4* lrec = reinterpret_cast<float4*>(scratch[threadIdx.x / 64u]);
-    const PairLds pl_lds{reinterpret_cast<float*>(scratch[threadIdx.x / 64u]),
-                         reinterpret_cast<uint32_t*>(scratch[threadIdx.x / 64u] + 6 * 64 * 4),
-                         reinterpret_cast<uint64_t*>(scratch[threadIdx.x / 64u] + 6 * 64 * 4 + 2 * kLeafRing * 4)};
+    const PairLds pl_lds{reinterpret_cast<uint32_t*>(scratch[threadIdx.x / 64u]),
+                         reinterpret_cast<uint64_t*>(scratch[threadIdx.x / 64u] + 2 * kLeafRing * 4)};
     const uint32_t wv = threadIdx.x / 64u, lane = threadIdx.x & 63u;
     // the queue the next traversal launch reads, as k_wf_trace reads it (a trace that gave up: nothing)
     const uint32_t count = wb.ctl[WF_WATCHDOG] ? 0u : wb.ctl[in_q ? WF_COUNT1 : WF_COUNT0];
