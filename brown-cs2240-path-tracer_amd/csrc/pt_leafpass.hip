@@ -243,9 +243,10 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         wave_lds_sync();  // the ring's entries were written by other lanes
         const cint_p pl = (cint_p)(sc.pre + b);
         const int rec0 = pl[0];
-        // a full batch of a leaf with chunks takes the pair walk, one ray per lane (option
-        // leaf_pairs: 0 never — the whole leaf, rays spread over lanes when few; 2 at every size: tests)
-        const bool use_pairs = pairs && sc.lnodes && ((cint_p)(sc.tris + rec0))[11] > 0 && (pairs == 2 || avail == 64);
+        // a batch of >= 32 rays of a leaf with chunks takes the pair walk, one ray per lane (its checks
+        // cost the same per wave whatever the batch; fewer rays walk the whole leaf spread over lanes)
+        // (option leaf_pairs: 0 never; 2 at every batch size: tests)
+        const bool use_pairs = pairs && sc.lnodes && ((cint_p)(sc.tris + rec0))[11] > 0 && (pairs == 2 || avail >= 32);
         const int lg = use_pairs ? 6 : (avail > 1 ? 32 - __builtin_clz(avail - 1) : 0);  // ceil(log2 avail)
         const uint32_t ri = lane & ((1u << lg) - 1u);
         const bool valid = ri < avail;
@@ -263,10 +264,12 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
             key = resolve_leaf<FAST_RCP>(sc, rec0, pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec);
         if (lane < avail) wb.pres[(size_t)b * wb.pres_stride + i] = key;
     };
-    // windows of wr queue entries per wave: 64, or fewer when the queue cannot give every wave a
-    // window of 64 (the last depths): then each wave's rays are few and each is walked by many lanes
+    // windows of wr queue entries per wave: 64, or fewer when the queue cannot give every other wave a
+    // window (the last depths): then each wave's rays are few and each is walked by many lanes.  (The
+    // bar is half the waves, not all: a batch of 64 rays in the pair walk costs a wave less than
+    // fewer rays walking the whole leaf, as long as the batches still fill the chip.)
     uint32_t wr = 64;
-    while (wr > 1 && (uint64_t)count < (uint64_t)nwaves * wr) wr >>= 1;
+    while (wr > 1 && 2 * (uint64_t)count < (uint64_t)nwaves * wr) wr >>= 1;
     const uint32_t nwin = (count + wr - 1) / wr;
     for (uint32_t win = w; win < nwin; win += nwaves) {
         const uint32_t i = win * wr + lane;
