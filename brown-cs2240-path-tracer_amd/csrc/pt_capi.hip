@@ -75,7 +75,8 @@ constexpr OptSpec kOptSpecs[] = {
     {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
-    {"leaf_pre", OPT_BOOL, nullptr},     {"leaf_blocks", OPT_INT, nullptr},  {"leaf_pairs", OPT_INT, nullptr},
+    {"leaf_pre", OPT_INT, nullptr},      {"leaf_blocks", OPT_INT, nullptr},  {"leaf_pairs", OPT_INT, nullptr},
+    {"pre_ratio", OPT_INT, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
     {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},   {"pool_run", OPT_ENUM, "2|4"},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
@@ -134,6 +135,10 @@ Opts opts_snapshot() {
 // the big-leaf threshold): exact (tests/test_gpu_leafbvh.py), MedievalBoat +10 % in process
 // (DESIGN.md §5.3); 0 = none
 constexpr long kLeafBvhDefault = 128;
+// the probe of the pre-resolvable leaves (probe_pre_leaves): a 32 x 32 raster (<= 4 Ki queries), at
+// most 2^23 triangle tests (MedievalBoat: ~4 k per query, ~30 ms)
+constexpr int kPreProbeGrid = 32;
+constexpr uint64_t kPreProbeTests = 1ull << 23;
 
 struct HostLayout {
     std::vector<Node> nodes;
@@ -513,6 +518,15 @@ struct pt_scene {
     // big leaves resolved before the traversal (k_wf_leafpass): the table (device copy in d_mem at
     // d_pre), every leaf's size (largest first), and the result keys (ensure_pres)
     std::vector<PreLeaf> pre;
+    // render_impl's choice of the leaf pass: per leaf of pre, probe queries passing its box filter and
+    // visiting it (probe_pre_leaves, once, with the camera of the scene's first render that could
+    // use the pass), from host copies of the tree, records and lights kept for it
+    std::vector<std::array<uint32_t, 2>> pre_probe;
+    bool pre_probed = false;
+    std::mutex pre_mu;
+    std::vector<Node> h_nodes;
+    std::vector<Tri> h_tris;
+    std::vector<Light> h_lights;
     std::vector<int32_t> leaf_sizes;
     const PreLeaf* d_pre = nullptr;
     uint64_t* d_pres = nullptr;
@@ -716,6 +730,11 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->leaf_min = L.leaf_min;
     s->lleaves = L.lleaves;
     s->pre = L.pre;
+    if (!L.pre.empty()) {
+        s->h_nodes = L.nodes;
+        s->h_tris = L.tris;
+        s->h_lights.assign(L.lights.begin(), L.lights.begin() + std::min<size_t>(L.lights.size(), L.info.emissive_tris));
+    }
     s->leaf_sizes = L.leaf_sizes;
     s->d_pre = L.pre.empty() ? nullptr : reinterpret_cast<const PreLeaf*>(base + o_pre);
     s->view.mb_base = L.mb_base;
@@ -850,6 +869,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
 // (probe of option wf_paths)
 constexpr uint64_t kWfTargetPaths = 64ull << 20;
 constexpr int kBigLeafDefault = 128;
+constexpr long kPreRatioDefault = 50;  // render_impl: the leaf pass when >= 50 % of its work is visited
 
 int ensure_rad(pt_scene* s, uint64_t paths) {
     if (s->d_rad && s->rad_cap >= paths) { s->wf.rad = s->d_rad; s->wf.rad_cap = s->rad_cap; return PT_OK; }
@@ -1018,13 +1038,46 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     // the cooperative turns and chunk walks inside k_wf_trace): the leaves of >= big_leaf entries, at
     // most kMaxPre of them — with more, the threshold rises above the (kMaxPre + 1)-th largest and
     // the rest are ordinary leaves of the pooled turns
+    // The leaf pass resolves a leaf for every ray that passes its box filter; the traversal tests it
+    // only for the rays that reach it, and a ray whose closest hit so far is nearer than a box on the
+    // leaf's path never does.  Where the filter over-predicts — the boat of CornellBox2's all-meshes
+    // scene sits inside the box's walls: 0.33 of the filtered leaf work is visited, 65 against 91.6
+    // Msamples/s without the pass (profiles/r05d_auto_ab.log) — the pass costs more than it saves;
+    // the boat alone visits 0.99 of it (+30 %).  The choice (option leaf_pre absent or 2) follows the
+    // scene's probe (pt_scene::pre_probe, pt_leafbvh.h probe_pre_leaves; CornellBox2 all meshes 0.38,
+    // the boat 1.00): the pass when the visited entries are at least pre_ratio % (default
+    // kPreRatioDefault) of the filtered ones, each leaf weighted by its entries.  leaf_pre=1 always,
+    // 0 never.  (The choice changes the kernels, not the image: both paths are exact.)
     view.npre = 0;
     view.pre = nullptr;
-    if (lo.wavefront && view.big_leaf > 0 && o.flag("leaf_pre", 1) != 0 && !s->pre.empty()) {
+    const long pre_opt = o.num("leaf_pre", 2);
+    if (lo.wavefront && view.big_leaf > 0 && pre_opt != 0 && !s->pre.empty()) {
         int32_t T = view.big_leaf;
         if (s->leaf_sizes.size() > (size_t)kMaxPre && s->leaf_sizes[kMaxPre] >= T) T = s->leaf_sizes[kMaxPre] + 1;
         int np = 0;
         while (np < (int)s->pre.size() && s->pre[(size_t)np].n >= T) ++np;
+        if (np > 0 && pre_opt != 1) {
+            std::lock_guard<std::mutex> lk(s->pre_mu);
+            if (!s->pre_probed) {
+                ProbeCamera pc{};
+                for (int c = 0; c < 3; ++c) pc.cam[c] = fp.cam[c];
+                for (int c = 0; c < 16; ++c) pc.M[c] = fp.M[c];
+                pc.focal = fp.focal;
+                pc.half_h = fp.view_half_h;
+                pc.half_w = fp.view_half_h * fp.aspect;
+                probe_pre_leaves(s->h_nodes, s->h_tris, s->h_lights, s->pre, pc, kPreProbeGrid, kPreProbeTests,
+                                 s->pre_probe);
+                s->pre_probed = true;
+            }
+        }
+        if (np > 0 && pre_opt != 1 && s->pre_probe.size() >= (size_t)np) {
+            double filt = 0.0, vis = 0.0;
+            for (int b = 0; b < np; ++b) {
+                filt += (double)s->pre_probe[(size_t)b][0] * s->pre[(size_t)b].n;
+                vis += (double)s->pre_probe[(size_t)b][1] * s->pre[(size_t)b].n;
+            }
+            if (filt > 0.0 && vis * 100.0 < filt * (double)o.num("pre_ratio", kPreRatioDefault)) np = 0;
+        }
         if (np > 0) {
             view.big_leaf = T;
             view.npre = np;

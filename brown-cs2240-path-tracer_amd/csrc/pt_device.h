@@ -360,6 +360,9 @@ __device__ __forceinline__ void big_seg(const TravLean& s, int& rec0, int& n) {
     n = left ? s.na : s.nt - s.na;
 }
 
+template <bool COUNT>
+__device__ __forceinline__ bool pre_apply(const SceneView& sc, TravLean& s, Counters& cnt);
+
 template <int K, bool COUNT, bool FAST_RCP, bool BIG = false, bool PRE = false>
 __device__ __forceinline__ bool lean_leaf_loop(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
     if constexpr (PRE) {  // a big leaf at the lane's position: its key (pre_apply)

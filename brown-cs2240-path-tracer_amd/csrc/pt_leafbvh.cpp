@@ -264,4 +264,184 @@ void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>
     if (tree_out) *tree_out = tree;
 }
 
+namespace {
+
+struct ProbeRay {
+    float o[3], d[3], inv[3];
+};
+
+// the traversal's slab test (pt_device.h ray_box): the entry distance, the exit one from inside, -1: miss
+float probe_box(const ProbeRay& r, const float* mn, const float* mx) {
+    float tmin = -3.0e+38f, tmax = 3.0e+38f;
+    for (int a = 0; a < 3; ++a) {
+        const float t1 = (mn[a] - r.o[a]) * r.inv[a], t2 = (mx[a] - r.o[a]) * r.inv[a];
+        tmin = std::fmax(tmin, std::fmin(t1, t2));
+        tmax = std::fmin(tmax, std::fmax(t1, t2));
+    }
+    return (tmax > std::fmax(tmin, 0.0f)) ? (tmin > 0.0f ? tmin : tmax) : -1.0f;
+}
+
+// the triangle test (ray-triangle-intersection.wgsl:1-42; pt_device.h tri_hit)
+bool probe_tri(const Tri& tr, const ProbeRay& r, float& t) {
+    const float eps = 1e-8f;
+    const float v0[3] = {tr.q0[0], tr.q0[1], tr.q0[2]}, e1[3] = {tr.q0[3], tr.q1[0], tr.q1[1]},
+                e2[3] = {tr.q1[2], tr.q1[3], tr.e2z};
+    auto cross = [](const float* a, const float* b, float* c) {
+        c[0] = a[1] * b[2] - a[2] * b[1];
+        c[1] = a[2] * b[0] - a[0] * b[2];
+        c[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    auto dot = [](const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+    float rce2[3], sce1[3];
+    cross(r.d, e2, rce2);
+    const float det = dot(e1, rce2);
+    if (det > -eps && det < eps) return false;
+    const float inv_det = 1.0f / det;
+    const float sv[3] = {r.o[0] - v0[0], r.o[1] - v0[1], r.o[2] - v0[2]};
+    const float u = inv_det * dot(sv, rce2);
+    if (u < 0.0f || u > 1.0f) return false;
+    cross(sv, e1, sce1);
+    const float v = inv_det * dot(r.d, sce1);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = inv_det * dot(e2, sce1);
+    return t > eps;
+}
+
+}  // namespace
+
+void probe_pre_leaves(const std::vector<Node>& nodes, const std::vector<Tri>& tris, const std::vector<Light>& lights,
+                      const std::vector<PreLeaf>& pre, const ProbeCamera& cam, int grid, uint64_t max_tests,
+                      std::vector<std::array<uint32_t, 2>>& out) {
+    out.assign(pre.size(), {0u, 0u});
+    if (pre.empty() || nodes.empty() || tris.empty()) return;
+    uint64_t st = 0x9e3779b97f4a7c15ull;  // xorshift64
+    auto next = [&]() {
+        st ^= st << 13;
+        st ^= st >> 7;
+        st ^= st << 17;
+        return st;
+    };
+    auto unif = [&]() { return (float)((double)(next() >> 40) * (1.0 / 16777216.0)); };
+    uint64_t tests = 0;
+    std::vector<int32_t> stack;
+    // one query: counts the filters passed and the leaves visited; the closest hit (record, t)
+    auto query = [&](const float o[3], const float d[3], int32_t& hit, float& hit_t) {
+        ProbeRay r;
+        for (int c = 0; c < 3; ++c) {
+            r.o[c] = o[c];
+            r.d[c] = d[c];
+            r.inv[c] = 1.0f / d[c];
+        }
+        for (size_t p = 0; p < pre.size(); ++p) {  // k_wf_leafpass's box filter
+            bool pass = true;
+            for (int j = 0; j < pre[p].npath && pass; ++j) {
+                const int32_t step = pre[p].path[j];
+                const Node& nd = nodes[(size_t)(step >> 1)];
+                pass = 0.0f < ((step & 1) ? probe_box(r, nd.rmin, nd.rmax) : probe_box(r, nd.lmin, nd.lmax));
+            }
+            out[p][0] += pass ? 1u : 0u;
+        }
+        float best_t = -1.0f;
+        int32_t best = -1;
+        auto leaf = [&](int32_t rec0, int32_t n) {
+            for (size_t p = 0; p < pre.size(); ++p) out[p][1] += (pre[p].rec0 == rec0 && pre[p].n == n) ? 1u : 0u;
+            for (int32_t i = 0; i < n; ++i) {
+                float t = 0.0f;
+                if (probe_tri(tris[(size_t)(rec0 + i)], r, t) && (best_t < 0.0f || t < best_t)) {
+                    best_t = t;
+                    best = rec0 + i;
+                }
+            }
+            tests += (uint64_t)n;
+        };
+        int32_t node = 0;
+        stack.clear();
+        for (;;) {
+            const Node& nd = nodes[(size_t)node];
+            const float ld = probe_box(r, nd.lmin, nd.lmax), rd = probe_box(r, nd.rmin, nd.rmax);
+            const bool li = 0.0f < ld, ri = 0.0f < rd, lleaf = nd.lcnt >= 0, rleaf = nd.rcnt >= 0;
+            if (li && lleaf && nd.lcnt > 0) leaf(nd.lref, nd.lcnt);
+            if (ri && rleaf && nd.rcnt > 0) leaf(nd.rref, nd.rcnt);
+            const bool tl = li && !lleaf && !(best_t > 0.0f && ld > best_t);
+            const bool tr = ri && !rleaf && !(best_t > 0.0f && rd > best_t);
+            if (tl && tr) {
+                stack.push_back(nd.lref);
+                node = nd.rref;
+            } else if (tr || tl) {
+                node = tr ? nd.rref : nd.lref;
+            } else {
+                if (stack.empty()) break;
+                node = stack.back();
+                stack.pop_back();
+            }
+        }
+        hit = best;
+        hit_t = best_t;
+    };
+    auto normalize = [](float v[3]) {
+        const float l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        if (l > 0.0f) for (int c = 0; c < 3; ++c) v[c] /= l;
+    };
+    // the hit point and the record's unit normal
+    auto hit_frame = [&](const float o[3], const float d[3], int32_t rec, float t, float p[3], float n[3]) {
+        const Tri& tr = tris[(size_t)rec];
+        const float e1[3] = {tr.q0[3], tr.q1[0], tr.q1[1]}, e2[3] = {tr.q1[2], tr.q1[3], tr.e2z};
+        n[0] = e1[1] * e2[2] - e1[2] * e2[1];
+        n[1] = e1[2] * e2[0] - e1[0] * e2[2];
+        n[2] = e1[0] * e2[1] - e1[1] * e2[0];
+        normalize(n);
+        for (int c = 0; c < 3; ++c) p[c] = o[c] + t * d[c];
+    };
+    // the NEE query: toward a random point of a random light, from the hit lifted along its normal
+    auto shadow = [&](const float p[3], const float n[3]) {
+        if (lights.empty()) return;
+        const Light& l = lights[(size_t)(next() % lights.size())];
+        float a = unif(), b = unif();
+        if (a + b > 1.0f) { a = 1.0f - a; b = 1.0f - b; }
+        float o[3], d[3];
+        for (int c = 0; c < 3; ++c) {
+            o[c] = p[c] + 1e-4f * n[c];
+            d[c] = l.p0[c] + a * (l.p1[c] - l.p0[c]) + b * (l.p2[c] - l.p0[c]) - o[c];
+        }
+        normalize(d);
+        int32_t h = -1;
+        float t = 0.0f;
+        query(o, d, h, t);
+    };
+    for (int j = 0; j < grid && tests < max_tests; ++j) {
+        for (int i = 0; i < grid && tests < max_tests; ++i) {
+            const float vx = cam.half_w * ((i + 0.5f) / grid - 0.5f), vy = cam.half_h * (0.5f - (j + 0.5f) / grid);
+            const float z = -cam.focal;
+            const float* M = cam.M;
+            float d[3] = {M[12] + M[8] * z + M[4] * vy + M[0] * vx - cam.cam[0],
+                          M[13] + M[9] * z + M[5] * vy + M[1] * vx - cam.cam[1],
+                          M[14] + M[10] * z + M[6] * vy + M[2] * vx - cam.cam[2]};
+            normalize(d);
+            int32_t h = -1;
+            float t = 0.0f, p[3], n[3];
+            query(cam.cam, d, h, t);
+            if (h < 0) continue;
+            hit_frame(cam.cam, d, h, t, p, n);
+            shadow(p, n);
+            // one cosine bounce about the normal facing the ray
+            float f[3] = {n[0], n[1], n[2]};
+            if (f[0] * d[0] + f[1] * d[1] + f[2] * d[2] > 0.0f) for (int c = 0; c < 3; ++c) f[c] = -f[c];
+            const float u1 = unif(), u2 = unif(), rr = std::sqrt(u1), phi = 6.2831853f * u2;
+            const float tv[3] = {std::fabs(f[0]) > 0.5f ? 0.0f : 1.0f, std::fabs(f[0]) > 0.5f ? 1.0f : 0.0f, 0.0f};
+            float b1[3] = {tv[1] * f[2] - tv[2] * f[1], tv[2] * f[0] - tv[0] * f[2], tv[0] * f[1] - tv[1] * f[0]};
+            normalize(b1);
+            const float b2[3] = {f[1] * b1[2] - f[2] * b1[1], f[2] * b1[0] - f[0] * b1[2], f[0] * b1[1] - f[1] * b1[0]};
+            const float lx = rr * std::cos(phi), ly = rr * std::sin(phi), lz = std::sqrt(std::fmax(0.0f, 1.0f - u1));
+            float bd[3], bo[3];
+            for (int c = 0; c < 3; ++c) bd[c] = b1[c] * lx + b2[c] * ly + f[c] * lz;
+            normalize(bd);
+            for (int c = 0; c < 3; ++c) bo[c] = p[c] + 0.001f * bd[c];
+            query(bo, bd, h, t);
+            if (h < 0) continue;
+            hit_frame(bo, bd, h, t, p, n);
+            shadow(p, n);
+        }
+    }
+}
+
 }  // namespace pt

@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <array>
 #include <vector>
 
 #include "pt_layout.h"
@@ -16,5 +17,25 @@ namespace pt {
 // depth-first order (LNode::skip = the node after its subtree; leaves: info >= 0, in chunk order).
 void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
                     int32_t& root, int32_t& end, std::vector<LNode>* tree = nullptr);
+
+// How often the rays that pass a big leaf's box filter (its path of child boxes from the root,
+// PreLeaf) go on to visit it in the reference traversal, for a render's camera: out[b] = {rays that
+// pass leaf b's filter, rays that visit it} over a stand-in of the render's queries — the camera
+// rays through the centres of a grid x grid raster of the image, from each hit a shadow ray toward
+// a random point of a random light (the NEE query) and one cosine bounce, and from the bounce's hit
+// another shadow ray (seeded, so the same scene and camera give the same counts;
+// scripts/leaf_visit_stats.c PROBE_GRID replays it through the oracle: CornellBox2 all meshes
+// 0.377 of the filtered leaf work visited against 0.335 over the render's own queries, the boat
+// 0.999 against ~0.99).  The traversal is the reference's (right child first, a child box skipped
+// once the closest hit so far is nearer than its distance; leaves in order, strict <) in plain f32.
+// Work is capped at max_tests triangle tests.
+struct ProbeCamera {
+    float cam[3];
+    float M[16];         // cam_to_world, column-major (FrameParams::M)
+    float focal, half_h, half_w;  // view plane at z = -focal, half extents
+};
+void probe_pre_leaves(const std::vector<Node>& nodes, const std::vector<Tri>& tris, const std::vector<Light>& lights,
+                      const std::vector<PreLeaf>& pre, const ProbeCamera& cam, int grid, uint64_t max_tests,
+                      std::vector<std::array<uint32_t, 2>>& out);
 
 }  // namespace pt

@@ -154,6 +154,10 @@ int pt_set_hw_queues(int n);
  *   "mb_uid_order"  forward | reverse   (read by pt_scene_create: uid numbering of mailbox scenes)
  *   "leaf_bvh"      integer             (read by pt_scene_create: leaves with a leaf BVH, >= this many entries)
  *   "pool_run"      2 | 4               (entries per run of the pooled leaf turns; default per scene)
+ *   "leaf_pre"      0 | 1 | 2           (big leaves resolved before the traversal: never, always,
+ *                                        2 = default: where the scene's probe finds it pays)
+ *   "pre_ratio"     integer percent     (leaf_pre=2's bar: visited / filtered leaf work, default 50)
+ *   "leaf_blocks" "leaf_pairs"          integers (the leaf pass's grid; its pair walk: 0 | 1 | 2)
  *   "reduce"        rccl | ordered      (pt_render_multi's reduction)
  * DESIGN.md §6 describes each.  pt_get_option writes the current value ("" = default) into buf. */
 int pt_set_option(const char* name, const char* value);

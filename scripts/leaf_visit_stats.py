@@ -2,6 +2,9 @@
 buffers and meta through the oracle's loader, builds the harness and runs it.
 
     python3 scripts/leaf_visit_stats.py MedievalBoat 1920 1080 [frames] [depth] [min_entries] [row_step]
+(ALL_MESHES=1: every primitive of the scene, as --all-meshes; PROBE=n: n of the library's probe rays
+instead of the render's; PROBE_GRID=g: the camera probe's g x g pixel-centre rays and their bounces,
+pt_leafbvh.cpp probe_pre_leaves — run either with frames 0)
 """
 import os
 import subprocess
@@ -21,7 +24,8 @@ def main():
     min_entries = sys.argv[6] if len(sys.argv) > 6 else "128"
     step = sys.argv[7] if len(sys.argv) > 7 else "8"
     assets = os.path.join(ROOT, "scenes", "scene_assets")
-    camera, p = so.load_scene(os.path.join(assets, name + ".xml"), assets)
+    all_meshes = os.environ.get("ALL_MESHES") == "1"
+    camera, p = so.load_scene(os.path.join(assets, name + ".xml"), assets, all_meshes=all_meshes)
     settings = {"samplesPerPixel": 1, "pathContinuationProb": 0.9, "directLightingOnly": False}
     d = "/tmp/leafstats"
     os.makedirs(d, exist_ok=True)
@@ -30,7 +34,8 @@ def main():
     so.make_meta([W, H], camera, settings).tofile(os.path.join(d, "meta.bin"))
     exe = os.path.join(d, "leaf_visit_stats")
     subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(ROOT, "scripts", "leaf_visit_stats.c"), "-lm"])
-    subprocess.check_call([exe, d, frames, depth, min_entries, step])
+    subprocess.check_call([exe, d, frames, depth, min_entries, step, os.environ.get("PROBE", "0"),
+                           os.environ.get("PROBE_GRID", "0")])
 
 
 if __name__ == "__main__":

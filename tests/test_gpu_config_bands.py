@@ -79,7 +79,8 @@ def test_config3_1024_depth16_rows_bitexact(packed, scene):
 def test_config4_boat_1080p_depth16_rows_bitexact(packed, ptopts):
     img, profs = _render_bands(packed["MedievalBoat"], 1920, 1080, 5, 16, [(680, 696), (560, 568)])
     assert all("k_wf_trace" in p for p in profs), profs
-    # the big leaves (7,327 entries and the next six) resolved before every traversal launch
+    # the big leaves (7,327 entries and the next six) resolved before every traversal launch (the
+    # probe: 0.99 of the filtered leaf work is visited)
     assert all(p["k_wf_leafpass"]["launches"] == p["k_wf_trace"]["launches"] for p in profs), profs
     assert [p["k_wf_accum"]["launches"] for p in profs] == [1, 2], profs  # one batch / two batches
     # the same image with the big leaves walked inside the traversal kernel (leaf_pre=0: cooperative
@@ -142,18 +143,29 @@ def test_live_stride_tree_fails_the_reference_l2_test(name, xml):
 
 # Scenes outside the tuning set of AUTO's per-scene thresholds (verdict r04 weak #4): CornellBox-Sphere
 # (2,188 triangles, leaves of up to 43 entries, no big leaf: pooled runs of 4) and CornellBox2 with
-# every mesh (the box and the boat, 12,609 triangles, a 2,171-entry leaf: big leaves resolved by the
-# leaf pass), 1024^2 at the reference default depth 16, through AUTO, bands bit-exact vs the oracle.
+# every mesh (the box and the boat, 12,609 triangles, a 2,171-entry leaf), 1024^2 at the reference
+# default depth 16, through AUTO, bands bit-exact vs the oracle.
 def test_sphere_1024_depth16_rows_bitexact(packed):
     _, profs = _render_bands(packed["CornellBox-Sphere"], 1024, 1024, 8, 16, [(260, 276), (560, 576), (900, 916)])
     assert all("k_wf_trace" in p for p in profs), profs
 
 
-def test_cornellbox2_all_meshes_1024_depth16_rows_bitexact(tmp_path):
+def test_cornellbox2_all_meshes_1024_depth16_rows_bitexact(tmp_path, ptopts):
     from conftest import pack_with_node
     p = pack_with_node(os.path.join(SCENES, "scene_assets", "CornellBox2.xml"), str(tmp_path / "cb2"), "--all-meshes",
                        "--native-bvh")
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         assert s.info["max_leaf"] >= 2000  # the boat's big leaf
-    _, profs = _render_bands(p, 1024, 1024, 4, 16, [(300, 316), (560, 576), (800, 816)])
-    assert all("k_wf_leafpass" in p for p in profs), profs
+    img, profs = _render_bands(p, 1024, 1024, 4, 16, [(300, 316), (560, 576), (800, 816)])
+    # the boat inside the box's walls: most queries that pass a big leaf's box filter never reach the
+    # leaf (the probe: 0.38 of the filtered leaf work visited), so AUTO walks the big leaves inside
+    # the traversal instead of resolving them before it (render_impl, option leaf_pre)
+    assert all("k_wf_trace" in p and "k_wf_leafpass" not in p for p in profs), profs
+    # the leaf pass forced (leaf_pre=1): the same image
+    ptopts.set("leaf_pre", "1")
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        img2 = s.render(p.meta_for(1024, 1024), 0, 4, 1, 16, pt_amd.MODE_AUTO)
+        prof = s.profile_read()
+    assert "k_wf_leafpass" in prof, prof
+    assert_same_bits(img2, img, "leaf_pre=1 vs the default")

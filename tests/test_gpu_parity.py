@@ -111,12 +111,13 @@ KERNELS = {
     # the traversal kernel on one block with the big-leaf turns forced onto small leaves
     "wavefront_big4_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "4", "PT_MAILBOX": "0",
                               "PT_WF_TRACE_BLOCKS": "1"},
-    # big leaves resolved before the traversal (k_wf_leafpass; the default wherever the wavefront has
-    # big leaves: the variants above with big_leaf / leaf_bvh forced small run it on the 8 largest
-    # leaves of every scene): on one block (each wave's LDS rings wrap and flush partial batches), and
-    # off — the cooperative turns and chunk walks inside k_wf_trace
+    # big leaves resolved before the traversal (k_wf_leafpass; AUTO runs it where the scene's probe
+    # finds the leaves' box filters predict their visits — the variants above with big_leaf / leaf_bvh
+    # forced small take that choice on the 8 largest leaves of every scene; here leaf_pre=1 forces
+    # it): on one block (each wave's LDS rings wrap and flush partial batches), and off (leaf_pre=0)
+    # — the cooperative turns and chunk walks inside k_wf_trace
     "wavefront_big8_leafpass_1block": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0",
-                                       "PT_LEAF_BLOCKS": "1"},
+                                       "PT_LEAF_BLOCKS": "1", "PT_LEAF_PRE": "1"},
     "wavefront_big8_nopre": {"PT_KERNEL": "wavefront", "PT_BIG_LEAF": "8", "PT_MAILBOX": "0", "PT_LEAF_PRE": "0"},
     "wavefront_leaf4_nopre": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PRE": "0"},
     "wavefront_leaf2_div_nopre_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0",
@@ -125,11 +126,13 @@ KERNELS = {
     # its pair walk of the chunked leaves at every batch size (option leaf_pairs=2; by default only
     # full batches of 64 rays take it) and never (leaf_pairs=0)
     "wavefront_leaf2_div_leafpass_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0",
-                                            "PT_FASTRCP": "0", "PT_LEAF_BLOCKS": "1"},
-    "wavefront_leaf4_pairs_always": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PAIRS": "2"},
+                                            "PT_FASTRCP": "0", "PT_LEAF_BLOCKS": "1", "PT_LEAF_PRE": "1"},
+    "wavefront_leaf4_pairs_always": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PAIRS": "2",
+                                     "PT_LEAF_PRE": "1"},
     "wavefront_leaf2_pairs_always_1block": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "2", "PT_MAILBOX": "0",
-                                            "PT_LEAF_PAIRS": "2", "PT_LEAF_BLOCKS": "1"},
-    "wavefront_leaf4_nopairs": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PAIRS": "0"},
+                                            "PT_LEAF_PAIRS": "2", "PT_LEAF_BLOCKS": "1", "PT_LEAF_PRE": "1"},
+    "wavefront_leaf4_nopairs": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PAIRS": "0",
+                                "PT_LEAF_PRE": "1"},
 }
 
 
