@@ -601,7 +601,7 @@ __device__ __forceinline__ void chunk_leaf(const SceneView& sc, const Ray& q, in
         // the next while this one is tested) costs the trace kernel 14 VGPRs and a wave per SIMD,
         // measured slower on the boat (profiles/r04g_ab_chunkwalk.log, r04h_ab_chunkwalk.log)
 #pragma unroll 2
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < kChunkMax; ++e) {
             if (e < cnt) {
                 const Tri* rec = sc.ltris + first + e;
                 const int k = rec->lbvh;
@@ -697,7 +697,7 @@ __device__ __forceinline__ void chunk_leaf_multi(const SceneView& sc, const Ray&
         float bt = __builtin_inff();
         int bk = 0x7fffffff;
 #pragma unroll 2
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < kChunkMax; ++e) {
             if (e < cnt_l) {
                 const Tri* rec = sc.ltris + first + e;
                 const int k = rec->lbvh;

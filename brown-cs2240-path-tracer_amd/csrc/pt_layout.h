@@ -64,6 +64,12 @@ inline void tri_set(Tri& t, const float v0[3], const float e1[3], const float e2
 }
 static_assert(sizeof(Tri) == 48, "tri record is 3 x 16 B");
 
+// entries per leaf chunk (LNode; build_leaf_bvh's leaf size, the chunk walks' test loops)
+#ifndef PT_LEAF_CHUNK
+#define PT_LEAF_CHUNK 8
+#endif
+constexpr int kChunkMax = PT_LEAF_CHUNK;
+
 // Leaf chunk (pt_leafbvh.cpp): up to 8 entries of one big leaf of the reference tree, grouped by
 // position and normal direction.  A chunk is skipped only when none of its entries can report a
 // hit at t <= the closest t so far: the ray misses, or enters late, the chunk's box grown by

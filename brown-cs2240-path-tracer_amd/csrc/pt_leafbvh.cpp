@@ -30,10 +30,7 @@ namespace {
 constexpr double kEps = 5.9604644775390625e-8;  // 2^-24
 constexpr double kK1 = 216.0, kK2 = 98.0;       // the rounding bound's coefficients (with the factor 2)
 constexpr double kThin = 0.05;                  // s_i below this: the thin group
-#ifndef PT_LEAF_CHUNK
-#define PT_LEAF_CHUNK 8
-#endif
-constexpr int kLeafMax = PT_LEAF_CHUNK;         // entries per chunk (leaf node of the build tree)
+constexpr int kLeafMax = kChunkMax;             // entries per chunk (leaf node of the build tree)
 constexpr int kBins = 16;
 
 struct Item {

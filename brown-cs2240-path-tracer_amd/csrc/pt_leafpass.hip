@@ -165,7 +165,7 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         float bt = 0.0f;
         int bk = 0x7fffffff;
 #pragma unroll 2
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < kChunkMax; ++e) {
             if (e < cnt) {
                 const float4* rp = lt + 3 * (size_t)(first + e);
                 const float4 a = rp[0], b = rp[1], c = rp[2];
