@@ -110,6 +110,47 @@ int main(int argc, char** argv) {
                 cone / R, box / R, tests / R, bad);
     std::printf("chunk_leaf wave-steps ~%.0f (checks %d + tests %.1f); cooperative turn %d\n",
                 (nc + 63) / 64 + open / R / 8, (nc + 63) / 64, open / R / 8, (n + 63) / 64);
+    // a walk of the whole build tree per ray (DFS order, skip links): nodes checked per ray, and the
+    // most any ray of a group of 64 checks (a wave walking its 64 rays in lockstep runs that long)
+    {
+        std::vector<LNode> tch, tree;
+        std::vector<int32_t> tl;
+        int32_t r0 = 0, r1 = 0;
+        build_leaf_bvh(tris.data(), 0, n, tch, tl, r0, r1, &tree);
+        std::mt19937 rng2(7);
+        double vis = 0, vmax = 0, opened = 0;
+        for (int g = 0; g < R / 64; ++g) {
+            double gm = 0;
+            for (int r = 0; r < 64; ++r) {
+                const int k = (int)(rng2() % (unsigned)n);
+                float bu = U(rng2), bv = U(rng2);
+                if (bu + bv > 1) { bu = 1 - bu; bv = 1 - bv; }
+                const Tri& T = tris[(size_t)k];
+                const float P[3] = {T.q0[0] + bu * T.q0[3] + bv * T.q1[2], T.q0[1] + bu * T.q1[0] + bv * T.q1[3],
+                                    T.q0[2] + bu * T.q1[1] + bv * T.e2z};
+                const float o[3] = {P[0] + 10 * U(rng2) - 5, P[1] + 10 * U(rng2) - 5, P[2] + 10 * U(rng2) - 5};
+                float d[3] = {N(rng2), N(rng2), N(rng2)};
+                const float l = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+                for (int a = 0; a < 3; ++a) d[a] /= l;
+                const float inv[3] = {1.0f / d[0], 1.0f / d[1], 1.0f / d[2]};
+                const float on = std::sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+                int v = 0;
+                for (size_t i = 0; i < tree.size();) {
+                    const LNode& q = tree[i];
+                    ++v;
+                    if (!chunk_skip(q, o, d, inv, on, INFINITY)) { i = (size_t)q.skip; continue; }
+                    if (q.info >= 0) ++opened;
+                    ++i;
+                }
+                vis += v;
+                gm = std::max(gm, (double)v);
+            }
+            vmax += gm;
+        }
+        const int G = R / 64;
+        std::printf("tree walk: %zu nodes; per ray %.1f checked (%.1f leaves open), max of 64 rays %.1f (flat: %d)\n",
+                    tree.size(), vis / (G * 64), opened / (G * 64), vmax / G, nc);
+    }
     int hist[10] = {0};
     for (int c = root; c < end; ++c) hist[std::min(9, (int)(ch[(size_t)c].sa * 10.0f))]++;
     for (int b = 0; b < 10; ++b) std::printf("chunks with cone sine in [%.1f, %.1f): %d\n", b / 10.0, (b + 1) / 10.0, hist[b]);
