@@ -299,19 +299,45 @@ def main():
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     # the step ends with the accumulator on the host ("from the first kernel launch to
     # the accumulator on the host"; the reference copies it to a MAP_READ buffer each frame,
-    # program-raymarch.ts:262-293): rank 0 copies the reduced accumulator to pinned host memory
-    host_acc = torch.empty((H, W, 3), dtype=torch.float32, pin_memory=True) if rank == 0 else None
+    # program-raymarch.ts:262-293): rank 0 copies the reduced accumulator to pinned host memory.
+    # Two accumulators: step k renders into slot k % 2 while a copy stream brings step k - 1's to the
+    # host (readback pipelined with the next step's render, ~0.23 ms of PCIe per 12 MB at 1024^2 —
+    # 2 % of a rank's share of an 8-GPU run, profiles/r05o_share.log); every step's copy completes
+    # inside the timed region, which ends with both streams drained.
+    accs = [acc, torch.zeros_like(acc)]
+    hosts = ([torch.empty((H, W, 3), dtype=torch.float32, pin_memory=True) for _ in range(2)] if rank == 0
+             else [None, None])
+    copy_stream = torch.cuda.Stream(device=dev)
+    slot_free = [None, None]  # per slot: the event after which its accumulator may be zeroed again
+    nstep = [0]
 
-    def to_host():
-        if host_acc is not None:
-            host_acc.copy_(acc, non_blocking=True)
-
-    def step():
+    def step(ev0=None, ev1=None):
+        k = nstep[0] % 2
+        nstep[0] += 1
+        a = accs[k]
         with torch.cuda.stream(stream):
-            acc.zero_()
-            scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
-            reduce_accum(acc, dist)
-            to_host()
+            if slot_free[k] is not None:
+                stream.wait_event(slot_free[k])  # step k - 2's host copy of this slot is done
+            a.zero_()
+            if ev0 is not None:
+                ev0.record(stream)
+            scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, a.data_ptr(), stream.cuda_stream)
+            if ev1 is not None:
+                ev1.record(stream)
+            reduce_accum(a, dist)
+            done = torch.cuda.Event()
+            done.record(stream)
+        if hosts[k] is not None:
+            with torch.cuda.stream(copy_stream):
+                copy_stream.wait_event(done)
+                hosts[k].copy_(a, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(copy_stream)
+        slot_free[k] = done
+
+    def drain():
+        stream.synchronize()
+        copy_stream.synchronize()
 
     # work counters for the roofline's algorithmic bytes (separate pass, not timed)
     cnt = torch.zeros(6, dtype=torch.int64, device=dev)
@@ -329,7 +355,7 @@ def main():
     scene.profile_enable(True)
     for _ in range(args.warmup):
         step()
-    stream.synchronize()
+    drain()
     prof_warm = scene.profile_read()
     scene.profile_enable(False)
     dominant = max(prof_warm, key=lambda k: prof_warm[k]["total_ms"]) if prof_warm else None
@@ -343,14 +369,8 @@ def main():
     scene.profile_enable(not args.no_kernel_timing and dominant is not None)
     t0 = time.perf_counter()
     for ev0, ev1 in evs:
-        with torch.cuda.stream(stream):
-            acc.zero_()
-            ev0.record(stream)
-            scene.render_async(meta, frame0, nframes, fstride, args.depth, mode, acc.data_ptr(), stream.cuda_stream)
-            ev1.record(stream)
-            reduce_accum(acc, dist)
-            to_host()
-    stream.synchronize()
+        step(ev0, ev1)
+    drain()
     render_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
     if world > 1:
         dist.barrier()
@@ -429,7 +449,8 @@ def main():
                                                                         if world > 1 else ""),
                        "mode": args.mode, "bvh": args.bvh, "samples_per_step": total_samples,
                        "timed_to": "accumulator on the host (rank 0: pinned device-to-host copy after the "
-                                   "reduce, inside each timed step)",
+                                   "reduce, every step's inside the timed region; step k's copy overlaps step "
+                                   "k + 1's render, two accumulators)",
                        "ranks": ranks_seen, "backend": backend if world > 1 else None,
                        "options": dict(kv.partition("=")[::2] for kv in args.opt) or None,
                        "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size),
