@@ -76,7 +76,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"leaf_pre", OPT_INT, nullptr},      {"leaf_blocks", OPT_INT, nullptr},  {"leaf_pairs", OPT_INT, nullptr},
-    {"pre_ratio", OPT_INT, nullptr},
+    {"pre_ratio", OPT_INT, nullptr},     {"leaf_refine", OPT_BOOL, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
     {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},   {"pool_run", OPT_ENUM, "2|4"},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
@@ -152,6 +152,7 @@ struct HostLayout {
     std::vector<LNode> lnodes;    // leaf BVHs (SceneView::lnodes), and per such leaf (first record, entries, nodes)
     std::vector<int32_t> lidx;
     std::vector<Tri> ltris;       // per chunk slot: its entry's record, lbvh = the entry's position in its leaf
+    std::vector<float4> lnorm;    // per chunk slot: its entry's unit normal (SceneView::lnorm)
     std::vector<std::array<int32_t, 3>> lleaves;
     int32_t leaf_min = 0;         // leaves of at least this many entries have one (option leaf_bvh; 0: none)
     std::vector<PreLeaf> pre;     // the kMaxPre largest leaves with their paths (SceneView::pre), largest first
@@ -358,6 +359,14 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                     Tri t = L.tris[(size_t)(lr.first + L.lidx[j])];
                     t.lbvh = L.lidx[j];
                     L.ltris.push_back(t);
+                    // the entry's normal in double, rounded (the pass's check allows 1e-5 for it)
+                    const double e1[3] = {t.q0[3], t.q1[0], t.q1[1]}, e2[3] = {t.q1[2], t.q1[3], t.e2z};
+                    const double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                                          e1[0] * e2[1] - e1[1] * e2[0]};
+                    const double ln = std::sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+                    const bool ok = ln > 0.0 && std::isfinite(ln);
+                    L.lnorm.push_back(make_float4(ok ? (float)(nv[0] / ln) : 0.0f, ok ? (float)(nv[1] / ln) : 0.0f,
+                                                  ok ? (float)(nv[2] / ln) : 0.0f, 0.0f));
                 }
                 L.tris[(size_t)lr.first].lbvh = root + 1;
                 L.tris[(size_t)lr.first + 1].lbvh = end;
@@ -683,7 +692,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
     const size_t o_lnode = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
-    const size_t o_pre = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
+    const size_t o_lnorm = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
+    const size_t o_pre = align_up(o_lnorm + std::max<size_t>(1, L.lnorm.size()) * sizeof(float4), 256);
     const size_t total = align_up(o_pre + std::max<size_t>(1, L.pre.size()) * sizeof(PreLeaf), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
@@ -700,6 +710,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
         up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess ||
+        up(o_lnorm, L.lnorm.data(), L.lnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_pre, L.pre.data(), L.pre.size() * sizeof(PreLeaf)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
@@ -727,6 +738,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.vnormals = 0;
     s->view.lnodes = L.lnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_lnode);
     s->view.ltris = L.lnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_lidx);
+    s->view.lnorm = L.lnodes.empty() ? nullptr : reinterpret_cast<const float4*>(base + o_lnorm);
     s->leaf_min = L.leaf_min;
     s->lleaves = L.lleaves;
     s->pre = L.pre;
@@ -853,7 +865,9 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);
     lo.leaf_blocks = (int)o.num("leaf_blocks", 0);
-    lo.leaf_pairs = (int)std::min(2L, o.num("leaf_pairs", 1));
+    // | 4: the pair walk's second check of the open chunks with the entries' own normals (option
+    // leaf_refine, default on; pt_leafpass.hip)
+    lo.leaf_pairs = (int)std::max(0L, std::min(2L, o.num("leaf_pairs", 1))) | (o.flag("leaf_refine", 1) != 0 ? 4 : 0);
     if (o.has("trav")) {
         static const char* const names[] = {"nested", "flat1", "pred", "lean", "lean2", "lean4", "lean8", "lean16", "lean32"};
         for (int k = 0; k < 9; ++k)

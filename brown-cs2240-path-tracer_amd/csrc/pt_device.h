@@ -547,15 +547,13 @@ __device__ __forceinline__ float wave_min_t(float t) {
 // so every operand of the check is used unconditionally and the node's four loads issue together
 // (with the returns the compiler sank the last load into the branch: two memory round trips per
 // check); a lane whose escape holds computes the box on meaningless values and is not skipped.
-__device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const float4 c, const float4 e, const Ray& r,
-                                           float idl, float on, float bound) {
-    // |cos(d, n)| >= cos(angle(d, axis) + half-angle) over the chunk's normals, less a slack for
-    // this arithmetic's rounding (the reciprocals here are within 1 ulp; the slack is 1e-5)
-    const float cb = fabsf(r.d.x * a.w + r.d.y * b.w + r.d.z * c.x) * idl;
-    const float sb = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cb * cb));
-    const float cf = cb * c.y - sb * c.z - 1e-5f;
+// chunk_box_skip: the same rule for a given lower bound cf of |cos(d, n)| over the chunk's entries
+// (B = c.w of the node); chunk_skip takes cf from the chunk's cone, the leaf pass also from the
+// entries' own normals (pt_leafpass.hip)
+__device__ __forceinline__ bool chunk_box_skip(const float4 a, const float4 b, const float4 e, float B, const Ray& r,
+                                               float on, float bound, float cf) {
     // delta, rounded up by 1e-5 relative against the approximate reciprocal
-    const float dl = (e.x + c.w * on) * __builtin_amdgcn_rcpf(cf) * 1.00001f + 1e-5f * on + e.y;
+    const float dl = (e.x + B * on) * __builtin_amdgcn_rcpf(cf) * 1.00001f + 1e-5f * on + e.y;
     const bool bounded = (cf > 1e-4f) & (dl < 1e30f);
     float tn = -3.0e38f, tf = 3.0e38f;
     float t1 = (a.x - dl - r.o.x) * r.inv.x, t2 = (b.x + dl - r.o.x) * r.inv.x;
@@ -568,6 +566,15 @@ __device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const
     tn = fmaxf(tn, fminf(t1, t2));
     tf = fminf(tf, fmaxf(t1, t2));
     return bounded & ((tf < tn) | (tf < 0.0f) | (tn > bound));
+}
+__device__ __forceinline__ bool chunk_skip(const float4 a, const float4 b, const float4 c, const float4 e, const Ray& r,
+                                           float idl, float on, float bound) {
+    // |cos(d, n)| >= cos(angle(d, axis) + half-angle) over the chunk's normals, less a slack for
+    // this arithmetic's rounding (the reciprocals here are within 1 ulp; the slack is 1e-5)
+    const float cb = fabsf(r.d.x * a.w + r.d.y * b.w + r.d.z * c.x) * idl;
+    const float sb = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cb * cb));
+    const float cf = cb * c.y - sb * c.z - 1e-5f;
+    return chunk_box_skip(a, b, e, c.w, r, on, bound, cf);
 }
 
 // The leaf whose records start at rec0, for ONE ray q (wave-uniform: every lane holds it), by

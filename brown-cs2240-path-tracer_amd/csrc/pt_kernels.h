@@ -73,7 +73,7 @@ struct LaunchOpts {
     int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
     int leaf_blocks = 0;   // k_wf_leafpass grid (A/B): 0 = occupancy-derived
-    int leaf_pairs = 1;    // k_wf_leafpass walks chunked leaves by (ray, chunk) pairs (option leaf_pairs)
+    int leaf_pairs = 5;    // k_wf_leafpass walks chunked leaves by (ray, chunk) pairs (option leaf_pairs; | 4: leaf_refine)
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -146,7 +146,7 @@ struct WfStreams {
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
     int leaf_blocks = 0;   // LaunchOpts::leaf_blocks
-    int leaf_pairs = 1;    // LaunchOpts::leaf_pairs
+    int leaf_pairs = 5;    // LaunchOpts::leaf_pairs
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

@@ -160,6 +160,9 @@ struct SceneView {
     // in its leaf (ltris: one load per test, no index indirection)
     const LNode* lnodes;
     const Tri* ltris;
+    // per chunk slot: its entry's unit normal (x, y, z, 0; zero when degenerate), for the leaf
+    // pass's second check of a chunk the cone could not skip (pt_leafpass.hip)
+    const float4* lnorm;
     // leaf turns of the traversal kernel pool the leaf lanes' entries over the wave (lean_leaf_pool;
     // every tree by default, option leaf_pool).  The value is the run length (2 or 4; 0: off),
     // chosen per scene by pt_capi.hip, option pool_run

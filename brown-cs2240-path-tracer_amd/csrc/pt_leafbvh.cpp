@@ -32,6 +32,9 @@ constexpr double kK1 = 216.0, kK2 = 98.0;       // the rounding bound's coeffici
 constexpr double kThin = 0.05;                  // s_i below this: the thin group
 constexpr int kLeafMax = kChunkMax;             // entries per chunk (leaf node of the build tree)
 constexpr int kBins = 16;
+#ifndef PT_LEAF_CONE_WEIGHT
+#define PT_LEAF_CONE_WEIGHT 2.0  // the split cost's weight of a child without a bound (below)
+#endif
 
 struct Item {
     double lo[3], hi[3], c[3], n[3];  // box, centroid, unit normal (zero when degenerate)
@@ -176,7 +179,7 @@ void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<
                     // a cone without a bound opens the child for every ray that meets the leaf's
                     // box, not just those meeting the child's: weighted 2 (scripts/leafbvh_harness.cpp:
                     // open chunks per ray 264 -> 174 on the boat; 4 and 8 weigh worse)
-                    cost += (double)cnt[h] * std::min(1.0, 2.0 * sn + (1.0 - sn) * std::min(1.0, area(lo2[h], hi2[h]) / AN));
+                    cost += (double)cnt[h] * std::min(1.0, PT_LEAF_CONE_WEIGHT * sn + (1.0 - sn) * std::min(1.0, area(lo2[h], hi2[h]) / AN));
                 }
                 if (cost < best) { best = cost; bkind = kind; bax = ax; bsplit = s; bkmin = kmin; bkext = kext; }
             }

@@ -121,22 +121,31 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
 // ltris), testing only the entries each ray can hit.  Chunk c's node — wave-uniform, in SGPRs
 // through the scalar cache, the next one in flight — is checked by every lane against its ray
 // and its best so far (chunk_skip, pt_device.h: no entry of a skipped chunk can report a hit at t <=
-// the bound); the (ray, chunk) pairs that stay open are queued in LDS, and every 64 of them a pass
-// tests one pair per lane — the chunk's <= 8 records (ltris, copies in chunk order holding the
-// entry's position in the leaf) against the pair's ray (from its lane, ds_bpermute) — and lowers
-// the ray's LDS key (f32 bits of t << 32 | position) with ds_min_u64.  chunk_leaf_multi's argument
-// (round 4): every entry able to report a hit at t <= its ray's bound at check time is tested, and
-// the bound (the ray's best so far, +inf first) never drops below the leaf's final answer, so each
-// ray ends with the smallest (t, position) over the leaf's hitting entries — the key resolve_leaf
-// computes.  Round 4 walked the chunks inside the traversal kernel at 4 waves per SIMD, a chain of
-// L2 round trips; here the checks need no memory and the passes have the kernel's other waves.
+// the bound).  The (ray, chunk) pairs that stay open are queued in LDS (chunk << 6 | the ray's lane)
+// and every 64 of them a pass tests one pair per lane — the chunk's <= 8 records (ltris, copies in
+// chunk order holding the entry's position in the leaf) against the pair's ray (from its lane,
+// ds_bpermute) — and lowers the ray's LDS key (f32 bits of t << 32 | position) with ds_min_u64.
+// REFINE: a chunk stays open for a ray mostly because its normal cone admits a direction
+// perpendicular to the ray (a grazing ray: the rounding bound is infinite) — 171 of the ~174 chunks a
+// boat ray opens (scripts/leafbvh_harness.cpp) — although its actual entries' |cos(d, n)| is
+// rarely that small.  So open pairs queue first for a second check, one pair per lane, with cf =
+// min over the chunk's entries of |d . n_i| (SceneView::lnorm, less the same 1e-5 slack) in place of
+// the cone's bound and the pair's ray's current best as the bound (chunk_box_skip): the harness
+// keeps 4.8 chunks open per ray.  Only the pairs that survive it are tested.
+// chunk_leaf_multi's argument (round 4): every entry able to report a hit at t <= its ray's bound at
+// check time is tested (cf <= |cos(d, n_i)| for each entry is all the rule needs, whether from the
+// cone or from the entries), and the bound (the ray's best so far, +inf first) never drops below the
+// leaf's final answer, so each ray ends with the smallest (t, position) over the leaf's hitting
+// entries — the key resolve_leaf computes.  Round 4 walked the chunks inside the traversal kernel at
+// 4 waves per SIMD, a chain of L2 round trips; here the checks need no memory and the passes have
+// the kernel's other waves.
 struct PairLds {
-    uint32_t* pq;      // [2][kLeafRing]: queued pairs: ray lane, (first record | count << 24)
+    uint32_t* pq;      // [2][kLeafRing]: queued pairs (chunk << 6 | ray lane): to check again, to test
     uint64_t* keys;    // [64]: the rays' keys
 };
 template <bool FAST_RCP>
 __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int rec0, const f3 o, const f3 d, bool rvalid,
-                                                       const PairLds& L) {
+                                                       const PairLds& L, bool refine) {
     const float eps = 1e-8f;
     const uint32_t lane = threadIdx.x & 63u;
     const cint_p tr0 = (cint_p)(sc.tris + rec0);
@@ -150,18 +159,25 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
     const float idl = 1.0f / sqrtf(dot(d, d));
     const float on = sqrtf(dot(o, o));
     float bound = __builtin_inff();
-    uint32_t head = 0, tail = 0;  // pairs queued / tested (wave-uniform)
+    uint32_t* qa = L.pq;               // pairs to check again (refine)
+    uint32_t* qb = L.pq + kLeafRing;   // pairs to test
+    uint32_t ha = 0, ta = 0, hb = 0, tb = 0;  // pushed / taken (wave-uniform)
     const float4* __restrict__ lt = reinterpret_cast<const float4*>(sc.ltris);
-    // one pass: lane l tests queued pair tail + l (l < avail)
+    const float4* __restrict__ ln4 = reinterpret_cast<const float4*>(sc.lnodes);
+    auto bp = [](float v, uint32_t ro) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((int)(ro << 2), __builtin_bit_cast(int, v)));
+    };
+    // one pass: lane l tests queued pair tb + l (l < avail)
     auto pass = [&](uint32_t avail) {
         wave_lds_sync();
         const bool has = lane < avail;
-        const uint32_t slot = (tail + lane) & (kLeafRing - 1);
-        const uint32_t ro = has ? L.pq[slot] : 0u, info = has ? L.pq[kLeafRing + slot] : 0u;
-        const int first = (int)(info & 0xffffffu), cnt = (int)(info >> 24);
-        auto bp = [&](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((int)(ro << 2), __builtin_bit_cast(int, v))); };
-        const f3 qo = mk(bp(o.x), bp(o.y), bp(o.z));  // the pair's ray, from its lane
-        const f3 qd = mk(bp(d.x), bp(d.y), bp(d.z));
+        const uint32_t item = has ? qb[(tb + lane) & (kLeafRing - 1)] : 0u;
+        const uint32_t ro = item & 63u;
+        int info = 0;
+        if (has) info = reinterpret_cast<const int*>(ln4 + 4 * (size_t)(item >> 6) + 3)[3];  // LNode::info
+        const int first = info & 0xffffff, cnt = info >> 24;
+        const f3 qo = mk(bp(o.x, ro), bp(o.y, ro), bp(o.z, ro));  // the pair's ray, from its lane
+        const f3 qd = mk(bp(d.x, ro), bp(d.y, ro), bp(d.z, ro));
         float bt = 0.0f;
         int bk = 0x7fffffff;
 #pragma unroll 2
@@ -188,9 +204,44 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
             atomicMin(reinterpret_cast<unsigned long long*>(L.keys + ro),
                       ((unsigned long long)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk);
         wave_lds_sync();
-        const uint64_t mk = L.keys[lane];  // this lane's ray: checks against its best so far
-        if (mk != ~0ull) bound = __builtin_bit_cast(float, (uint32_t)(mk >> 32));
-        tail += avail;
+        const uint64_t mkey = L.keys[lane];  // this lane's ray: checks against its best so far
+        if (mkey != ~0ull) bound = __builtin_bit_cast(float, (uint32_t)(mkey >> 32));
+        tb += avail;
+    };
+    // one second check: lane l takes queued pair ta + l (l < avail) and keeps it for a pass only if
+    // the chunk's entries' own normals leave it open
+    auto check = [&](uint32_t avail) {
+        wave_lds_sync();
+        const bool has = lane < avail;
+        const uint32_t item = has ? qa[(ta + lane) & (kLeafRing - 1)] : 0u;
+        const uint32_t ro = item & 63u;
+        const size_t c = item >> 6;
+        Ray q;
+        q.o = mk(bp(o.x, ro), bp(o.y, ro), bp(o.z, ro));
+        q.d = mk(bp(d.x, ro), bp(d.y, ro), bp(d.z, ro));
+        q.inv = rcp3(q.d);
+        const float qidl = 1.0f / sqrtf(dot(q.d, q.d));
+        const float qon = sqrtf(dot(q.o, q.o));
+        float4 na = make_float4(0, 0, 0, 0), nb = na, nc = na, ne = na;
+        if (has) { na = ln4[4 * c]; nb = ln4[4 * c + 1]; nc = ln4[4 * c + 2]; ne = ln4[4 * c + 3]; }
+        const int info = __builtin_bit_cast(int, ne.w);
+        const int first = info & 0xffffff, cnt = info >> 24;
+        float cmin = 1.0f;
+#pragma unroll 2
+        for (int e = 0; e < kChunkMax; ++e) {
+            if (e < cnt) {
+                const float4 n = sc.lnorm[first + e];
+                cmin = fminf(cmin, fabsf(q.d.x * n.x + q.d.y * n.y + q.d.z * n.z));
+            }
+        }
+        const uint64_t qk = L.keys[ro];  // the pair's ray's best so far
+        const float qbound = qk != ~0ull ? __builtin_bit_cast(float, (uint32_t)(qk >> 32)) : __builtin_inff();
+        const bool keep = has && !chunk_box_skip(na, nb, ne, nc.w, q, qon, qbound, cmin * qidl - 1e-5f);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
+        if (keep) qb[(hb + lp_rank_below(m)) & (kLeafRing - 1)] = item;
+        hb += (uint32_t)__popcll(m);
+        ta += avail;
+        if (hb - tb >= 64) pass(64);  // uniform (never more than 127 queued)
     };
     const cfloat_p nf = (cfloat_p)sc.lnodes;  // chunk nodes, 16 floats each, through the scalar cache
     auto node4 = [&](int q) { return make_float4(nf[4 * q], nf[4 * q + 1], nf[4 * q + 2], nf[4 * q + 3]); };
@@ -203,15 +254,19 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         const bool open = rvalid & !chunk_skip(a, b, cc, e, r, idl, on, bound);
         const uint64_t m = __builtin_amdgcn_ballot_w64(open);
         if (!m) continue;  // uniform
-        if (open) {
-            const uint32_t slot = (head + lp_rank_below(m)) & (kLeafRing - 1);
-            L.pq[slot] = lane;
-            L.pq[kLeafRing + slot] = (uint32_t)__builtin_bit_cast(int, e.w);  // the chunk's first slot | count << 24
+        const uint32_t item = ((uint32_t)c << 6) | lane;
+        if (refine) {  // uniform
+            if (open) qa[(ha + lp_rank_below(m)) & (kLeafRing - 1)] = item;
+            ha += (uint32_t)__popcll(m);
+            if (ha - ta >= 64) check(64);  // uniform (never more than 127 queued: kLeafRing)
+        } else {
+            if (open) qb[(hb + lp_rank_below(m)) & (kLeafRing - 1)] = item;
+            hb += (uint32_t)__popcll(m);
+            if (hb - tb >= 64) pass(64);
         }
-        head += (uint32_t)__popcll(m);
-        if (head - tail >= 64) pass(64);  // uniform (never more than 127 queued: kLeafRing)
     }
-    if (head != tail) pass(head - tail);
+    if (ha != ta) check(ha - ta);
+    if (hb != tb) pass(hb - tb);
     wave_lds_sync();
     return L.keys[lane];
 }
@@ -246,7 +301,8 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         // a batch of >= 32 rays of a leaf with chunks takes the pair walk, one ray per lane (its checks
         // cost the same per wave whatever the batch; fewer rays walk the whole leaf spread over lanes)
         // (option leaf_pairs: 0 never; 2 at every batch size: tests)
-        const bool use_pairs = pairs && sc.lnodes && ((cint_p)(sc.tris + rec0))[11] > 0 && (pairs == 2 || avail >= 32);
+        const int pmode = pairs & 3;  // option leaf_pairs; bit 2: the second check (option leaf_refine)
+        const bool use_pairs = pmode && sc.lnodes && ((cint_p)(sc.tris + rec0))[11] > 0 && (pmode == 2 || avail >= 32);
         const int lg = use_pairs ? 6 : (avail > 1 ? 32 - __builtin_clz(avail - 1) : 0);  // ceil(log2 avail)
         const uint32_t ri = lane & ((1u << lg) - 1u);
         const bool valid = ri < avail;
@@ -259,7 +315,8 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(c.x), "v"(c.y));
         uint64_t key;
         if (use_pairs)  // uniform
-            key = resolve_leaf_pairs<FAST_RCP>(sc, rec0, mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, pl_lds);
+            key = resolve_leaf_pairs<FAST_RCP>(sc, rec0, mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, pl_lds,
+                                               (pairs & 4) != 0 && sc.lnorm);
         else
             key = resolve_leaf<FAST_RCP>(sc, rec0, pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec);
         if (lane < avail) wb.pres[(size_t)b * wb.pres_stride + i] = key;

@@ -158,6 +158,7 @@ int pt_set_hw_queues(int n);
  *                                        2 = default: where the scene's probe finds it pays)
  *   "pre_ratio"     integer percent     (leaf_pre=2's bar: visited / filtered leaf work, default 50)
  *   "leaf_blocks" "leaf_pairs"          integers (the leaf pass's grid; its pair walk: 0 | 1 | 2)
+ *   "leaf_refine"   0 | 1               (the pair walk's second check with the entries' normals)
  *   "reduce"        rccl | ordered      (pt_render_multi's reduction)
  * DESIGN.md §6 describes each.  pt_get_option writes the current value ("" = default) into buf. */
 int pt_set_option(const char* name, const char* value);

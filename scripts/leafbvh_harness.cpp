@@ -151,6 +151,73 @@ int main(int argc, char** argv) {
         std::printf("tree walk: %zu nodes; per ray %.1f checked (%.1f leaves open), max of 64 rays %.1f (flat: %d)\n",
                     tree.size(), vis / (G * 64), opened / (G * 64), vmax / G, nc);
     }
+    // the cone-open chunks again with the entries' own normals: cf = min |d . n_i| over the chunk
+    // (the bound the cone only approximates), then the same expanded-box test
+    {
+        std::mt19937 rng3(5);
+        double open2 = 0, tests2 = 0, bad2 = 0;
+        for (int r = 0; r < R; ++r) {
+            const int k = (int)(rng3() % (unsigned)n);
+            float bu = U(rng3), bv = U(rng3);
+            if (bu + bv > 1) { bu = 1 - bu; bv = 1 - bv; }
+            const Tri& T = tris[(size_t)k];
+            const float P[3] = {T.q0[0] + bu * T.q0[3] + bv * T.q1[2], T.q0[1] + bu * T.q1[0] + bv * T.q1[3],
+                                T.q0[2] + bu * T.q1[1] + bv * T.e2z};
+            const float o[3] = {P[0] + 10 * U(rng3) - 5, P[1] + 10 * U(rng3) - 5, P[2] + 10 * U(rng3) - 5};
+            float d[3] = {N(rng3), N(rng3), N(rng3)};
+            const float l = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+            for (int a = 0; a < 3; ++a) d[a] /= l;
+            const float inv[3] = {1.0f / d[0], 1.0f / d[1], 1.0f / d[2]};
+            const float on = std::sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+            float lt = INFINITY;
+            for (int j = 0; j < n; ++j) {
+                float tt;
+                if (tri_hit(tris[(size_t)j], o, d, tt) && tt < lt) lt = tt;
+            }
+            float bt = INFINITY;
+            for (int c = root; c < end; ++c) {
+                const LNode& q = ch[(size_t)c];
+                int why = chunk_skip(q, o, d, inv, on, INFINITY);
+                const int first = q.info & 0xffffff, cnt = q.info >> 24;
+                if (why == 1) {  // refine: the entries' own normals
+                    float cmin = 1.0f;
+                    for (int j = 0; j < cnt; ++j) {
+                        const Tri& E = tris[(size_t)lidx[(size_t)(first + j)]];
+                        const double e1[3] = {E.q0[3], E.q1[0], E.q1[1]}, e2[3] = {E.q1[2], E.q1[3], E.e2z};
+                        double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+                        const double ln = std::sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+                        float nf[3] = {0, 0, 0};
+                        if (ln > 0) for (int a = 0; a < 3; ++a) nf[a] = (float)(nv[a] / ln);
+                        cmin = std::fmin(cmin, std::fabs(d[0] * nf[0] + d[1] * nf[1] + d[2] * nf[2]));
+                    }
+                    const float cf = cmin - 1e-5f;
+                    why = 1;
+                    if (cf > 1e-4f) {
+                        const float dl = (q.A + q.B * on) / cf + 1e-5f * on + q.C;
+                        if (dl < 1e30f) {
+                            float tn = -3e38f, tf = 3e38f;
+                            for (int a = 0; a < 3; ++a) {
+                                const float t1 = (q.lo[a] - dl - o[a]) * inv[a], t2 = (q.hi[a] + dl - o[a]) * inv[a];
+                                tn = std::fmax(tn, std::fmin(t1, t2));
+                                tf = std::fmin(tf, std::fmax(t1, t2));
+                            }
+                            why = ((tf < tn) || (tf < 0)) ? 0 : 2;
+                        }
+                    }
+                }
+                if (!why) continue;
+                open2++;
+                for (int j = 0; j < cnt; ++j) {
+                    float tt;
+                    tests2++;
+                    if (tri_hit(tris[(size_t)lidx[(size_t)(first + j)]], o, d, tt) && tt < bt) bt = tt;
+                }
+            }
+            if (!(bt == lt || (std::isinf(bt) && std::isinf(lt)))) bad2++;
+        }
+        std::printf("entries' own normals for cone-open chunks: per ray %.1f open chunks, %.1f entries tested, mismatches %.0f\n",
+                    open2 / R, tests2 / R, bad2);
+    }
     int hist[10] = {0};
     for (int c = root; c < end; ++c) hist[std::min(9, (int)(ch[(size_t)c].sa * 10.0f))]++;
     for (int b = 0; b < 10; ++b) std::printf("chunks with cone sine in [%.1f, %.1f): %d\n", b / 10.0, (b + 1) / 10.0, hist[b]);

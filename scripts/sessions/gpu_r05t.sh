@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5: the pair walk's second check of the open chunks with the entries' own normals
+# (leaf_refine): leaf-pass parity variants, the boat / CornellBox2 bands, and the boat in process
+# against HEAD's library (ablib/head) and leaf_refine=0.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+P=gpurun_out/profiles
+mkdir -p $P
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "big or leaf or nopre" > $P/r05t_pytest_parity.log 2>&1
+rc=$?; tail -2 $P/r05t_pytest_parity.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_config_bands.py -m gpu -x -q -p no:cacheprovider --timeout 600 --timeout-method thread -k "boat or cornellbox2" > $P/r05t_pytest_bands.log 2>&1
+rc=$?; tail -2 $P/r05t_pytest_bands.log; [ $rc -eq 0 ] || exit $rc
+L=brown-cs2240-path-tracer_amd/lib/libpt_hip.so
+timeout -k 10 600 python3 scripts/ab_libs.py $L ablib/head/libpt_hip.so --scene MedievalBoat --res 960 --spp 8 --depth 16 --rounds 4 > $P/r05t_ab_refine.log 2>&1
+rc=$?; grep '"lib"' $P/r05t_ab_refine.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 scripts/ab_libs.py ablib/head/libpt_hip.so $L --scene MedievalBoat --res 960 --spp 8 --depth 16 --rounds 4 >> $P/r05t_ab_refine.log 2>&1
+rc=$?; grep '"lib"' $P/r05t_ab_refine.log | tail -2; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 scripts/env_ab.py --scene MedievalBoat --width 960 --height 960 --spp 8 --depth 16 --reps 2 '' 'leaf_refine=0' > $P/r05t_env_refine.log 2>&1
+rc=$?; grep variant $P/r05t_env_refine.log; [ $rc -eq 0 ] || exit $rc

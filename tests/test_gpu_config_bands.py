@@ -100,6 +100,12 @@ def test_config4_boat_1080p_depth16_rows_bitexact(packed, ptopts):
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         img3 = s.render(p.meta_for(1920, 1080), 0, 5, 1, 16, pt_amd.MODE_AUTO)
     assert_same_bits(img3, img, "leaf_pairs=0 vs the default")
+    # the pair walk without the second check of its open chunks (leaf_refine=0)
+    ptopts.set("leaf_pairs", None)
+    ptopts.set("leaf_refine", "0")
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        img4 = s.render(p.meta_for(1920, 1080), 0, 5, 1, 16, pt_amd.MODE_AUTO)
+    assert_same_bits(img4, img, "leaf_refine=0 vs the default")
 
 
 def test_config5_image_4096_depth8_rows_bitexact(packed):

@@ -133,6 +133,10 @@ KERNELS = {
                                             "PT_LEAF_PAIRS": "2", "PT_LEAF_BLOCKS": "1", "PT_LEAF_PRE": "1"},
     "wavefront_leaf4_nopairs": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0", "PT_LEAF_PAIRS": "0",
                                 "PT_LEAF_PRE": "1"},
+    # the pair walk without its second check of the open chunks by the entries' own normals
+    # (option leaf_refine=0), at every batch size
+    "wavefront_leaf4_pairs_norefine": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0",
+                                       "PT_LEAF_PAIRS": "2", "PT_LEAF_PRE": "1", "PT_LEAF_REFINE": "0"},
 }
 
 
@@ -140,7 +144,8 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
             "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
-            "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS")
+            "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS",
+            "PT_LEAF_REFINE")
 
 
 @pytest.fixture(params=list(KERNELS))
