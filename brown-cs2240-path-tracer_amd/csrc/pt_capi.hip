@@ -152,7 +152,9 @@ struct HostLayout {
     std::vector<LNode> lnodes;    // leaf BVHs (SceneView::lnodes), and per such leaf (first record, entries, nodes)
     std::vector<int32_t> lidx;
     std::vector<Tri> ltris;       // per chunk slot: its entry's record, lbvh = the entry's position in its leaf
-    std::vector<float4> lnorm;    // per chunk slot: its entry's unit normal (SceneView::lnorm)
+    std::vector<LNode> pnodes;    // the leaf pass's chunks of the pre-resolvable leaves (SceneView::pnodes, PreLeaf c0 / c1)
+    std::vector<Tri> ptris;       // per pass chunk slot: its entry's record, lbvh = the entry's position in its leaf
+    std::vector<float4> pnorm;    // per pass chunk slot: its entry's unit normal
     std::vector<std::array<int32_t, 3>> lleaves;
     int32_t leaf_min = 0;         // leaves of at least this many entries have one (option leaf_bvh; 0: none)
     std::vector<PreLeaf> pre;     // the kMaxPre largest leaves with their paths (SceneView::pre), largest first
@@ -359,14 +361,6 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
                     Tri t = L.tris[(size_t)(lr.first + L.lidx[j])];
                     t.lbvh = L.lidx[j];
                     L.ltris.push_back(t);
-                    // the entry's normal in double, rounded (the pass's check allows 1e-5 for it)
-                    const double e1[3] = {t.q0[3], t.q1[0], t.q1[1]}, e2[3] = {t.q1[2], t.q1[3], t.e2z};
-                    const double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
-                                          e1[0] * e2[1] - e1[1] * e2[0]};
-                    const double ln = std::sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
-                    const bool ok = ln > 0.0 && std::isfinite(ln);
-                    L.lnorm.push_back(make_float4(ok ? (float)(nv[0] / ln) : 0.0f, ok ? (float)(nv[1] / ln) : 0.0f,
-                                                  ok ? (float)(nv[2] / ln) : 0.0f, 0.0f));
                 }
                 L.tris[(size_t)lr.first].lbvh = root + 1;
                 L.tris[(size_t)lr.first + 1].lbvh = end;
@@ -410,6 +404,30 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
         std::sort(all.begin(), all.end(), [](const PreLeaf& a, const PreLeaf& b) { return a.n > b.n || (a.n == b.n && a.rec0 < b.rec0); });
         if (!deep) {  // (a leaf below kMaxPrePath steps could be among the largest: no table then)
             for (size_t k = 0; k < all.size() && k < (size_t)kMaxPre; ++k) L.pre.push_back(all[k]);
+        }
+        // the leaf pass's own chunks (kPassChunkMax entries) of the leaves that have traversal chunks
+        std::vector<int32_t> plidx;
+        for (PreLeaf& pl : L.pre) {
+            pl.c0 = pl.c1 = 0;
+            if (L.leaf_min <= 0 || pl.n < L.leaf_min || L.ptris.size() + (size_t)pl.n >= (1u << 24)) continue;
+            const size_t slot0 = plidx.size();
+            int32_t root = 0, end = 0;
+            build_leaf_bvh(L.tris.data(), pl.rec0, pl.n, L.pnodes, plidx, root, end, nullptr, kPassChunkMax);
+            for (size_t j = slot0; j < plidx.size(); ++j) {
+                Tri t = L.tris[(size_t)(pl.rec0 + plidx[j])];
+                t.lbvh = plidx[j];
+                L.ptris.push_back(t);
+                // the entry's normal in double, rounded (the pass's check allows 1e-5 for it)
+                const double e1[3] = {t.q0[3], t.q1[0], t.q1[1]}, e2[3] = {t.q1[2], t.q1[3], t.e2z};
+                const double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                                      e1[0] * e2[1] - e1[1] * e2[0]};
+                const double ln = std::sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+                const bool ok = ln > 0.0 && std::isfinite(ln);
+                L.pnorm.push_back(make_float4(ok ? (float)(nv[0] / ln) : 0.0f, ok ? (float)(nv[1] / ln) : 0.0f,
+                                              ok ? (float)(nv[2] / ln) : 0.0f, 0.0f));
+            }
+            pl.c0 = root;
+            pl.c1 = end;
         }
     }
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
@@ -692,8 +710,10 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_tn = align_up(o_cnt + sizeof(Counters), 256);
     const size_t o_lnode = align_up(o_tn + std::max<size_t>(1, L.tnorm.size()) * sizeof(float4), 256);
     const size_t o_lidx = align_up(o_lnode + L.lnodes.size() * sizeof(LNode), 256);
-    const size_t o_lnorm = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
-    const size_t o_pre = align_up(o_lnorm + std::max<size_t>(1, L.lnorm.size()) * sizeof(float4), 256);
+    const size_t o_pnode = align_up(o_lidx + std::max<size_t>(1, L.ltris.size()) * sizeof(Tri), 256);
+    const size_t o_ptris = align_up(o_pnode + std::max<size_t>(1, L.pnodes.size()) * sizeof(LNode), 256);
+    const size_t o_pnorm = align_up(o_ptris + std::max<size_t>(1, L.ptris.size()) * sizeof(Tri), 256);
+    const size_t o_pre = align_up(o_pnorm + std::max<size_t>(1, L.pnorm.size()) * sizeof(float4), 256);
     const size_t total = align_up(o_pre + std::max<size_t>(1, L.pre.size()) * sizeof(PreLeaf), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
@@ -710,7 +730,9 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_tn, L.tnorm.data(), L.tnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_lnode, L.lnodes.data(), L.lnodes.size() * sizeof(LNode)) != hipSuccess ||
         up(o_lidx, L.ltris.data(), L.ltris.size() * sizeof(Tri)) != hipSuccess ||
-        up(o_lnorm, L.lnorm.data(), L.lnorm.size() * sizeof(float4)) != hipSuccess ||
+        up(o_pnode, L.pnodes.data(), L.pnodes.size() * sizeof(LNode)) != hipSuccess ||
+        up(o_ptris, L.ptris.data(), L.ptris.size() * sizeof(Tri)) != hipSuccess ||
+        up(o_pnorm, L.pnorm.data(), L.pnorm.size() * sizeof(float4)) != hipSuccess ||
         up(o_pre, L.pre.data(), L.pre.size() * sizeof(PreLeaf)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
@@ -738,7 +760,9 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.vnormals = 0;
     s->view.lnodes = L.lnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_lnode);
     s->view.ltris = L.lnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_lidx);
-    s->view.lnorm = L.lnodes.empty() ? nullptr : reinterpret_cast<const float4*>(base + o_lnorm);
+    s->view.pnodes = L.pnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_pnode);
+    s->view.ptris = L.pnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_ptris);
+    s->view.pnorm = L.pnodes.empty() ? nullptr : reinterpret_cast<const float4*>(base + o_pnorm);
     s->leaf_min = L.leaf_min;
     s->lleaves = L.lleaves;
     s->pre = L.pre;

@@ -18,6 +18,7 @@
 //            plus one extra entry k == Ntri for hash1 == 1.0 (the reference's
 //            out-of-range else-branch, resolved with Tint's clamped reads).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace pt {
@@ -69,6 +70,14 @@ static_assert(sizeof(Tri) == 48, "tri record is 3 x 16 B");
 #define PT_LEAF_CHUNK 8
 #endif
 constexpr int kChunkMax = PT_LEAF_CHUNK;
+// entries per chunk of the leaf pass's own chunking of its leaves (pt_leafpass.hip): twice the
+// traversal's — with the pass's second check the tests are cheap and the uniform chunk checks are
+// the cost (boat in process +5 %, profiles/r05w_ab_chunk_refine.log), while 16-entry chunks cost the
+// traversal's walks 13 % (r05x_ab_chunk16.log)
+#ifndef PT_PASS_CHUNK
+#define PT_PASS_CHUNK 16
+#endif
+constexpr int kPassChunkMax = PT_PASS_CHUNK;
 
 // Leaf chunk (pt_leafbvh.cpp): up to 8 entries of one big leaf of the reference tree, grouped by
 // position and normal direction.  A chunk is skipped only when none of its entries can report a
@@ -94,8 +103,10 @@ constexpr int kMaxPre = 8;        // big leaves resolved per scene (the largest 
 constexpr int kMaxPrePath = 40;   // > the deepest tree the builders make (reference 16 + 1, SAH 28 + 1)
 struct alignas(16) PreLeaf {
     int32_t rec0, n, npath, pad;
+    int32_t c0, c1, pad1, pad2;  // the leaf pass's chunks of this leaf: SceneView::pnodes[c0 .. c1) (none: c0 == c1)
     int32_t path[kMaxPrePath];
 };
+static_assert(offsetof(PreLeaf, c0) == 16 && offsetof(PreLeaf, path) == 32, "k_wf_leafpass reads PreLeaf as ints 4, 5, 8..");
 
 struct alignas(16) Material {
     float Ns, Ni, illum, phong;  // phong = (Ns + 2) / (2 pi), f32, as program-raymarch.wgsl:271
@@ -160,9 +171,12 @@ struct SceneView {
     // in its leaf (ltris: one load per test, no index indirection)
     const LNode* lnodes;
     const Tri* ltris;
-    // per chunk slot: its entry's unit normal (x, y, z, 0; zero when degenerate), for the leaf
-    // pass's second check of a chunk the cone could not skip (pt_leafpass.hip)
-    const float4* lnorm;
+    // the leaf pass's own chunks of the pre-resolved leaves (kPassChunkMax entries at most; PreLeaf
+    // c0 / c1), laid out as lnodes / ltris, and per chunk slot its entry's unit normal (x, y, z, 0;
+    // zero when degenerate) for the pass's second check of a chunk the cone could not skip
+    const LNode* pnodes;
+    const Tri* ptris;
+    const float4* pnorm;
     // leaf turns of the traversal kernel pool the leaf lanes' entries over the wave (lean_leaf_pool;
     // every tree by default, option leaf_pool).  The value is the run length (2 or 4; 0: off),
     // chosen per scene by pt_capi.hip, option pool_run

@@ -30,7 +30,6 @@ namespace {
 constexpr double kEps = 5.9604644775390625e-8;  // 2^-24
 constexpr double kK1 = 216.0, kK2 = 98.0;       // the rounding bound's coefficients (with the factor 2)
 constexpr double kThin = 0.05;                  // s_i below this: the thin group
-constexpr int kLeafMax = kChunkMax;             // entries per chunk (leaf node of the build tree)
 constexpr int kBins = 16;
 #ifndef PT_LEAF_CONE_WEIGHT
 #define PT_LEAF_CONE_WEIGHT 2.0  // the split cost's weight of a child without a bound (below)
@@ -105,11 +104,12 @@ LNode make_node(const std::vector<Item>& it, size_t b, size_t e, int axis_cls) {
 // is opened when its cone admits no bound (probability ~ sin(half-angle) for uniform directions)
 // or else when the ray meets its box (~ area ratio, as SAH).  Curved and closed surfaces put
 // every direction into a spatially small node, so the upper levels split by direction.
-void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<LNode>& nodes, std::vector<int32_t>& lidx) {
+void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
+           int leaf_max) {
     const size_t me = nodes.size();
     nodes.push_back(make_node(it, b, e, axis_cls));
     const size_t n = e - b;
-    if (n <= (size_t)kLeafMax) {
+    if (n <= (size_t)leaf_max) {
         nodes[me].info = (int32_t)lidx.size() | (int32_t)(n << 24);
         for (size_t i = b; i < e; ++i) lidx.push_back(it[i].k);
         nodes[me].skip = (int32_t)nodes.size();
@@ -203,15 +203,15 @@ void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<
         std::nth_element(it.begin() + (std::ptrdiff_t)b, it.begin() + (std::ptrdiff_t)mid, it.begin() + (std::ptrdiff_t)e,
                          [&](const Item& x, const Item& y) { return x.c[ax] < y.c[ax] || (x.c[ax] == y.c[ax] && x.k < y.k); });
     }
-    build(it, b, mid, axis_cls, nodes, lidx);
-    build(it, mid, e, axis_cls, nodes, lidx);
+    build(it, b, mid, axis_cls, nodes, lidx, leaf_max);
+    build(it, mid, e, axis_cls, nodes, lidx, leaf_max);
     nodes[me].skip = (int32_t)nodes.size();
 }
 
 }  // namespace
 
 void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
-                    int32_t& root, int32_t& end, std::vector<LNode>* tree_out) {
+                    int32_t& root, int32_t& end, std::vector<LNode>* tree_out, int leaf_max) {
     std::vector<Item> it((size_t)n);
     for (int32_t k = 0; k < n; ++k) {
         const Tri& t = tris[rec0 + k];
@@ -253,7 +253,7 @@ void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>
     for (size_t b = 0; b < it.size();) {
         size_t e = b;
         while (e < it.size() && it[e].cls == it[b].cls) ++e;
-        build(it, b, e, it[b].cls % 3, tree, lidx);
+        build(it, b, e, it[b].cls % 3, tree, lidx, leaf_max);
         b = e;
     }
     // the device checks chunks, not the tree: keep its leaf nodes, in depth-first order

@@ -117,19 +117,19 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
     return key;
 }
 
-// The same key for 64 rays (one per lane) of a leaf with chunks (pt_leafbvh.cpp: SceneView::lnodes,
-// ltris), testing only the entries each ray can hit.  Chunk c's node — wave-uniform, in SGPRs
+// The same key for 64 rays (one per lane) of a leaf with chunks (the pass's own: SceneView::pnodes,
+// ptris, chunks c0 .. c1 of PreLeaf; pt_leafbvh.cpp), testing only the entries each ray can hit.  Chunk c's node — wave-uniform, in SGPRs
 // through the scalar cache, the next one in flight — is checked by every lane against its ray
 // and its best so far (chunk_skip, pt_device.h: no entry of a skipped chunk can report a hit at t <=
 // the bound).  The (ray, chunk) pairs that stay open are queued in LDS (chunk << 6 | the ray's lane)
-// and every 64 of them a pass tests one pair per lane — the chunk's <= 8 records (ltris, copies in
+// and every 64 of them a pass tests one pair per lane — the chunk's <= 16 records (ptris, copies in
 // chunk order holding the entry's position in the leaf) against the pair's ray (from its lane,
 // ds_bpermute) — and lowers the ray's LDS key (f32 bits of t << 32 | position) with ds_min_u64.
 // REFINE: a chunk stays open for a ray mostly because its normal cone admits a direction
 // perpendicular to the ray (a grazing ray: the rounding bound is infinite) — 171 of the ~174 chunks a
 // boat ray opens (scripts/leafbvh_harness.cpp) — although its actual entries' |cos(d, n)| is
 // rarely that small.  So open pairs queue first for a second check, one pair per lane, with cf =
-// min over the chunk's entries of |d . n_i| (SceneView::lnorm, less the same 1e-5 slack) in place of
+// min over the chunk's entries of |d . n_i| (SceneView::pnorm, less the same 1e-5 slack) in place of
 // the cone's bound and the pair's ray's current best as the bound (chunk_box_skip): the harness
 // keeps 4.8 chunks open per ray.  Only the pairs that survive it are tested.
 // chunk_leaf_multi's argument (round 4): every entry able to report a hit at t <= its ray's bound at
@@ -144,12 +144,10 @@ struct PairLds {
     uint64_t* keys;    // [64]: the rays' keys
 };
 template <bool FAST_RCP>
-__device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int rec0, const f3 o, const f3 d, bool rvalid,
-                                                       const PairLds& L, bool refine) {
+__device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int c0, int c1, const f3 o, const f3 d,
+                                                       bool rvalid, const PairLds& L, bool refine) {
     const float eps = 1e-8f;
     const uint32_t lane = threadIdx.x & 63u;
-    const cint_p tr0 = (cint_p)(sc.tris + rec0);
-    const int c0 = tr0[11] - 1, c1 = tr0[12 + 11];  // Tri::lbvh of the leaf's first two records
     L.keys[lane] = ~0ull;
     wave_lds_sync();
     Ray r;
@@ -162,8 +160,8 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
     uint32_t* qa = L.pq;               // pairs to check again (refine)
     uint32_t* qb = L.pq + kLeafRing;   // pairs to test
     uint32_t ha = 0, ta = 0, hb = 0, tb = 0;  // pushed / taken (wave-uniform)
-    const float4* __restrict__ lt = reinterpret_cast<const float4*>(sc.ltris);
-    const float4* __restrict__ ln4 = reinterpret_cast<const float4*>(sc.lnodes);
+    const float4* __restrict__ lt = reinterpret_cast<const float4*>(sc.ptris);
+    const float4* __restrict__ ln4 = reinterpret_cast<const float4*>(sc.pnodes);
     auto bp = [](float v, uint32_t ro) {
         return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((int)(ro << 2), __builtin_bit_cast(int, v)));
     };
@@ -181,7 +179,7 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         float bt = 0.0f;
         int bk = 0x7fffffff;
 #pragma unroll 2
-        for (int e = 0; e < kChunkMax; ++e) {
+        for (int e = 0; e < kPassChunkMax; ++e) {
             if (e < cnt) {
                 const float4* rp = lt + 3 * (size_t)(first + e);
                 const float4 a = rp[0], b = rp[1], c = rp[2];
@@ -194,7 +192,7 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
                 const f3 sce1 = cross(sv, e1);
                 const float v = inv_det * dot(qd, sce1);
                 const float t = inv_det * dot(e2, sce1);
-                const int k = __builtin_bit_cast(int, c.w);  // Tri::lbvh of an ltris copy: the position in the leaf
+                const int k = __builtin_bit_cast(int, c.w);  // Tri::lbvh of a ptris copy: the position in the leaf
                 const bool hit = !(det > -eps && det < eps) & !(u < 0.0f) & !(u > 1.0f) & !(v < 0.0f) &
                                  !(u + v > 1.0f) & (t > eps);
                 if (hit & ((bk == 0x7fffffff) | (t < bt) | ((t == bt) & (k < bk)))) { bt = t; bk = k; }
@@ -228,9 +226,9 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         const int first = info & 0xffffff, cnt = info >> 24;
         float cmin = 1.0f;
 #pragma unroll 2
-        for (int e = 0; e < kChunkMax; ++e) {
+        for (int e = 0; e < kPassChunkMax; ++e) {
             if (e < cnt) {
-                const float4 n = sc.lnorm[first + e];
+                const float4 n = sc.pnorm[first + e];
                 cmin = fminf(cmin, fabsf(q.d.x * n.x + q.d.y * n.y + q.d.z * n.z));
             }
         }
@@ -243,7 +241,7 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         ta += avail;
         if (hb - tb >= 64) pass(64);  // uniform (never more than 127 queued)
     };
-    const cfloat_p nf = (cfloat_p)sc.lnodes;  // chunk nodes, 16 floats each, through the scalar cache
+    const cfloat_p nf = (cfloat_p)sc.pnodes;  // chunk nodes, 16 floats each, through the scalar cache
     auto node4 = [&](int q) { return make_float4(nf[4 * q], nf[4 * q + 1], nf[4 * q + 2], nf[4 * q + 3]); };
     float4 na = node4(4 * c0), nb = node4(4 * c0 + 1), nc = node4(4 * c0 + 2), ne = node4(4 * c0 + 3);
     for (int c = c0; c < c1; ++c) {
@@ -302,7 +300,8 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         // cost the same per wave whatever the batch; fewer rays walk the whole leaf spread over lanes)
         // (option leaf_pairs: 0 never; 2 at every batch size: tests)
         const int pmode = pairs & 3;  // option leaf_pairs; bit 2: the second check (option leaf_refine)
-        const bool use_pairs = pmode && sc.lnodes && ((cint_p)(sc.tris + rec0))[11] > 0 && (pmode == 2 || avail >= 32);
+        const int c0 = pl[4], c1 = pl[5];  // PreLeaf::c0, c1
+        const bool use_pairs = pmode && sc.pnodes && c1 > c0 && (pmode == 2 || avail >= 32);
         const int lg = use_pairs ? 6 : (avail > 1 ? 32 - __builtin_clz(avail - 1) : 0);  // ceil(log2 avail)
         const uint32_t ri = lane & ((1u << lg) - 1u);
         const bool valid = ri < avail;
@@ -315,8 +314,8 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
         asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(c.x), "v"(c.y));
         uint64_t key;
         if (use_pairs)  // uniform
-            key = resolve_leaf_pairs<FAST_RCP>(sc, rec0, mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, pl_lds,
-                                               (pairs & 4) != 0 && sc.lnorm);
+            key = resolve_leaf_pairs<FAST_RCP>(sc, c0, c1, mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, pl_lds,
+                                               (pairs & 4) != 0);
         else
             key = resolve_leaf<FAST_RCP>(sc, rec0, pl[1], mk(a.x, a.y, a.z), mk(a.w, c.x, c.y), valid, lg, lrec);
         if (lane < avail) wb.pres[(size_t)b * wb.pres_stride + i] = key;
@@ -345,7 +344,7 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
             bool pass = valid;
             for (int k = 0; k < npath; ++k) {
                 if (!__builtin_amdgcn_ballot_w64(pass)) break;  // uniform
-                pass = pass && enters(sc, pl[4 + k], r);
+                pass = pass && enters(sc, pl[8 + k], r);  // PreLeaf::path
             }
             const uint64_t m = __builtin_amdgcn_ballot_w64(pass);
             if (!m) continue;

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--all-meshes", action="store_true", help="every primitive of the scene (pt-pack --all-meshes)")
     ap.add_argument("--async-torch", action="store_true", help="pt_render_async on a torch stream (as bench.py)")
     ap.add_argument("--counters", action="store_true",
                     help="after the timed rounds, one counted render per variant; print its work counters")
@@ -47,7 +48,8 @@ def main():
         else:
             xml = os.path.join(ROOT, "scenes", "scene_assets", a.scene + ".xml")
         subprocess.run(["node", os.path.join(ROOT, "brown-cs2240-path-tracer_amd", "node", "bin", "pt-pack.js"),
-                        xml, td, "--width", str(a.res), "--height", str(a.res)], check=True, capture_output=True)
+                        xml, td, "--width", str(a.res), "--height", str(a.res)] + (["--all-meshes"] if a.all_meshes else []),
+                       check=True, capture_output=True)
         tri = np.fromfile(os.path.join(td, "triangle_data.f32"), np.float32)
         bvh = np.fromfile(os.path.join(td, "bvh_data.f32"), np.float32)
         meta = np.fromfile(os.path.join(td, "meta.f32"), np.float32)
