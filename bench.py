@@ -42,6 +42,7 @@ sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector), spec
+L2_PEAK_GBS = 16800.0  # MI355X_MICROARCH.md: rows gathered from the XCDs' L2, 16.8-18.8 TB/s chip-wide
 
 
 def pack_scene(scene: str, out_dir: str, W: int, H: int, spp: int, synthetic: int = 0, bvh: str = "reference",
@@ -414,6 +415,11 @@ def main():
     # logic per bounce): 40 flop per triangle test + 2 x 24 per node step + 150 per extension query
     flop_per_render = 40.0 * c[4] + 48.0 * c[3] + 150.0 * q_ext
     valu_tflops = flop_per_render / max(samples_c, 1) * value * 1e6 / 1e12  # at the step's samples/s
+    # and the scene bytes the reference's traversal reads (SURVEY.md §8d secondary: 56 B per node
+    # step, 52 B per triangle test, 60 B per material fetch — one per extension query), the figure
+    # that bounds the traversal scenes from L2 rather than HBM
+    scene_per_render = 56.0 * c[3] + 52.0 * c[4] + 60.0 * q_ext
+    scene_gbs = scene_per_render / max(samples_c, 1) * value * 1e6 / 1e9
 
     if rank == 0:
         prefixes = {"k_wf_trace": ("k_wf_trace<", "k_wf_trace_bf<"), "k_wf_step": ("k_wf_step_bf<",),
@@ -483,6 +489,13 @@ def main():
                                       "def": "(40 x triangle tests + 48 x node steps + 150 x extension queries) of "
                                              "the reference's traversal, from the GPU's work counters (SURVEY.md 8d "
                                              "secondary), per sample x samples/s of the step / the f32 vector peak"},
+                         "scene_bytes": {"bytes_per_sample": round(scene_per_render / max(samples_c, 1), 1),
+                                         "achieved": round(scene_gbs, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                                         "frac": round(scene_gbs / L2_PEAK_GBS, 4),
+                                         "def": "(56 x node steps + 52 x triangle tests + 60 x extension queries) "
+                                                "bytes of the reference's traversal, from the GPU's work counters "
+                                                "(SURVEY.md 8d secondary), per sample x samples/s / the chip's L2 "
+                                                "gather rate (MI355X_MICROARCH.md: 16.8-18.8 TB/s, the lower end)"},
                          "pipeline": {"bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
                                       "achieved": round(pipeline, 2), "frac": round(pipeline / HBM_PEAK_GBS, 4)},
                          # not a utilisation (it can exceed 1): VALU wave-instructions priced at the
