@@ -491,11 +491,13 @@ def main():
                                              "secondary), per sample x samples/s of the step / the f32 vector peak"},
                          "scene_bytes": {"bytes_per_sample": round(scene_per_render / max(samples_c, 1), 1),
                                          "achieved": round(scene_gbs, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
-                                         "frac": round(scene_gbs / L2_PEAK_GBS, 4),
+                                         "vs_l2": round(scene_gbs / L2_PEAK_GBS, 4),
                                          "def": "(56 x node steps + 52 x triangle tests + 60 x extension queries) "
                                                 "bytes of the reference's traversal, from the GPU's work counters "
-                                                "(SURVEY.md 8d secondary), per sample x samples/s / the chip's L2 "
-                                                "gather rate (MI355X_MICROARCH.md: 16.8-18.8 TB/s, the lower end)"},
+                                                "(SURVEY.md 8d secondary), per sample x samples/s, against the chip's "
+                                                "L2 gather rate (MI355X_MICROARCH.md: 16.8-18.8 TB/s, the lower end); "
+                                                "above 1 where the kernels do not read what that traversal would "
+                                                "(scenes brute-forced from LDS, leaf entries culled by chunks)"},
                          "pipeline": {"bytes_per_sample": round(b_alg / max(samples_c, 1), 1),
                                       "achieved": round(pipeline, 2), "frac": round(pipeline / HBM_PEAK_GBS, 4)},
                          # not a utilisation (it can exceed 1): VALU wave-instructions priced at the
