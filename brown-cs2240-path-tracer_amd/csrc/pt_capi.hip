@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <array>
+#include <cfloat>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -428,6 +429,15 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             }
             pl.c0 = root;
             pl.c1 = end;
+        }
+        // the pass's check takes A and B times 1.00001 (pt_leafpass.hip pass_box_skip), rounded up;
+        // a degenerate chunk's FLT_MAX stays (its delta is never bounded)
+        for (LNode& nd : L.pnodes) {
+            auto up5 = [](float v) {
+                return v >= FLT_MAX ? v : std::nextafter((float)((double)v * 1.00001), FLT_MAX);
+            };
+            nd.A = up5(nd.A);
+            nd.B = up5(nd.B);
         }
     }
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or

@@ -548,8 +548,8 @@ __device__ __forceinline__ float wave_min_t(float t) {
 // (with the returns the compiler sank the last load into the branch: two memory round trips per
 // check); a lane whose escape holds computes the box on meaningless values and is not skipped.
 // chunk_box_skip: the same rule for a given lower bound cf of |cos(d, n)| over the chunk's entries
-// (B = c.w of the node); chunk_skip takes cf from the chunk's cone, the leaf pass also from the
-// entries' own normals (pt_leafpass.hip)
+// (B = c.w of the node); chunk_skip takes cf from the chunk's cone.  (The leaf pass has its own
+// form of both, pt_leafpass.hip pass_box_skip.)
 __device__ __forceinline__ bool chunk_box_skip(const float4 a, const float4 b, const float4 e, float B, const Ray& r,
                                                float on, float bound, float cf) {
     // delta, rounded up by 1e-5 relative against the approximate reciprocal

@@ -120,8 +120,8 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
 // The same key for 64 rays (one per lane) of a leaf with chunks (the pass's own: SceneView::pnodes,
 // ptris, chunks c0 .. c1 of PreLeaf; pt_leafbvh.cpp), testing only the entries each ray can hit.  Chunk c's node — wave-uniform, in SGPRs
 // through the scalar cache, the next one in flight — is checked by every lane against its ray
-// and its best so far (chunk_skip, pt_device.h: no entry of a skipped chunk can report a hit at t <=
-// the bound).  The (ray, chunk) pairs that stay open are queued in LDS (chunk << 6 | the ray's lane)
+// and its best so far (pass_chunk_skip: chunk_skip's rule, pt_device.h — no entry of a skipped chunk
+// can report a hit at t <= the bound).  The (ray, chunk) pairs that stay open are queued in LDS (chunk << 6 | the ray's lane)
 // and every 64 of them a pass tests one pair per lane — the chunk's <= 16 records (ptris, copies in
 // chunk order holding the entry's position in the leaf) against the pair's ray (from its lane,
 // ds_bpermute) — and lowers the ray's LDS key (f32 bits of t << 32 | position) with ds_min_u64.
@@ -130,7 +130,7 @@ __device__ __forceinline__ uint64_t resolve_leaf(const SceneView& sc, int rec0, 
 // boat ray opens (scripts/leafbvh_harness.cpp) — although its actual entries' |cos(d, n)| is
 // rarely that small.  So open pairs queue first for a second check, one pair per lane, with cf =
 // min over the chunk's entries of |d . n_i| (SceneView::pnorm, less the same 1e-5 slack) in place of
-// the cone's bound and the pair's ray's current best as the bound (chunk_box_skip): the harness
+// the cone's bound and the pair's ray's current best as the bound (pass_box_skip): the harness
 // keeps 4.8 chunks open per ray.  Only the pairs that survive it are tested.
 // chunk_leaf_multi's argument (round 4): every entry able to report a hit at t <= its ray's bound at
 // check time is tested (cf <= |cos(d, n_i)| for each entry is all the rule needs, whether from the
@@ -143,6 +143,50 @@ struct PairLds {
     uint32_t* pq;      // [2][kLeafRing]: queued pairs (chunk << 6 | ray lane): to check again, to test
     uint64_t* keys;    // [64]: the rays' keys
 };
+
+// The pass's chunk check: chunk_skip's rule (pt_device.h; pt_layout.h LNode) in fewer
+// instructions, on the pass's own chunks, whose A and B are stored times 1.00001 rounded up
+// (pt_capi.hip), so delta = (A' + B' |o|) / cf + 1e-5 |o| + C takes one FMA beside the reciprocal.
+// The grown box is taken in t: on axis x its planes at fma(lo, inv, -o inv) and fma(hi, inv, -o inv),
+// moved out by delta |inv| — in exact arithmetic the interval ((lo - delta) - o) inv .. ((hi + delta)
+// - o) inv that chunk_skip rounds differently, with roundings of the same size (a few ulps of (|lo| +
+// |o| + delta) |inv|), which the rule's 1e-5 |o| + C slack covers ~80 times.  A coordinate of d that
+// is 0 (inv infinite) yields NaN or infinite bounds on that axis that only widen the interval (tn
+// never +inf, tf never -inf): never a skip the rule would not make.
+struct PassRay {
+    f3 inv, oi;  // 1 / d (rcp3, as everywhere), o * inv
+    float on;    // |o|
+};
+__device__ __forceinline__ PassRay pass_ray(const f3 o, const f3 d) {
+    PassRay r;
+    r.inv = rcp3(d);
+    r.oi = mk(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    r.on = sqrtf(dot(o, o));
+    return r;
+}
+// the rule for a lower bound cf of |cos(d, n)| over the chunk's entries (a, b, e: the node's first,
+// second and fourth float4; Bp: its B')
+__device__ __forceinline__ bool pass_box_skip(const float4 a, const float4 b, const float4 e, float Bp, const PassRay& r,
+                                              float bound, float cf) {
+    const float dl = fmaf(Bp, r.on, e.x) * __builtin_amdgcn_rcpf(cf) + fmaf(1e-5f, r.on, e.y);
+    const bool bounded = (cf > 1e-4f) & (dl < 1e30f);
+    const float px = fmaf(a.x, r.inv.x, -r.oi.x), qx = fmaf(b.x, r.inv.x, -r.oi.x);
+    const float py = fmaf(a.y, r.inv.y, -r.oi.y), qy = fmaf(b.y, r.inv.y, -r.oi.y);
+    const float pz = fmaf(a.z, r.inv.z, -r.oi.z), qz = fmaf(b.z, r.inv.z, -r.oi.z);
+    const float tn = fmaxf(fmaxf(fmaf(-dl, fabsf(r.inv.x), fminf(px, qx)), fmaf(-dl, fabsf(r.inv.y), fminf(py, qy))),
+                           fmaf(-dl, fabsf(r.inv.z), fminf(pz, qz)));
+    const float tf = fminf(fminf(fmaf(dl, fabsf(r.inv.x), fmaxf(px, qx)), fmaf(dl, fabsf(r.inv.y), fmaxf(py, qy))),
+                           fmaf(dl, fabsf(r.inv.z), fmaxf(pz, qz)));
+    return bounded & ((tf < tn) | (tf < 0.0f) | (tn > bound));
+}
+// the first check: cf from the chunk's normal cone (c: the node's third float4), as chunk_skip
+__device__ __forceinline__ bool pass_chunk_skip(const float4 a, const float4 b, const float4 c, const float4 e, const f3 d,
+                                                float idl, const PassRay& r, float bound) {
+    const float cb = fabsf(fmaf(d.z, c.x, fmaf(d.y, b.w, d.x * a.w))) * idl;
+    const float sb = __builtin_amdgcn_sqrtf(fmaxf(0.0f, fmaf(-cb, cb, 1.0f)));
+    const float cf = fmaf(cb, c.y, -fmaf(sb, c.z, 1e-5f));
+    return pass_box_skip(a, b, e, c.w, r, bound, cf);
+}
 template <bool FAST_RCP>
 __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int c0, int c1, const f3 o, const f3 d,
                                                        bool rvalid, const PairLds& L, bool refine) {
@@ -150,12 +194,8 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
     const uint32_t lane = threadIdx.x & 63u;
     L.keys[lane] = ~0ull;
     wave_lds_sync();
-    Ray r;
-    r.o = o;
-    r.d = d;
-    r.inv = rcp3(d);
+    const PassRay r = pass_ray(o, d);
     const float idl = 1.0f / sqrtf(dot(d, d));
-    const float on = sqrtf(dot(o, o));
     float bound = __builtin_inff();
     uint32_t* qa = L.pq;               // pairs to check again (refine)
     uint32_t* qb = L.pq + kLeafRing;   // pairs to test
@@ -214,12 +254,10 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         const uint32_t item = has ? qa[(ta + lane) & (kLeafRing - 1)] : 0u;
         const uint32_t ro = item & 63u;
         const size_t c = item >> 6;
-        Ray q;
-        q.o = mk(bp(o.x, ro), bp(o.y, ro), bp(o.z, ro));
-        q.d = mk(bp(d.x, ro), bp(d.y, ro), bp(d.z, ro));
-        q.inv = rcp3(q.d);
-        const float qidl = 1.0f / sqrtf(dot(q.d, q.d));
-        const float qon = sqrtf(dot(q.o, q.o));
+        const f3 qo = mk(bp(o.x, ro), bp(o.y, ro), bp(o.z, ro));  // the pair's ray, from its lane
+        const f3 qd = mk(bp(d.x, ro), bp(d.y, ro), bp(d.z, ro));
+        const PassRay q = pass_ray(qo, qd);
+        const float qidl = 1.0f / sqrtf(dot(qd, qd));
         float4 na = make_float4(0, 0, 0, 0), nb = na, nc = na, ne = na;
         if (has) { na = ln4[4 * c]; nb = ln4[4 * c + 1]; nc = ln4[4 * c + 2]; ne = ln4[4 * c + 3]; }
         const int info = __builtin_bit_cast(int, ne.w);
@@ -229,12 +267,12 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         for (int e = 0; e < kPassChunkMax; ++e) {
             if (e < cnt) {
                 const float4 n = sc.pnorm[first + e];
-                cmin = fminf(cmin, fabsf(q.d.x * n.x + q.d.y * n.y + q.d.z * n.z));
+                cmin = fminf(cmin, fabsf(fmaf(qd.z, n.z, fmaf(qd.y, n.y, qd.x * n.x))));
             }
         }
         const uint64_t qk = L.keys[ro];  // the pair's ray's best so far
         const float qbound = qk != ~0ull ? __builtin_bit_cast(float, (uint32_t)(qk >> 32)) : __builtin_inff();
-        const bool keep = has && !chunk_box_skip(na, nb, ne, nc.w, q, qon, qbound, cmin * qidl - 1e-5f);
+        const bool keep = has && !pass_box_skip(na, nb, ne, nc.w, q, qbound, fmaf(cmin, qidl, -1e-5f));
         const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
         if (keep) qb[(hb + lp_rank_below(m)) & (kLeafRing - 1)] = item;
         hb += (uint32_t)__popcll(m);
@@ -249,7 +287,7 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         if (c + 1 < c1) {  // the next chunk's node, in flight while this one is checked
             na = node4(4 * c + 4); nb = node4(4 * c + 5); nc = node4(4 * c + 6); ne = node4(4 * c + 7);
         }
-        const bool open = rvalid & !chunk_skip(a, b, cc, e, r, idl, on, bound);
+        const bool open = rvalid & !pass_chunk_skip(a, b, cc, e, d, idl, r, bound);
         const uint64_t m = __builtin_amdgcn_ballot_w64(open);
         if (!m) continue;  // uniform
         const uint32_t item = ((uint32_t)c << 6) | lane;

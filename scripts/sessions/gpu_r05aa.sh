@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 5: the leaf pass's own leaner chunk check (pass_chunk_skip / pass_box_skip: planes in t by
+# FMA, A and B pre-scaled) — leaf-pass parity variants, boat / CornellBox2 bands, and the boat in
+# process against HEAD's library (ablib/head).
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+P=gpurun_out/profiles
+mkdir -p $P
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "big or leaf or nopre" > $P/r05aa_pytest_parity.log 2>&1
+rc=$?; tail -2 $P/r05aa_pytest_parity.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_config_bands.py tests/test_gpu_fast_trees.py -m gpu -x -q -p no:cacheprovider --timeout 600 --timeout-method thread > $P/r05aa_pytest_bands.log 2>&1
+rc=$?; tail -2 $P/r05aa_pytest_bands.log; [ $rc -eq 0 ] || exit $rc
+L=brown-cs2240-path-tracer_amd/lib/libpt_hip.so
+timeout -k 10 600 python3 scripts/ab_libs.py $L ablib/head/libpt_hip.so --scene MedievalBoat --res 960 --spp 8 --depth 16 --rounds 4 > $P/r05aa_ab_lean.log 2>&1
+rc=$?; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 scripts/ab_libs.py ablib/head/libpt_hip.so $L --scene MedievalBoat --res 960 --spp 8 --depth 16 --rounds 4 >> $P/r05aa_ab_lean.log 2>&1
+rc=$?; grep '"lib"' $P/r05aa_ab_lean.log; [ $rc -eq 0 ] || exit $rc
