@@ -350,8 +350,11 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffer
 }
 // The instances with pre-resolved big leaves (TRAV 26x / 27x): held to 80 VGPRs, 6 waves per SIMD
 // (83 unconstrained: 5 waves)
+#ifndef PT_TRACE_PRE_WAVES
+#define PT_TRACE_PRE_WAVES 6
+#endif
 template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_wf_trace_pre(
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(PT_TRACE_PRE_WAVES, 8))) void k_wf_trace_pre(
     SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out, uint32_t watchdog, int sparse) {
     wf_trace_body<LDS, TRAV, COUNT, RING, PRUN>(sc, wb, in_q, cnt_out, watchdog, sparse);
 }
