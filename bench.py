@@ -366,10 +366,16 @@ def main():
     # one event pair per step, read after the loop: the host enqueues step k + 1 while the GPU still
     # runs step k (a synchronisation per step would leave the GPU idle while ~150 launches are issued)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # the dominant kernel's launches carry HIP events in the LAST timed step only: an event pair per
+    # launch costs the step ~1 % at configs[1] (144 launches in 95 ms) and ~5 % for one rank's
+    # 1/8 share (36 launches in 13 ms; profiles/r05ae_share_events.jsonl), so the other steps run
+    # uninstrumented and the kernel's average launch and busy time come from that one step
     scene.profile_select(dominant)
-    scene.profile_enable(not args.no_kernel_timing and dominant is not None)
+    timed = not args.no_kernel_timing and dominant is not None
     t0 = time.perf_counter()
-    for ev0, ev1 in evs:
+    for i, (ev0, ev1) in enumerate(evs):
+        if timed and i == len(evs) - 1:
+            scene.profile_enable(True)
         step(ev0, ev1)
     drain()
     render_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
@@ -392,9 +398,9 @@ def main():
     b_alg = (48.0 * (q_ext + q_sh) + 96.0 * q_ext + 24.0 * samples_c)  # bytes per render
     if prof:
         kernel = max(prof, key=lambda k: prof[k]["total_ms"])
-        launches_per_render = prof[kernel]["launches"] / args.steps
+        launches_per_render = prof[kernel]["launches"]  # of the last timed step
         k_ms = prof[kernel]["avg_ms"]
-        busy_ms = prof[kernel]["busy_ms"] / args.steps  # union of the launches' intervals, per step
+        busy_ms = prof[kernel]["busy_ms"]  # union of the launches' intervals in that step
         if kernel in ("k_wf_trace", "k_wf_leafpass"):
             # the traversal's model: a ray record read and a hit record written per query (the big-leaf
             # pass reads the same records and writes a key per query that meets a big leaf's boxes)
@@ -479,7 +485,8 @@ def main():
                                             tu["source"] + ")") if tu else None,
                          "achieved_def": "algorithmic bytes per launch (SURVEY.md 8d model from the GPU's work counters) x "
                                          "launches per step / the kernel's busy time per step (union of its launches' "
-                                         "HIP-event intervals on every part stream)",
+                                         "HIP-event intervals on every part stream, in the last timed step: the "
+                                         "others carry no events)",
                          "launches_per_step": launches_per_render, "bytes_per_launch": round(bytes_per_launch),
                          "queries_per_sample": round((q_ext + q_sh) / max(samples_c, 1), 3),
                          "valu_alg_frac": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
