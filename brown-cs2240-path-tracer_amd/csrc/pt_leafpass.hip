@@ -254,10 +254,13 @@ __device__ __forceinline__ uint64_t resolve_leaf_pairs(const SceneView& sc, int 
         const uint32_t item = has ? qa[(ta + lane) & (kLeafRing - 1)] : 0u;
         const uint32_t ro = item & 63u;
         const size_t c = item >> 6;
-        const f3 qo = mk(bp(o.x, ro), bp(o.y, ro), bp(o.z, ro));  // the pair's ray, from its lane
+        // the pair's ray, from its lane: its direction and the check's terms (no reciprocals here)
         const f3 qd = mk(bp(d.x, ro), bp(d.y, ro), bp(d.z, ro));
-        const PassRay q = pass_ray(qo, qd);
-        const float qidl = 1.0f / sqrtf(dot(qd, qd));
+        PassRay q;
+        q.inv = mk(bp(r.inv.x, ro), bp(r.inv.y, ro), bp(r.inv.z, ro));
+        q.oi = mk(bp(r.oi.x, ro), bp(r.oi.y, ro), bp(r.oi.z, ro));
+        q.on = bp(r.on, ro);
+        const float qidl = bp(idl, ro);
         float4 na = make_float4(0, 0, 0, 0), nb = na, nc = na, ne = na;
         if (has) { na = ln4[4 * c]; nb = ln4[4 * c + 1]; nc = ln4[4 * c + 2]; ne = ln4[4 * c + 3]; }
         const int info = __builtin_bit_cast(int, ne.w);
