@@ -139,6 +139,15 @@ constexpr long kLeafBvhDefault = 128;
 // the probe of the pre-resolvable leaves (probe_pre_leaves): a 32 x 32 raster (<= 4 Ki queries), at
 // most 2^23 triangle tests (MedievalBoat: ~4 k per query, ~30 ms)
 constexpr int kPreProbeGrid = 32;
+// the leaf pass's chunks: the builder's leaves of at most PT_PASS_LEAF entries, neighbours merged
+// while they fit PT_PASS_MERGE (<= kPassChunkMax; 0: no merging)
+#ifndef PT_PASS_LEAF
+#define PT_PASS_LEAF kPassChunkMax
+#endif
+#ifndef PT_PASS_MERGE
+#define PT_PASS_MERGE kPassChunkMax
+#endif
+static_assert(PT_PASS_LEAF <= kPassChunkMax && PT_PASS_MERGE <= kPassChunkMax, "pass chunks fit the pass's loops");
 constexpr uint64_t kPreProbeTests = 1ull << 23;
 
 struct HostLayout {
@@ -413,7 +422,7 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             if (L.leaf_min <= 0 || pl.n < L.leaf_min || L.ptris.size() + (size_t)pl.n >= (1u << 24)) continue;
             const size_t slot0 = plidx.size();
             int32_t root = 0, end = 0;
-            build_leaf_bvh(L.tris.data(), pl.rec0, pl.n, L.pnodes, plidx, root, end, nullptr, kPassChunkMax);
+            build_leaf_bvh(L.tris.data(), pl.rec0, pl.n, L.pnodes, plidx, root, end, nullptr, PT_PASS_LEAF, PT_PASS_MERGE);
             for (size_t j = slot0; j < plidx.size(); ++j) {
                 Tri t = L.tris[(size_t)(pl.rec0 + plidx[j])];
                 t.lbvh = plidx[j];

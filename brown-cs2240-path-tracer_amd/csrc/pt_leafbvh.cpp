@@ -211,7 +211,7 @@ void build(std::vector<Item>& it, size_t b, size_t e, int axis_cls, std::vector<
 }  // namespace
 
 void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
-                    int32_t& root, int32_t& end, std::vector<LNode>* tree_out, int leaf_max) {
+                    int32_t& root, int32_t& end, std::vector<LNode>* tree_out, int leaf_max, int merge_max) {
     std::vector<Item> it((size_t)n);
     for (int32_t k = 0; k < n; ++k) {
         const Tri& t = tris[rec0 + k];
@@ -250,16 +250,43 @@ void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>
     // groups in a fixed order; within a group the entries keep their leaf order until split
     std::stable_sort(it.begin(), it.end(), [](const Item& a, const Item& b) { return a.cls < b.cls; });
     std::vector<LNode> tree;
+    std::vector<size_t> cls_end;  // per class group: the tree's size after it
     for (size_t b = 0; b < it.size();) {
         size_t e = b;
         while (e < it.size() && it[e].cls == it[b].cls) ++e;
         build(it, b, e, it[b].cls % 3, tree, lidx, leaf_max);
+        cls_end.push_back(tree.size());
         b = e;
     }
-    // the device checks chunks, not the tree: keep its leaf nodes, in depth-first order
+    // the device checks chunks, not the tree: keep its leaf nodes, in depth-first order (a leaf
+    // covers the next items of `it`); merge_max > 0: neighbours of one class group merged while
+    // their entries fit merge_max (one node over the merged items)
     root = (int32_t)nodes.size();
-    for (const LNode& nd : tree)
-        if (nd.info >= 0) nodes.push_back(nd);
+    size_t ci = 0, item = 0, gb = 0, gcls = 0;
+    int32_t ginfo = -1;  // the open merged chunk: first slot | count << 24 (-1: none)
+    auto flush = [&]() {
+        if (ginfo < 0) return;
+        LNode g = make_node(it, gb, gb + (size_t)(ginfo >> 24), it[gb].cls % 3);
+        g.info = ginfo;
+        g.skip = 0;
+        nodes.push_back(g);
+        ginfo = -1;
+    };
+    for (size_t t = 0; t < tree.size(); ++t) {
+        while (ci < cls_end.size() && t >= cls_end[ci]) ++ci;
+        const LNode& nd = tree[t];
+        if (nd.info < 0) continue;
+        const int32_t cnt = nd.info >> 24;
+        if (merge_max <= 0) {
+            nodes.push_back(nd);
+        } else {
+            if (ginfo >= 0 && (gcls != ci || (ginfo >> 24) + cnt > merge_max)) flush();
+            if (ginfo < 0) { ginfo = nd.info; gb = item; gcls = ci; }
+            else ginfo += cnt << 24;
+        }
+        item += (size_t)cnt;
+    }
+    flush();
     end = (int32_t)nodes.size();
     if (tree_out) *tree_out = tree;
 }

@@ -16,9 +16,11 @@ namespace pt {
 // (LNode), the entries' positions in the leaf to `lidx`.  tree (optional): the whole build tree in
 // depth-first order (LNode::skip = the node after its subtree; leaves: info >= 0, in chunk order).
 // leaf_max: entries per chunk at most (kChunkMax for the traversal's walks, kPassChunkMax for the
-// leaf pass's).
+// leaf pass's); merge_max > 0: neighbouring chunks of one normal class merged while their entries
+// fit merge_max.
 void build_leaf_bvh(const Tri* tris, int32_t rec0, int32_t n, std::vector<LNode>& nodes, std::vector<int32_t>& lidx,
-                    int32_t& root, int32_t& end, std::vector<LNode>* tree = nullptr, int leaf_max = kChunkMax);
+                    int32_t& root, int32_t& end, std::vector<LNode>* tree = nullptr, int leaf_max = kChunkMax,
+                    int merge_max = 0);
 
 // How often the rays that pass a big leaf's box filter (its path of child boxes from the root,
 // PreLeaf) go on to visit it in the reference traversal, for a render's camera: out[b] = {rays that

@@ -11,11 +11,12 @@
 // two-level walk saves only ~29 % of the checks.)
 // Build: hipcc -x hip --offload-arch=gfx950 -O2 -std=c++17 -ffp-contract=off
 //        -I brown-cs2240-path-tracer_amd/csrc scripts/leafbvh_harness.cpp brown-cs2240-path-tracer_amd/csrc/pt_leafbvh.cpp
-// Run:   ./a.out leaf_records.bin
+// Run:   ./a.out leaf_records.bin [entries per chunk [merge neighbours up to]]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <random>
 #include <vector>
 
@@ -69,7 +70,8 @@ int main(int argc, char** argv) {
     std::vector<LNode> ch;
     std::vector<int32_t> lidx;
     int32_t root = 0, end = 0;
-    build_leaf_bvh(tris.data(), 0, n, ch, lidx, root, end);
+    const int lmax = argc > 2 ? std::atoi(argv[2]) : kChunkMax, mmax = argc > 3 ? std::atoi(argv[3]) : 0;
+    build_leaf_bvh(tris.data(), 0, n, ch, lidx, root, end, nullptr, lmax, mmax);
     const int nc = end - root;
     std::printf("entries %d chunks %d\n", n, nc);
     std::mt19937 rng(5);
