@@ -314,7 +314,7 @@ template <bool FAST_RCP>
 __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, WfBuffers wb, int in_q, int pairs) {
     __shared__ uint32_t ring[kLeafPassBlock / 64][kMaxPre][kLeafRing];
     __shared__ uint32_t pos[kLeafPassBlock / 64][kMaxPre][2];  // per wave and leaf: head, tail (wave-uniform)
-    // per wave: a block of leaf records (resolve_leaf) or the pair walk's ray table, pair queue and
+    // per wave: a block of leaf records (resolve_leaf) or the pair walk's two pair rings and its rays'
     // keys (resolve_leaf_pairs), one region for both
     constexpr uint32_t kScratch = 2 * kLeafRing * 4 + 64 * 8;  // 1,536 B >= 3 * kRecBlock * 16
     static_assert(kScratch >= 3 * kRecBlock * 16, "the record block fits the pair walk's region");
