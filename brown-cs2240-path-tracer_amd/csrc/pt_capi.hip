@@ -80,6 +80,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"pre_ratio", OPT_INT, nullptr},     {"leaf_refine", OPT_BOOL, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
     {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},   {"pool_run", OPT_ENUM, "2|4"},
+    {"leaf_skip", OPT_BOOL, nullptr},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
     {"reduce", OPT_ENUM, "rccl|ordered"},
 };
@@ -149,6 +150,8 @@ constexpr int kPreProbeGrid = 32;
 #endif
 static_assert(PT_PASS_LEAF <= kPassChunkMax && PT_PASS_MERGE <= kPassChunkMax, "pass chunks fit the pass's loops");
 constexpr uint64_t kPreProbeTests = 1ull << 23;
+// the leaf remainders' probe (build_leaf_skips): at most 2^24 triangle tests (Glossy ~1.7 M, ~20 ms)
+constexpr uint64_t kLeafSkipProbeTests = 1ull << 24;
 
 struct HostLayout {
     std::vector<Node> nodes;
@@ -169,6 +172,8 @@ struct HostLayout {
     int32_t leaf_min = 0;         // leaves of at least this many entries have one (option leaf_bvh; 0: none)
     std::vector<PreLeaf> pre;     // the kMaxPre largest leaves with their paths (SceneView::pre), largest first
     std::vector<int32_t> leaf_sizes;  // every non-empty leaf's entries, largest first
+    std::vector<int2> nalt;       // leaf remainders (SceneView::nalt; empty: none)
+    LeafSkipStats skip{};
     int32_t mb_base = 0;          // record of uid 0 (mailbox scenes)
     bool mailbox = false;
     pt_scene_info info{};
@@ -449,6 +454,11 @@ int build_layout(const float* tri, size_t tri_len, const float* bvh, size_t bvh_
             nd.B = up5(nd.B);
         }
     }
+    // Leaf remainders (pt_leafskip.cpp; option leaf_skip, read here and per render, default on):
+    // scenes without mailbox (their kernels test every distinct entry once per ray anyway)
+    if (!L.mailbox && opts_snapshot().flag("leaf_skip", 1) != 0)
+        build_leaf_skips(L.nodes, L.tris, L.tnorm, L.lights, kLeafSkipMaxLeaf, kLeafAlt, kLeafSkipProbeTests, L.nalt,
+                         &L.skip);
     // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (every ray direction is normalised or
     // a reflection/refraction of unit vectors; non-finite ones give no hit on either path)
     double emax = 0.0;
@@ -733,7 +743,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_ptris = align_up(o_pnode + std::max<size_t>(1, L.pnodes.size()) * sizeof(LNode), 256);
     const size_t o_pnorm = align_up(o_ptris + std::max<size_t>(1, L.ptris.size()) * sizeof(Tri), 256);
     const size_t o_pre = align_up(o_pnorm + std::max<size_t>(1, L.pnorm.size()) * sizeof(float4), 256);
-    const size_t total = align_up(o_pre + std::max<size_t>(1, L.pre.size()) * sizeof(PreLeaf), 256);
+    const size_t o_nalt = align_up(o_pre + std::max<size_t>(1, L.pre.size()) * sizeof(PreLeaf), 256);
+    const size_t total = align_up(o_nalt + std::max<size_t>(1, L.nalt.size()) * sizeof(int2), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }
@@ -752,7 +763,8 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
         up(o_pnode, L.pnodes.data(), L.pnodes.size() * sizeof(LNode)) != hipSuccess ||
         up(o_ptris, L.ptris.data(), L.ptris.size() * sizeof(Tri)) != hipSuccess ||
         up(o_pnorm, L.pnorm.data(), L.pnorm.size() * sizeof(float4)) != hipSuccess ||
-        up(o_pre, L.pre.data(), L.pre.size() * sizeof(PreLeaf)) != hipSuccess) {
+        up(o_pre, L.pre.data(), L.pre.size() * sizeof(PreLeaf)) != hipSuccess ||
+        up(o_nalt, L.nalt.data(), L.nalt.size() * sizeof(int2)) != hipSuccess) {
         pt_scene_destroy(s);
         return fail(PT_ERR_HIP, "scene upload failed");
     }
@@ -782,6 +794,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.pnodes = L.pnodes.empty() ? nullptr : reinterpret_cast<const LNode*>(base + o_pnode);
     s->view.ptris = L.pnodes.empty() ? nullptr : reinterpret_cast<const Tri*>(base + o_ptris);
     s->view.pnorm = L.pnodes.empty() ? nullptr : reinterpret_cast<const float4*>(base + o_pnorm);
+    s->view.nalt = L.nalt.empty() ? nullptr : reinterpret_cast<const int4*>(base + o_nalt);
     s->leaf_min = L.leaf_min;
     s->lleaves = L.lleaves;
     s->pre = L.pre;
@@ -1088,6 +1101,10 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         const long run = o.num("pool_run", run2 ? 2 : 4);
         view.leaf_pool = pool ? (int32_t)run : 0;
     }
+    // leaf remainders (pt_device.h lean_node_unit): option leaf_skip=0 keeps them out (A/B); a big-leaf
+    // threshold below kLeafSkipMaxLeaf too (a leaf the cooperative turns or the leaf pass take by its
+    // first record must keep it)
+    if (o.flag("leaf_skip", 1) == 0 || (view.big_leaf > 0 && view.big_leaf < kLeafSkipMaxLeaf)) view.nalt = nullptr;
     // the brute-force replay walks the BfNode tree without a stack (bf_stackless=0: the stack walk; A/B)
     if (o.flag("bf_stackless", 1) == 0) view.bfnode = nullptr;
     const LaunchOpts lo = launch_opts(o, mode, npix * (accum ? nframes : 1), view);

@@ -300,9 +300,10 @@ struct TravLean {
     uint64_t tested, rem;  // mailbox flavours only: uids tested by this query / left in this pair
     uint32_t qi;           // pre-resolved big leaves only: the query's queue entry (SceneView::pres) ...
     uint64_t pkey;         // ... and the key of the first big leaf of its current leaf pair (pre_node_prefetch)
+    int last;              // leaf remainders (SceneView::nalt): first record of the last non-empty leaf tested, -1 none
 };
 __device__ __forceinline__ void trav_init(TravLean& s, bool active) {
-    s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1; s.qi = 0; s.pkey = ~0ull;
+    s.node = 0; s.sp = 0; s.k = 0; s.na = 0; s.nt = 0; s.la = 0; s.lb = 0; s.best = -1; s.qi = 0; s.pkey = ~0ull; s.last = -1;
     s.fl = active ? 0 : TF_DONE;
     s.ld = 0.0f; s.rd = 0.0f; s.best_t = -1.0f;
     s.tested = 0; s.rem = 0;
@@ -326,19 +327,51 @@ __device__ __forceinline__ int pre_slot(const SceneView& sc, int rec0) {
 // PRE: a node step whose hit leaf children include a pre-resolved big leaf loads that leaf's key
 // now (the first such leaf of the pair), so it arrives behind the next steps' own loads instead of
 // stalling the wave in its leaf turn (pre_apply)
+// Leaf remainders (SceneView::nalt, pt_leafskip.cpp): the descriptor of the remainder of a leaf
+// whose ray tested leaf `prev` last (first record << 7 | count), -1 when the leaf has none for it
+__device__ __forceinline__ int alt_pick(const int4 p, const int4 q, int prev) {
+    int v = -1;
+    v = prev == p.x ? p.y : v;
+    v = prev == p.z ? p.w : v;
+    v = prev == q.x ? q.y : v;
+    v = prev == q.z ? q.w : v;
+    return v;
+}
+static_assert(kLeafAlt == 4, "alt_pick reads four (prev, remainder) pairs per side");
+
 template <bool COUNT, bool PRE = false>
 __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
     const float4* np = reinterpret_cast<const float4*>(sc.nodes) + 4 * s.node;
     float4 a = np[0], b = np[1], c = np[2];
     int4 d = reinterpret_cast<const int4*>(np)[3];
+    // leaf remainders: loaded beside the node (the counting build walks the reference's leaves)
+    const bool alt = !COUNT && sc.nalt != nullptr;
+    int4 al0{}, al1{}, ar0{}, ar1{};
+    if (alt) {
+        const int4* ap = sc.nalt + 4 * s.node;
+        al0 = ap[0]; al1 = ap[1]; ar0 = ap[2]; ar1 = ap[3];
+    }
     if (COUNT) { cnt.nodes++; cnt.box_tests += 2; }
     s.ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
     s.rd = ray_box(r, b.z, b.w, c.x, c.y, c.z, c.w);
     const bool li = 0.0f < s.ld, ri = 0.0f < s.rd;
     const bool lleaf = d.z >= 0, rleaf = d.w >= 0;
-    s.na = (li & lleaf) ? d.z : 0;
-    s.nt = s.na + ((ri & rleaf) ? d.w : 0);
-    s.la = d.x; s.lb = d.y; s.k = 0;
+    int lrec = d.x, rrec = d.y, ln = d.z, rn = d.w;
+    if (alt) {
+        // a leaf child L entered by a ray whose last tested leaf M is one of L's: the remainder
+        // "L minus M" instead (exact: pt_leafskip.cpp); the right leaf's M is the left leaf when the
+        // left one is tested too.  The leaves keep their identity (first records) for `last`.
+        const bool lt = li & lleaf & (d.z > 0), rt = ri & rleaf & (d.w > 0);
+        const int dl = alt_pick(al0, al1, s.last);
+        const int pr = lt ? d.x : s.last;
+        const int dr = alt_pick(ar0, ar1, pr);
+        if (lt & (dl >= 0)) { lrec = dl >> 7; ln = dl & 127; }
+        if (rt & (dr >= 0)) { rrec = dr >> 7; rn = dr & 127; }
+        s.last = rt ? d.y : pr;
+    }
+    s.na = (li & lleaf) ? ln : 0;
+    s.nt = s.na + ((ri & rleaf) ? rn : 0);
+    s.la = lrec; s.lb = rrec; s.k = 0;
     s.fl = ((li & !lleaf) ? TF_LINT : 0) | ((ri & !rleaf) ? TF_RINT : 0) | (s.nt > 0 ? TF_LEAF : 0);
     if constexpr (PRE) {
         const bool lbig = s.na >= sc.big_leaf, rbig = s.nt - s.na >= sc.big_leaf;

@@ -108,6 +108,12 @@ struct alignas(16) PreLeaf {
 };
 static_assert(offsetof(PreLeaf, c0) == 16 && offsetof(PreLeaf, path) == 32, "k_wf_leafpass reads PreLeaf as ints 4, 5, 8..");
 
+// leaf remainders (pt_leafskip.cpp, SceneView::nalt): per leaf child, kLeafAlt earlier leaves whose
+// entries its remainders leave out; leaves of fewer than kLeafSkipMaxLeaf entries have them (the
+// count is 7 bits of the descriptor; big-leaf thresholds below it turn the skip off, pt_capi.hip)
+constexpr int kLeafAlt = 4;
+constexpr int kLeafSkipMaxLeaf = 64;
+
 struct alignas(16) Material {
     float Ns, Ni, illum, phong;  // phong = (Ns + 2) / (2 pi), f32, as program-raymarch.wgsl:271
     float Kd[3], kd_pi0;         // kd_pi* = Kd / pi per channel, f32 (program-raymarch.wgsl:165,279)
@@ -193,6 +199,11 @@ struct SceneView {
     uint32_t pres_stride;
     const uint64_t* pres;
     int32_t pre_rec0[kMaxPre];  // pre[b].rec0 by value (kernel arguments: the traversal's slot lookup in SGPRs)
+    // leaf remainders (pt_leafskip.cpp; nullptr: none or option leaf_skip=0): per node, per side,
+    // kLeafAlt pairs (first record of the leaf M the ray tested last, the remainder "this leaf minus
+    // M" as first record << 7 | count); the lean node step takes the remainder whose M matches
+    // TravLean::last (pt_device.h lean_node_unit).  Global memory, never staged into LDS
+    const int4* nalt;
 };
 
 // Per-call camera/settings block derived from the reference's 48-float meta

@@ -42,4 +42,21 @@ void probe_pre_leaves(const std::vector<Node>& nodes, const std::vector<Tri>& tr
                       const std::vector<PreLeaf>& pre, const ProbeCamera& cam, int grid, uint64_t max_tests,
                       std::vector<std::array<uint32_t, 2>>& out);
 
+// Leaf remainders (pt_leafskip.cpp; the traversal's exact skip of entries the ray tested in the
+// leaf it tested just before, pt_device.h lean_node_unit): for every leaf of fewer than max_leaf
+// (<= kLeafSkipMaxLeaf) entries, up to `alts` (kLeafAlt) earlier leaves M are chosen — by a probe of
+// the reference traversal (rays from random points of the scene in random directions and toward
+// the lights, at most max_tests triangle tests), then by nearness in the visit order — and "the
+// leaf minus M" is appended to tris (and tnorm, 3 per record) in entry order.  nalt gets per node
+// and side `alts` int2 (M's first record, remainder first record << 7 | count), INT32_MIN: none.
+struct LeafSkipStats {
+    uint64_t probe_tests = 0;  // the probe's triangle tests
+    uint64_t remainders = 0;   // remainders built
+    uint64_t skipped = 0;      // entries they leave out, summed
+    uint64_t records = 0;      // records appended
+};
+void build_leaf_skips(const std::vector<Node>& nodes, std::vector<Tri>& tris, std::vector<float4>& tnorm,
+                      const std::vector<Light>& lights, int max_leaf, int alts, uint64_t max_tests,
+                      std::vector<int2>& nalt, LeafSkipStats* stats = nullptr);
+
 }  // namespace pt

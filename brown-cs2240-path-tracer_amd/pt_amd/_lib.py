@@ -14,7 +14,7 @@ _CSRC = os.path.join(_PKG_ROOT, "csrc")
 # csrc/Makefile BUILD_SRCS: the sources whose SHA-256 the library carries as pt_build_id()
 _BUILD_SRCS = ["pt_kernels.hip", "pt_wavefront.hip", "pt_leafpass.hip", "pt_image.hip", "pt_capi.hip", "pt_math.h", "pt_layout.h",
                "pt_device.h", "pt_path.h", "pt_kernels.h", "../../include/pt_hip.h", "pt_bvh.cpp", "pt_leafbvh.h",
-               "pt_leafbvh.cpp", "Makefile"]
+               "pt_leafbvh.cpp", "pt_leafskip.cpp", "Makefile"]
 MODE_AUTO, MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1, 2
 MATH_FNS = ["sin", "cos", "tan", "acos", "log2", "exp2", "pow", "sqrt", "div", "hash1u", "hash1", "hash2x",
             "hash2y", "min", "max"]

@@ -137,6 +137,14 @@ KERNELS = {
     # (option leaf_refine=0), at every batch size
     "wavefront_leaf4_pairs_norefine": {"PT_KERNEL": "wavefront", "PT_LEAF_BVH": "4", "PT_MAILBOX": "0",
                                        "PT_LEAF_PAIRS": "2", "PT_LEAF_PRE": "1", "PT_LEAF_REFINE": "0"},
+    # leaf remainders (option leaf_skip, on by default on scenes without mailbox: every variant above
+    # that keeps big_leaf >= 64 runs them on Glossy, the sphere and the boat) off, and on with the
+    # lane-per-pair leaf turns, the megakernel and one block
+    "wavefront_noskip": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "0"},
+    "wavefront_skip_nopool_lean4": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_LEAF_POOL": "0", "PT_TRAV": "lean4"},
+    "mega_skip_lean16": {"PT_KERNEL": "mega", "PT_LEAF_SKIP": "1", "PT_TRAV": "lean16"},
+    "wavefront_skip_1block_run2": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_WF_TRACE_BLOCKS": "1",
+                                   "PT_POOL_RUN": "2"},
 }
 
 
@@ -145,7 +153,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
             "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
             "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS",
-            "PT_LEAF_REFINE")
+            "PT_LEAF_REFINE", "PT_LEAF_SKIP")
 
 
 @pytest.fixture(params=list(KERNELS))
