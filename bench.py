@@ -129,6 +129,106 @@ def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int
     return sum(cands[k][field] for k in timed) / len(timed), src
 
 
+def gpu_sysfs_dir(pci_bus_id: str | None):
+    """The amdgpu sysfs directory of the GPU at this PCI address (torch's device properties give
+    domain:bus:device); None when not found (no sysfs, another driver)."""
+    import glob
+    found = []
+    for c in sorted(glob.glob("/sys/class/drm/card*/device")):
+        try:
+            addr = os.path.basename(os.path.realpath(c))
+        except OSError:
+            continue
+        if os.path.exists(os.path.join(c, "pp_dpm_sclk")) and addr not in [a for a, _ in found]:
+            found.append((addr, c))
+    if pci_bus_id:
+        for addr, c in found:
+            if addr.lower().startswith(pci_bus_id.lower()):
+                return c
+    return found[0][1] if len(found) == 1 else None
+
+
+def gpu_state(dev_dir: str | None) -> dict | None:
+    """The GPU's clock and power state from sysfs (read-only files; nothing is set): the current DPM
+    level of each clock domain (pp_dpm_*: the line marked '*'), the hwmon sclk, power (average or
+    input) and cap, and temperatures.  Lets a bench line from one box be compared with another's
+    (a 5 % spread between boxes with nothing recorded to tell a slow box from a slow
+    build)."""
+    if not dev_dir:
+        return None
+    import glob
+    out = {}
+
+    def rd(path):
+        try:
+            with open(path) as f:
+                return f.read()
+        except OSError:
+            return None
+    for dom in ("sclk", "mclk", "fclk", "socclk"):
+        txt = rd(os.path.join(dev_dir, f"pp_dpm_{dom}"))
+        if not txt:
+            continue
+        for line in txt.splitlines():
+            if line.rstrip().endswith("*"):
+                v = line.split(":", 1)[-1].replace("*", "").strip().lower()
+                try:
+                    out[f"{dom}_mhz"] = float(v.replace("mhz", "").strip())
+                except ValueError:
+                    out[f"{dom}_level"] = v
+    for hw in sorted(glob.glob(os.path.join(dev_dir, "hwmon", "hwmon*")))[:1]:
+        for name, key, scale in (("freq1_input", "sclk_hwmon_mhz", 1e-6), ("power1_average", "power_w", 1e-6),
+                                 ("power1_input", "power_input_w", 1e-6), ("power1_cap", "power_cap_w", 1e-6),
+                                 ("temp1_input", "temp_edge_c", 1e-3), ("temp2_input", "temp_junction_c", 1e-3),
+                                 ("temp3_input", "temp_mem_c", 1e-3)):
+            v = rd(os.path.join(hw, name))
+            if v is not None:
+                try:
+                    out[key] = round(float(v.strip()) * scale, 1)
+                except ValueError:
+                    pass
+    perf = rd(os.path.join(dev_dir, "power_dpm_force_performance_level"))
+    if perf:
+        out["perf_level"] = perf.strip()
+    return out or None
+
+
+class GpuStateSampler:
+    """Samples gpu_state every `period` s on a host thread while the timed region runs (sysfs reads
+    only); summary() gives min / median / max of the numeric fields."""
+
+    def __init__(self, dev_dir, period=0.05):
+        import threading
+        self.dev_dir, self.period, self.samples = dev_dir, period, []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True) if dev_dir else None
+
+    def _run(self):
+        while not self._stop.is_set():
+            st = gpu_state(self.dev_dir)
+            if st:
+                self.samples.append(st)
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        if self._t:
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t:
+            self._t.join()
+
+    def summary(self):
+        if not self.samples:
+            return None
+        keys = sorted({k for s in self.samples for k, v in s.items() if isinstance(v, float)})
+        return {"samples": len(self.samples),
+                **{k: [min(v), float(np.median(v)), max(v)] for k in keys
+                   for v in [[s[k] for s in self.samples if k in s]]}}
+
+
 def launch_ranks(n: int) -> int:
     """`bench.py --gpus N` (N > 1) started without a launcher: run this same command as N ranks
     under torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) and return its exit
@@ -296,6 +396,13 @@ def main():
         if world != 1:
             raise SystemExit("--share-of times one rank's share on one GPU (no launcher)")
         frame0, nframes, fstride = frames_for_rank(args.share_rank, args.share_of, args.spp)
+    try:
+        props = torch.cuda.get_device_properties(dev)
+        pci = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"
+    except Exception:  # noqa: BLE001  (older torch: no PCI fields)
+        pci = None
+    sysfs = gpu_sysfs_dir(pci)
+    state_start = gpu_state(sysfs)
     stream = torch.cuda.Stream(device=dev)
     acc = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     # the step ends with the accumulator on the host ("from the first kernel launch to
@@ -372,17 +479,19 @@ def main():
     # uninstrumented and the kernel's average launch and busy time come from that one step
     scene.profile_select(dominant)
     timed = not args.no_kernel_timing and dominant is not None
-    t0 = time.perf_counter()
-    for i, (ev0, ev1) in enumerate(evs):
-        if timed and i == len(evs) - 1:
-            scene.profile_enable(True)
-        step(ev0, ev1)
-    drain()
-    render_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    with GpuStateSampler(sysfs) as sampler:
+        t0 = time.perf_counter()
+        for i, (ev0, ev1) in enumerate(evs):
+            if timed and i == len(evs) - 1:
+                scene.profile_enable(True)
+            step(ev0, ev1)
+        drain()
+        render_ms = [ev0.elapsed_time(ev1) for ev0, ev1 in evs]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    state_end = gpu_state(sysfs)
     prof = scene.profile_read()
     scene.profile_enable(False)
     if world > 1:
@@ -469,6 +578,10 @@ def main():
                        "share": ({"of": args.share_of, "rank": args.share_rank, "frames": nframes, "stride": fstride,
                                   "implied_aggregate_before_reduce": round(value * args.share_of, 3)}
                                  if args.share_of > 1 else None)},
+            # the GPU's clocks, power and temperatures (sysfs, read-only) before the warm-up, sampled
+            # every 50 ms through the timed region (min / median / max), and after it
+            "gpu_state": {"pci": pci, "sysfs": sysfs, "start": state_start, "timed": sampler.summary(),
+                          "end": state_end},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic[0] * launches_per_render / (busy_ms * 1e-3) / 1e9 if traffic and busy_ms else None,

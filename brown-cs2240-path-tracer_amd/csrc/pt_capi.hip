@@ -579,6 +579,7 @@ struct pt_scene {
     // use the pass), from host copies of the tree, records and lights kept for it
     std::vector<std::array<uint32_t, 2>> pre_probe;
     bool pre_probed = false;
+    ProbeCamera pre_cam{};  // the camera pre_probe was taken with (a render with another probes again)
     std::mutex pre_mu;
     std::vector<Node> h_nodes;
     std::vector<Tri> h_tris;
@@ -1132,15 +1133,18 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         while (np < (int)s->pre.size() && s->pre[(size_t)np].n >= T) ++np;
         if (np > 0 && pre_opt != 1) {
             std::lock_guard<std::mutex> lk(s->pre_mu);
-            if (!s->pre_probed) {
-                ProbeCamera pc{};
-                for (int c = 0; c < 3; ++c) pc.cam[c] = fp.cam[c];
-                for (int c = 0; c < 16; ++c) pc.M[c] = fp.M[c];
-                pc.focal = fp.focal;
-                pc.half_h = fp.view_half_h;
-                pc.half_w = fp.view_half_h * fp.aspect;
+            ProbeCamera pc{};
+            for (int c = 0; c < 3; ++c) pc.cam[c] = fp.cam[c];
+            for (int c = 0; c < 16; ++c) pc.M[c] = fp.M[c];
+            pc.focal = fp.focal;
+            pc.half_h = fp.view_half_h;
+            pc.half_w = fp.view_half_h * fp.aspect;
+            // probed once per camera: a render whose camera differs from the probe's probes again
+            // (advisor r05: the choice is the camera's; both paths give the same bits)
+            if (!s->pre_probed || std::memcmp(&pc, &s->pre_cam, sizeof pc) != 0) {
                 probe_pre_leaves(s->h_nodes, s->h_tris, s->h_lights, s->pre, pc, kPreProbeGrid, kPreProbeTests,
                                  s->pre_probe);
+                s->pre_cam = pc;
                 s->pre_probed = true;
             }
         }
@@ -1153,6 +1157,13 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
             if (filt > 0.0 && vis * 100.0 < filt * (double)o.num("pre_ratio", kPreRatioDefault)) np = 0;
         }
         if (np > 0) {
+            // pt_device.h pre_slot finds a leaf's key slot by its first record among the first np table
+            // entries, and answers slot 0 for any other: every leaf of >= T entries must be among them
+            // (the table is the kMaxPre largest, and T was raised above the (kMaxPre + 1)-th; advisor r05)
+            for (size_t k = (size_t)np; k < s->pre.size(); ++k)
+                if (s->pre[k].n >= T) return fail(PT_ERR_SCENE, "internal: a leaf of >= big_leaf entries outside the pre-resolved table");
+            if (s->leaf_sizes.size() > (size_t)np && s->leaf_sizes[(size_t)np] >= T)
+                return fail(PT_ERR_SCENE, "internal: more leaves of >= big_leaf entries than the pre-resolved table holds");
             view.big_leaf = T;
             view.npre = np;
             view.pre = s->d_pre;
@@ -1400,13 +1411,26 @@ int pt_scene_leaf_bvh(const pt_scene* s, int leaf, int32_t* first_record, int32_
 
 int pt_selftest_leaf(pt_scene* s, int leaf, int mode, uint32_t seed, uint32_t nrays, int32_t* out) {
     if (!s || !out) return fail(PT_ERR_INVALID, "null argument");
-    if (leaf < 0 || (size_t)leaf >= s->lleaves.size()) return fail(PT_ERR_INVALID, "no such leaf BVH");
-    if (mode < 0 || mode > 7 || nrays == 0 || nrays > (1u << 24)) return fail(PT_ERR_INVALID, "bad mode or ray count");
+    if (mode < 0 || (mode > 7 && mode < 16) || mode > 31 || nrays == 0 || nrays > (1u << 24))
+        return fail(PT_ERR_INVALID, "bad mode or ray count");
+    const bool pass = mode >= 16;
+    if (!pass && (leaf < 0 || (size_t)leaf >= s->lleaves.size())) return fail(PT_ERR_INVALID, "no such leaf BVH");
+    if (pass && (leaf < 0 || (size_t)leaf >= s->pre.size())) return fail(PT_ERR_INVALID, "no such pre-resolvable leaf");
+    if (pass && ((mode >> 2) & 3) >= 2 && (!s->view.pnodes || s->pre[(size_t)leaf].c1 <= s->pre[(size_t)leaf].c0))
+        return fail(PT_ERR_INVALID, "the leaf has no pass chunks (option leaf_bvh)");
     HIP_TRY(hipSetDevice(s->device));
-    const auto& l = s->lleaves[(size_t)leaf];
     int32_t* d = nullptr;
     HIP_TRY(hipMalloc(&d, (size_t)nrays * 6 * sizeof(int32_t)));
-    hipError_t e = launch_selftest_leaf(s->view, l[0], l[1], mode, seed, nrays, d, nullptr);
+    hipError_t e;
+    if (pass) {
+        SceneView v = s->view;
+        v.pre = s->d_pre;
+        v.npre = (int32_t)s->pre.size();
+        e = launch_selftest_leafpass(v, leaf, mode & 15, seed, nrays, d, nullptr);
+    } else {
+        const auto& l = s->lleaves[(size_t)leaf];
+        e = launch_selftest_leaf(s->view, l[0], l[1], mode, seed, nrays, d, nullptr);
+    }
     if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)nrays * 6 * sizeof(int32_t), hipMemcpyDeviceToHost);
     hipFree(d);
     if (e != hipSuccess) return fail(PT_ERR_HIP, hipGetErrorString(e));

@@ -1259,4 +1259,55 @@ __device__ __forceinline__ Ray camera_ray(const FrameParams& fp, uint32_t x, uin
     return r;
 }
 
+// Stress rays of the leaf self-tests (pt_selftest_leaf: k_selftest_leaf, k_selftest_leafpass) for
+// ray i against the leaf of records rec0 .. rec0 + n - 1, family `mode`: 0 origins within 5 units of
+// a random point of an entry, directions uniform; 1 aimed at such a point from 10^-3 .. 20 units
+// away; 2 grazing: along the entry's plane, tilted by 10^-7 .. 10^-1 rad, so the test's rounding is
+// at its largest; 3 leaving a surface as the path tracer's bounces do (the point offset by 1e-4 along
+// the normal, directions uniform).  st: the generator's state after the ray (callers draw on).
+__device__ __forceinline__ uint32_t st_hash(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ Ray stress_ray(const SceneView& sc, int rec0, int n, int mode, uint32_t seed, uint32_t i,
+                                          uint32_t& st) {
+    st = st_hash(seed * 0x9e3779b9u + i * 0x85ebca6bu + (uint32_t)mode);
+    auto u01 = [&]() { st = st_hash(st + 0x6a09e667u); return (float)(st >> 8) * (1.0f / 16777216.0f); };
+    auto unit = [&]() {
+        const float z = 2.0f * u01() - 1.0f, ph = 6.2831853f * u01(), rr = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+        return mk(rr * cosf(ph), rr * sinf(ph), z);
+    };
+    auto nrm = [](f3 v) { const float l = sqrtf(dot(v, v)); return l > 0.0f ? mk(v.x / l, v.y / l, v.z / l) : mk(0.0f, 1.0f, 0.0f); };
+    const int k0 = (int)(st_hash(st) % (uint32_t)n);
+    const TriRec tr = load_tri(sc.tris, rec0 + k0);
+    const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
+    float bu = u01(), bv = u01();
+    if (bu + bv > 1.0f) { bu = 1.0f - bu; bv = 1.0f - bv; }
+    const f3 p = mk(v0.x + bu * e1.x + bv * e2.x, v0.y + bu * e1.y + bv * e2.y, v0.z + bu * e1.z + bv * e2.z);
+    const f3 nn = nrm(cross(e1, e2));
+    Ray r;
+    if (mode == 0) {
+        r.o = mk(p.x + 10.0f * u01() - 5.0f, p.y + 10.0f * u01() - 5.0f, p.z + 10.0f * u01() - 5.0f);
+        r.d = unit();
+    } else if (mode == 1) {
+        const f3 w = unit();
+        const float dist = exp2f(-10.0f + 14.3f * u01());
+        r.o = mk(p.x + dist * w.x, p.y + dist * w.y, p.z + dist * w.z);
+        r.d = nrm(mk(p.x - r.o.x, p.y - r.o.y, p.z - r.o.z));
+    } else if (mode == 2) {
+        const f3 t1 = nrm(e1), t2 = nrm(cross(nn, t1));
+        const float ph = 6.2831853f * u01(), tilt = exp2f(-23.0f + 19.7f * u01()) * (u01() < 0.5f ? -1.0f : 1.0f);
+        const f3 w = mk(cosf(ph) * t1.x + sinf(ph) * t2.x, cosf(ph) * t1.y + sinf(ph) * t2.y, cosf(ph) * t1.z + sinf(ph) * t2.z);
+        r.d = nrm(mk(w.x + tilt * nn.x, w.y + tilt * nn.y, w.z + tilt * nn.z));
+        const float dist = exp2f(-6.0f + 10.0f * u01());
+        r.o = mk(p.x - dist * r.d.x, p.y - dist * r.d.y, p.z - dist * r.d.z);
+    } else {
+        const float sg = u01() < 0.5f ? -1e-4f : 1e-4f;
+        r.o = mk(p.x + sg * nn.x, p.y + sg * nn.y, p.z + sg * nn.z);
+        r.d = unit();
+    }
+    r.inv = rcp3(r.d);
+    return r;
+}
+
 }  // namespace pt

@@ -171,6 +171,9 @@ hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, b
 hipError_t launch_selftest_rcp(int steps, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t stream);
 hipError_t launch_selftest_math(int fn, const float* a, const float* b, float* o, int n, hipStream_t stream);
 hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, hipStream_t stream);
+// the leaf pass's resolve_leaf / resolve_leaf_pairs against the sequential loop (pt_leafpass.hip)
+hipError_t launch_selftest_leafpass(const SceneView& sc, int b, int mode, uint32_t seed, uint32_t nrays, int32_t* out,
+                                    hipStream_t stream);
 hipError_t launch_selftest_leaf(const SceneView& sc, int rec0, int n, int mode, uint32_t seed, uint32_t nrays, int32_t* out,
                                 hipStream_t stream);
 

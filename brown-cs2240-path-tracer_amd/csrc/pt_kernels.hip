@@ -281,59 +281,18 @@ hipError_t launch_selftest_valu(int iters, int blocks, int packed, float* out, h
 // Leaf chunk stress (pt_selftest_leaf): rays against the leaf whose records start at rec0, tested
 // once by the reference's sequential loop over all n entries (each lane its own ray) and once by
 // chunk_leaf (the wave on each lane's ray in turn, as round 3's single-ray turn ran it), both against the same
-// closest t so far (prior; none for half the rays).  Ray families (mode): 0 origins
-// within 5 units of a random point of an entry, directions uniform; 1 aimed at such a point
-// from 10^-3 .. 20 units away; 2 grazing: along the entry's plane, tilted by 10^-7 .. 10^-1 rad,
-// so the test's rounding is at its largest; 3 leaving a surface as the path tracer's bounces do
-// (the point offset by 1e-4 along the normal, directions uniform).  Row i of out: the loop's
+// closest t so far (prior; none for half the rays).  Ray families (mode): pt_device.h stress_ray.  Row i of out: the loop's
 // result (position taken or -1, t bits), chunk_leaf's, its entry tests and open chunks.  mode + 4:
 // chunk_leaf_multi instead (the walk several rays share; tests and chunks not counted).
-__device__ __forceinline__ uint32_t st_hash(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-    return x;
-}
 __global__ __launch_bounds__(256) void k_selftest_leaf(SceneView sc, int rec0, int n, int mode_in, uint32_t seed,
                                                        uint32_t nrays, int32_t* __restrict__ out) {
     const int mode = mode_in & 3;
     const bool multi = (mode_in & 4) != 0;
     // every lane runs (chunk_leaf needs the whole wave); lanes past nrays store nothing
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t st = st_hash(seed * 0x9e3779b9u + i * 0x85ebca6bu + (uint32_t)mode);
+    uint32_t st = 0;
+    const Ray r = stress_ray(sc, rec0, n, mode, seed, i, st);
     auto u01 = [&]() { st = st_hash(st + 0x6a09e667u); return (float)(st >> 8) * (1.0f / 16777216.0f); };
-    auto unit = [&]() {
-        const float z = 2.0f * u01() - 1.0f, ph = 6.2831853f * u01(), rr = sqrtf(fmaxf(0.0f, 1.0f - z * z));
-        return mk(rr * cosf(ph), rr * sinf(ph), z);
-    };
-    auto nrm = [](f3 v) { const float l = sqrtf(dot(v, v)); return l > 0.0f ? mk(v.x / l, v.y / l, v.z / l) : mk(0.0f, 1.0f, 0.0f); };
-    const int k0 = (int)(st_hash(st) % (uint32_t)n);
-    const TriRec tr = load_tri(sc.tris, rec0 + k0);
-    const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
-    float bu = u01(), bv = u01();
-    if (bu + bv > 1.0f) { bu = 1.0f - bu; bv = 1.0f - bv; }
-    const f3 p = mk(v0.x + bu * e1.x + bv * e2.x, v0.y + bu * e1.y + bv * e2.y, v0.z + bu * e1.z + bv * e2.z);
-    const f3 nn = nrm(cross(e1, e2));
-    Ray r;
-    if (mode == 0) {
-        r.o = mk(p.x + 10.0f * u01() - 5.0f, p.y + 10.0f * u01() - 5.0f, p.z + 10.0f * u01() - 5.0f);
-        r.d = unit();
-    } else if (mode == 1) {
-        const f3 w = unit();
-        const float dist = exp2f(-10.0f + 14.3f * u01());
-        r.o = mk(p.x + dist * w.x, p.y + dist * w.y, p.z + dist * w.z);
-        r.d = nrm(mk(p.x - r.o.x, p.y - r.o.y, p.z - r.o.z));
-    } else if (mode == 2) {
-        const f3 t1 = nrm(e1), t2 = nrm(cross(nn, t1));
-        const float ph = 6.2831853f * u01(), tilt = exp2f(-23.0f + 19.7f * u01()) * (u01() < 0.5f ? -1.0f : 1.0f);
-        const f3 w = mk(cosf(ph) * t1.x + sinf(ph) * t2.x, cosf(ph) * t1.y + sinf(ph) * t2.y, cosf(ph) * t1.z + sinf(ph) * t2.z);
-        r.d = nrm(mk(w.x + tilt * nn.x, w.y + tilt * nn.y, w.z + tilt * nn.z));
-        const float dist = exp2f(-6.0f + 10.0f * u01());
-        r.o = mk(p.x - dist * r.d.x, p.y - dist * r.d.y, p.z - dist * r.d.z);
-    } else {
-        const float sg = u01() < 0.5f ? -1e-4f : 1e-4f;
-        r.o = mk(p.x + sg * nn.x, p.y + sg * nn.y, p.z + sg * nn.z);
-        r.d = unit();
-    }
-    r.inv = rcp3(r.d);
     const float prior = u01() < 0.5f ? -1.0f : exp2f(-10.0f + 15.0f * u01());
     const float pb = prior < 0.0f ? __builtin_inff() : prior;
     float lt = __builtin_inff();

@@ -410,6 +410,53 @@ __global__ __launch_bounds__(kLeafPassBlock) void k_wf_leafpass(SceneView sc, Wf
     }
 }
 
+// Leaf pass stress (pt_selftest_leaf, mode 16 + (method << 2 | family)): stress rays (pt_device.h
+// stress_ray) against the pre-resolvable leaf b (SceneView::pre), resolved once by the reference's
+// sequential strict-< loop over all its entries (tri_hit, each lane its own ray) and once by the
+// pass's own code — method 0: resolve_leaf with one ray per lane; 1: resolve_leaf with 8 rays per
+// wave, each over 8 lanes (the pass's short batches); 2: resolve_leaf_pairs without its second
+// check; 3: with it (pass_chunk_skip, then pass_box_skip with the entries' own normals and each
+// ray's running best as the bound).  Row i of out: the loop's (position or -1, t bits), the pass's
+// key as (position or -1, t bits), 0, 0.
+template <bool FAST_RCP>
+__global__ __launch_bounds__(kLeafPassBlock) void k_selftest_leafpass(SceneView sc, int b, int mode, uint32_t seed,
+                                                                    uint32_t nrays, int32_t* __restrict__ out) {
+    constexpr uint32_t kScratch = 2 * kLeafRing * 4 + 64 * 8;
+    __shared__ __attribute__((aligned(16))) char scratch[kLeafPassBlock / 64][kScratch];
+    const uint32_t wv = threadIdx.x / 64u, lane = threadIdx.x & 63u;
+    const int family = mode & 3, method = (mode >> 2) & 3;
+    const cint_p pl = (cint_p)(sc.pre + b);
+    const int rec0 = pl[0], n = pl[1], c0 = pl[4], c1 = pl[5];
+    // method 1: 8 rays per wave (lane & 7), each walked by 8 lanes; else one ray per lane
+    const int lg = method == 1 ? 3 : 6;
+    const uint32_t wave = blockIdx.x * (kLeafPassBlock / 64) + wv;
+    const uint32_t i = (wave << lg) + (lane & ((1u << lg) - 1u));
+    const bool valid = i < nrays;
+    uint32_t st = 0;
+    const Ray r = stress_ray(sc, rec0, n, family, seed, i, st);
+    float lt = __builtin_inff();
+    int lk = 0x7fffffff;
+    for (int k = 0; k < n; ++k) {
+        float t;
+        if (tri_hit<FAST_RCP>(sc.tris, rec0 + k, r, t) && t < lt) { lt = t; lk = k; }
+    }
+    uint64_t key;
+    if (method >= 2) {
+        const PairLds L{reinterpret_cast<uint32_t*>(scratch[wv]), reinterpret_cast<uint64_t*>(scratch[wv] + 2 * kLeafRing * 4)};
+        key = resolve_leaf_pairs<FAST_RCP>(sc, c0, c1, r.o, r.d, valid, L, method == 3);
+    } else {
+        key = resolve_leaf<FAST_RCP>(sc, rec0, n, r.o, r.d, valid, lg, reinterpret_cast<float4*>(scratch[wv]));
+    }
+    if (!valid || (lane >> lg) != 0) return;  // one lane per ray stores
+    int32_t* o = out + 6 * (size_t)i;
+    o[0] = lk != 0x7fffffff ? lk : -1;
+    o[1] = lk != 0x7fffffff ? __builtin_bit_cast(int32_t, lt) : 0;
+    o[2] = key != ~0ull ? (int32_t)(uint32_t)key : -1;
+    o[3] = key != ~0ull ? (int32_t)(uint32_t)(key >> 32) : 0;
+    o[4] = 0;
+    o[5] = 0;
+}
+
 int leafpass_blocks(const void* kernel) {
     static std::mutex mu;
     static std::map<const void*, int> cache;
@@ -426,6 +473,17 @@ int leafpass_blocks(const void* kernel) {
 }
 
 }  // namespace
+
+hipError_t launch_selftest_leafpass(const SceneView& sc, int b, int mode, uint32_t seed, uint32_t nrays, int32_t* out,
+                                    hipStream_t stream) {
+    const uint32_t per_block = (kLeafPassBlock / 64) << (((mode >> 2) & 3) == 1 ? 3 : 6);
+    const dim3 grid((nrays + per_block - 1) / per_block);
+    if (sc.fast_rcp)
+        hipLaunchKernelGGL(k_selftest_leafpass<true>, grid, dim3(kLeafPassBlock), 0, stream, sc, b, mode, seed, nrays, out);
+    else
+        hipLaunchKernelGGL(k_selftest_leafpass<false>, grid, dim3(kLeafPassBlock), 0, stream, sc, b, mode, seed, nrays, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_leafpass(const SceneView& sc, const WfBuffers& wb, int in_q, bool fast_rcp, int blocks, int pairs,
                            hipStream_t stream) {

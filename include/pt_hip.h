@@ -284,7 +284,12 @@ int pt_scene_leaf_bvh(const pt_scene* scene, int leaf, int32_t* first_record, in
  * chunk scheme the traversal uses, with the same closest-t-so-far.  out (host, nrays x 6): loop
  * (position taken or -1, t bits), chunks (position or -1, t bits), entries tested and chunks
  * opened.  mode + 4: the same families through the walk that several rays parked at one leaf share
- * (chunk_leaf_multi), out columns 4-5 zero.  Blocking. */
+ * (chunk_leaf_multi), out columns 4-5 zero.  mode 16 + (method << 2 | family): `leaf` indexes the
+ * scene's leaves the leaf pass can resolve (the 8 largest; PT_ERR_INVALID past the last) and the
+ * pass's own code resolves them — method 0 resolve_leaf one ray per lane, 1 resolve_leaf 8 rays per
+ * wave, 2 the (ray, chunk) pair walk without its second check, 3 with it (methods 2-3 need the
+ * leaf's pass chunks: PT_ERR_INVALID without) — out columns 2-3 = its key as (position or -1, t
+ * bits), 4-5 zero.  Blocking. */
 int pt_selftest_leaf(pt_scene* scene, int leaf, int mode, uint32_t seed, uint32_t nrays, int32_t* out);
 
 #ifdef __cplusplus
