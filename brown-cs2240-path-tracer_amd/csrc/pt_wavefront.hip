@@ -32,6 +32,37 @@
 
 namespace pt {
 
+// Diagnostic build only (make EXTRA=-DPT_PHASE_STATS=1 OUT_DIR=...; scripts/phase_stats.py): the fused
+// kernel's waves time their phases with s_memtime and count, per phase, loop iterations and the
+// active lanes at each (the mean over iterations of popcount(exec) / 64 is the phase's lane use for a
+// loop whose body issues the same instructions every iteration), summed over waves into
+// g_phase_stats[EXT][phase][cycles, iterations, lanes] at the end of each wave; read by
+// pt_phase_stats_read.  Phases (PH_*): the batch's loads, phase 1 (the entries' tests; PH_P1FULL
+// counts its iterations past the vote), the replay (PH_REPLAY: its node iterations; PH_RLEAF the
+// leaf-hit iterations), the path logic, the append and stores.
+#ifndef PT_PHASE_STATS
+#define PT_PHASE_STATS 0
+#endif
+enum { PH_LOAD = 0, PH_P1, PH_P1FULL, PH_REPLAY, PH_RLEAF, PH_SHADE, PH_APPEND, PH_COUNT };
+#if PT_PHASE_STATS
+struct PhaseAcc {
+    uint64_t v[PH_COUNT + 1][3];  // + a scratch row: the start of phase 1
+};
+__device__ unsigned long long g_phase_stats[2][PH_COUNT][3];
+__device__ __forceinline__ uint64_t ph_now() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ void ph_iter(PhaseAcc& pa, int ph) {
+    pa.v[ph][1] += 1;
+    pa.v[ph][2] += (uint64_t)__builtin_popcountll(__builtin_amdgcn_read_exec());
+}
+#define PH_PARAM , PhaseAcc& pa
+#define PH_PASS , pa
+#define PH_ITER(ph) ph_iter(pa, ph)
+#else
+#define PH_PARAM
+#define PH_PASS
+#define PH_ITER(ph) ((void)0)
+#endif
+
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // number of set bits of m below this lane
@@ -406,7 +437,7 @@ __device__ __forceinline__ bool mb_first_node(const SceneView& sc, int node, boo
 
 template <bool FAST_RCP>
 __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ray& r, bool active, uint64_t hits,
-                                                   float tmin, const float* slot, int nslots, float& t_out) {
+                                                   float tmin, const float* slot, int nslots, float& t_out PH_PARAM) {
     constexpr uint64_t kInner = 1ull << 63;
     uint64_t pend = active ? 1ull : 0ull;  // pre-order node 0 = the root
     uint64_t tested = 0;
@@ -414,6 +445,7 @@ __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ra
     float best_t = -1.0f;
     while (wave_any(pend != 0)) {
         if (pend != 0) {
+            PH_ITER(PH_REPLAY);
             const int n = (int)__builtin_ctzll(pend);
             pend &= pend - 1;
             const BfNode& bn = sc.bfnode[n];
@@ -426,6 +458,7 @@ __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ra
             tested |= m;
             bool bcur = false;  // the best came from this leaf pair
             while (rh) {
+                PH_ITER(PH_RLEAF);
                 const int u = (int)__builtin_ctzll(rh);
                 rh &= rh - 1;
                 const int k = __popcll(hits & ((1ull << u) - 1));
@@ -456,7 +489,7 @@ __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ra
 // phase 1 + phase 2 above.  Returns the record (or -1) and its t in t_out.
 template <bool FAST_RCP, bool COUNT>
 __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris, const Ray& r, bool valid, float* slot,
-                                          int nslots, const LStack32& stack, Counters& c, float& t_out) {
+                                          int nslots, const LStack32& stack, Counters& c, float& t_out PH_PARAM) {
     const int U = sc.n_tris - sc.mb_base;
     // phase 1: every distinct entry against all 64 rays.  The test is tri_hit's arithmetic cut
     // after u: when no lane passes the det and u tests (the early-out chain of
@@ -466,6 +499,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     const uint64_t vmask = __builtin_amdgcn_ballot_w64(valid);  // loop-invariant part of phase 1's vote
     float tmin = 3.0e38f;  // smallest t of any entry this ray hits
     for (int u = 0; u < U; ++u) {
+        PH_ITER(PH_P1);
         const TriRec tr = load_tri_scalar(gtris, sc.mb_base + u);
         const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
         const f3 rce2 = cross(r.d, e2);
@@ -480,6 +514,7 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         if ((vmask & __builtin_amdgcn_ballot_w64(ok_det) &
              __builtin_amdgcn_ballot_w64(ok_lo) & __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
             continue;  // wave-uniform
+        PH_ITER(PH_P1FULL);
         const f3 sce1 = cross(sv, e1);
         const float bv = inv_det * dot(r.d, sce1);
         const float t = inv_det * dot(e2, sce1);
@@ -496,9 +531,16 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
     // equal one can only win inside the pair just resolved (strict-< across pairs) — so the
     // result is final; a ray that hits nothing at all is final at once.  The counting build
     // (COUNT) walks on, to count the reference's work.
+#if PT_PHASE_STATS
+    {
+        const uint64_t t1 = ph_now();
+        pa.v[PH_P1][0] += t1 - pa.v[PH_COUNT][0];  // (the slot holds phase 1's start: set by the caller)
+        pa.v[PH_COUNT][0] = t1;
+    }
+#endif
     if constexpr (!COUNT) {
         if (sc.bfnode) {  // wave-uniform: the stackless walk (bf_replay_stackless)
-            return bf_replay_stackless<FAST_RCP>(sc, r, valid && hits != 0, hits, tmin, slot, nslots, t_out);
+            return bf_replay_stackless<FAST_RCP>(sc, r, valid && hits != 0, hits, tmin, slot, nslots, t_out PH_PASS);
         }
     }
     TravLean s;
@@ -567,7 +609,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
         const Ray r = unpack_ray(valid ? q[2 * (size_t)e] : make_float4(0, 0, 0, 1),
                                  valid ? q[2 * (size_t)e + 1] : make_float4(0, 0, 0, 0), p);
         float t;
-        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t);
+#if PT_PHASE_STATS
+        PhaseAcc pa{};
+#endif
+        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t PH_PASS);
         if (valid) wb.hitq[e] = make_int2(rec, __builtin_bit_cast(int, t));
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -593,7 +638,10 @@ template <bool EXT, bool FAST_RCP, bool COUNT, bool GEN = false, class Append>
 __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gtris, const FrameParams& fp,
                                               const WfBuffers& wb, size_t rbase, uint32_t b, uint32_t count,
                                               const BfLds& l, int nslots, Counters& c, Append append,
-                                              const GenArgs& gen = GenArgs{}, int64_t genk = -1) {
+                                              const GenArgs& gen, int64_t genk PH_PARAM) {
+#if PT_PHASE_STATS
+    const uint64_t t0 = ph_now();
+#endif
     const WfQueue& in = EXT ? wb.ext : wb.shd;
     const WfQueue& out = EXT ? wb.shd : wb.ext;
     const uint32_t lane = lane_id();
@@ -637,7 +685,19 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
         else { a1 = in.ray[2 * e + 1]; c2 = in.q2[e]; }
     }
     float t;
-    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t);
+#if PT_PHASE_STATS
+    {
+        const uint64_t t1 = ph_now();
+        pa.v[PH_LOAD][0] += t1 - t0;
+        pa.v[PH_COUNT][0] = t1;  // phase 1's start, for bf_closest
+    }
+#endif
+    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t PH_PASS);
+#if PT_PHASE_STATS
+    uint64_t t3 = ph_now();
+    pa.v[PH_REPLAY][0] += t3 - pa.v[PH_COUNT][0];
+    PH_ITER(PH_SHADE);  // the lanes entering the path logic (all of the batch's)
+#endif
     bool more = false;
     PathState ps;
     if (valid) {
@@ -667,17 +727,28 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
             o[0] = ps.L.x; o[1] = ps.L.y; o[2] = ps.L.z;
         }
     }
+#if PT_PHASE_STATS
+    {
+        const uint64_t t4 = ph_now();
+        pa.v[PH_SHADE][0] += t4 - t3;
+        t3 = t4;
+    }
+#endif
     const uint64_t keep = __ballot(more);
     if (keep) {  // wave-uniform
         uint32_t base = 0;
         if (lane == 0) base = append((uint32_t)__popcll(keep));
         base = __shfl(base, 0, 64);
         if (more) {
+            PH_ITER(PH_APPEND);
             const uint32_t j = (uint32_t)rbase + base + rank_below(keep);
             if (EXT) store_shadow_packed(wb, j, r, p, ps);
             else store_entry(out, j, r, p, ps);
         }
     }
+#if PT_PHASE_STATS
+    pa.v[PH_APPEND][0] += ph_now() - t3;
+#endif
 }
 
 // Trace + shade in one launch per iteration (mailbox scenes): queues are cut
@@ -724,11 +795,21 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     const uint32_t nb = nqb + nnew;
     const GenArgs ga{frame0, stride, fbase, R, tg, P, raw_salt};
     Counters c = {};
+#if PT_PHASE_STATS
+    PhaseAcc pa{};
+#endif
     for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves
         bf_step_batch<EXT, FAST_RCP, COUNT, GEN>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
                                                  [&](uint32_t n) { return atomicAdd(out_count, n); }, ga,
-                                                 b < nqb ? (int64_t)-1 : (int64_t)(b - nqb));
+                                                 b < nqb ? (int64_t)-1 : (int64_t)(b - nqb) PH_PASS);
     if (COUNT) flush_counters(c, cnt_out);
+#if PT_PHASE_STATS
+    if (!COUNT && lane_id() == 0) {
+        pa.v[PH_COUNT][0] = 0;  // (the scratch slot)
+        for (int ph = 0; ph < PH_COUNT; ++ph)
+            for (int f = 0; f < 3; ++f) atomicAdd(&g_phase_stats[EXT ? 1 : 0][ph][f], (unsigned long long)pa.v[ph][f]);
+    }
+#endif
 }
 
 // Shade blocks are 1024 threads so that compaction takes one atomicAdd per 1024 entries: all
@@ -1180,3 +1261,17 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
 }
 
 }  // namespace pt
+
+#if PT_PHASE_STATS
+// diagnostic builds only (not in include/pt_hip.h): the fused kernel's per-phase sums since the last
+// reset, [EXT][phase][cycles, iterations, lanes] as 2 x PH_COUNT x 3 u64 (scripts/phase_stats.py)
+extern "C" int pt_phase_stats_read(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -4;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(pt::g_phase_stats), sizeof(pt::g_phase_stats)) != hipSuccess) return -4;
+    if (reset) {
+        static const unsigned long long zero[2][pt::PH_COUNT][3] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pt::g_phase_stats), zero, sizeof zero) != hipSuccess) return -4;
+    }
+    return 0;
+}
+#endif

@@ -13,3 +13,9 @@ ab --synthetic 12500 --spp 16 --depth 8 --reps 3 'leaf_skip=1' 'leaf_skip=0' > g
 ab --synthetic 100000 --spp 8 --depth 8 --reps 3 'leaf_skip=1' 'leaf_skip=0' > gpurun_out/r06a_ab_syn100k.log 2>&1 || exit $?
 ab --scene MedievalBoat --width 1920 --height 1080 --spp 8 --depth 16 --reps 2 'leaf_skip=1' 'leaf_skip=0' > gpurun_out/r06a_ab_boat.log 2>&1 || exit $?
 cat gpurun_out/r06a_ab_*.log
+# the fused kernel's phases (diagnostic build of the same sources, ablib/phase: make EXTRA=-DPT_PHASE_STATS=1)
+timeout -k 10 300 python -u scripts/phase_stats.py ablib/phase/libpt_hip.so > gpurun_out/r06a_phase_stats.json 2> gpurun_out/r06a_phase_stats.err || exit $?
+cat gpurun_out/r06a_phase_stats.json
+# the bench line (now with the GPU's clock / power state)
+timeout -k 10 300 python -u bench.py > gpurun_out/r06a_bench.log 2>&1 || exit $?
+tail -c 3000 gpurun_out/r06a_bench.log
