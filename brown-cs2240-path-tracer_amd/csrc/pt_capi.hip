@@ -745,7 +745,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     const size_t o_pnorm = align_up(o_ptris + std::max<size_t>(1, L.ptris.size()) * sizeof(Tri), 256);
     const size_t o_pre = align_up(o_pnorm + std::max<size_t>(1, L.pnorm.size()) * sizeof(float4), 256);
     const size_t o_nalt = align_up(o_pre + std::max<size_t>(1, L.pre.size()) * sizeof(PreLeaf), 256);
-    const size_t total = align_up(o_nalt + std::max<size_t>(1, L.nalt.size()) * sizeof(int2), 256);
+    const size_t total = align_up(o_nalt + std::max<size_t>(2, L.nalt.size()) * sizeof(int2), 256);
     pt_scene* s = new pt_scene();
     s->device = device;
     if (hipMalloc(&s->d_mem, total) != hipSuccess) { delete s; return fail(PT_ERR_NOMEM, "hipMalloc scene"); }

@@ -337,7 +337,6 @@ __device__ __forceinline__ int alt_pick(const int4 p, const int4 q, int prev) {
     v = prev == q.z ? q.w : v;
     return v;
 }
-static_assert(kLeafAlt == 4, "alt_pick reads four (prev, remainder) pairs per side");
 
 template <bool COUNT, bool PRE = false>
 __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r, TravLean& s, Counters& cnt) {
@@ -346,10 +345,14 @@ __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r
     int4 d = reinterpret_cast<const int4*>(np)[3];
     // leaf remainders: loaded beside the node (the counting build walks the reference's leaves)
     const bool alt = !COUNT && sc.nalt != nullptr;
-    int4 al0{}, al1{}, ar0{}, ar1{};
+    int4 al0{}, al1{}, ar0{}, ar1{};  // kLeafAlt 1: al0 = (prevL, remL, prevR, remR); 4: two int4 per side
     if (alt) {
-        const int4* ap = sc.nalt + 4 * s.node;
-        al0 = ap[0]; al1 = ap[1]; ar0 = ap[2]; ar1 = ap[3];
+        if constexpr (kLeafAlt == 1) {
+            al0 = sc.nalt[s.node];
+        } else {
+            const int4* ap = sc.nalt + 4 * s.node;
+            al0 = ap[0]; al1 = ap[1]; ar0 = ap[2]; ar1 = ap[3];
+        }
     }
     if (COUNT) { cnt.nodes++; cnt.box_tests += 2; }
     s.ld = ray_box(r, a.x, a.y, a.z, a.w, b.x, b.y);
@@ -362,9 +365,15 @@ __device__ __forceinline__ bool lean_node_unit(const SceneView& sc, const Ray& r
         // "L minus M" instead (exact: pt_leafskip.cpp); the right leaf's M is the left leaf when the
         // left one is tested too.  The leaves keep their identity (first records) for `last`.
         const bool lt = li & lleaf & (d.z > 0), rt = ri & rleaf & (d.w > 0);
-        const int dl = alt_pick(al0, al1, s.last);
         const int pr = lt ? d.x : s.last;
-        const int dr = alt_pick(ar0, ar1, pr);
+        int dl, dr;
+        if constexpr (kLeafAlt == 1) {
+            dl = s.last == al0.x ? al0.y : -1;
+            dr = pr == al0.z ? al0.w : -1;
+        } else {
+            dl = alt_pick(al0, al1, s.last);
+            dr = alt_pick(ar0, ar1, pr);
+        }
         if (lt & (dl >= 0)) { lrec = dl >> 7; ln = dl & 127; }
         if (rt & (dr >= 0)) { rrec = dr >> 7; rn = dr & 127; }
         s.last = rt ? d.y : pr;

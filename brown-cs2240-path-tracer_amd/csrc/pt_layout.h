@@ -111,7 +111,11 @@ static_assert(offsetof(PreLeaf, c0) == 16 && offsetof(PreLeaf, path) == 32, "k_w
 // leaf remainders (pt_leafskip.cpp, SceneView::nalt): per leaf child, kLeafAlt earlier leaves whose
 // entries its remainders leave out; leaves of fewer than kLeafSkipMaxLeaf entries have them (the
 // count is 7 bits of the descriptor; big-leaf thresholds below it turn the skip off, pt_capi.hip)
-constexpr int kLeafAlt = 4;
+#ifndef PT_LEAF_ALT
+#define PT_LEAF_ALT 1
+#endif
+constexpr int kLeafAlt = PT_LEAF_ALT;
+static_assert(kLeafAlt == 1 || kLeafAlt == 4, "one or four (prev, remainder) pairs per side");
 constexpr int kLeafSkipMaxLeaf = 64;
 
 struct alignas(16) Material {

@@ -116,3 +116,19 @@ def test_many_emitters_rows_bitexact(synth_packed, bvh):
         assert p.bvh_data[left] == 1.0 and int(p.bvh_data[left + 4]) // 4 == 288
     _, profs = _render_bands(p, 1024, 1024, 4, 8, SYNTH_BANDS)
     _trace_kernel_ran(profs)
+
+
+def test_many_emitters_10k_rows_bitexact(synth_packed):
+    """A light of 10,082 emissive triangles (LIGHT_GRID 71) over the 1,000-triangle synthetic scene on
+    the fast tree (advisor r05): every one sits in the emitter leaf under the root, which is >= 128
+    entries, so it gets chunks (option leaf_bvh) and the big-leaf machinery by default — the leaf
+    pass or the cooperative turns, as the probe decides — and every shadow ray meets it.  Rows
+    through the light and the box, bit-exact against the oracle (at 256^2 so the oracle's 10k-test
+    shadow rays stay cheap)."""
+    p = synth_packed(1000, "sah", 71)
+    left = int(p.bvh_data[6 + 2])
+    assert p.bvh_data[left] == 1.0 and int(p.bvh_data[left + 4]) // 4 == 2 * 71 * 71
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        assert max(n for _, n, _ in s.leaf_bvhs()) == 2 * 71 * 71  # the emitter leaf has chunks
+    _, profs = _render_bands(p, 256, 256, 2, 8, [(48, 56), (80, 88)])
+    _trace_kernel_ran(profs)
