@@ -229,6 +229,54 @@ class GpuStateSampler:
                    for v in [[s[k] for s in self.samples if k in s]]}}
 
 
+def load_valu_exec(W: int, H: int, spp: int, depth: int, world: int, weights: dict):
+    """The VALU work the step's kernels actually execute, from the committed PMC pass
+    (scripts/collect_traffic.sh -> profiles/traffic.json, this configuration's key): per kernel family
+    (k_wf_step, k_wf_trace, k_wf_leafpass, ...; instances summed by their dispatches) the
+    FMA-calibrated issue density k x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE) times the lane use
+    SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) = the fraction of the SIMDs' f32 lane-op peak
+    the kernel executes; the step's figure weights each family by its time in the warm-up step
+    (`weights`: family -> ms).  Unlike valu_alg (the reference's work at this rate) it counts what the
+    kernels do, so it stays below 1.  None without a matching PMC pass."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f).get(f"{W}x{H}x{spp}x{depth}x{world}")
+        with open(os.path.join(ROOT, "profiles", "valu_calibration.json")) as f:
+            k_cal = json.load(f)["k_active"]
+    except (OSError, ValueError, KeyError):
+        return None
+    if not t:
+        return None
+    fam = {}
+    for name, e in t.items():
+        v = e.get("valu_counters") if isinstance(e, dict) else None
+        if not v or not v.get("GRBM_GUI_ACTIVE") or not v.get("SQ_ACTIVE_INST_VALU"):
+            continue
+        f = name.split("<")[0]
+        f = "k_wf_step" if f == "k_wf_step_bf" else ("k_wf_trace" if f == "k_wf_trace_pre" else f)
+        n = e.get("dispatches") or 1
+        a = fam.setdefault(f, [0.0, 0.0, 0.0])
+        a[0] += v["SQ_ACTIVE_INST_VALU"] * n
+        a[1] += v.get("SQ_THREAD_CYCLES_VALU", 0.0) * n
+        a[2] += v["GRBM_GUI_ACTIVE"] * n
+    per = {}
+    for f, (act, thr, grbm) in fam.items():
+        dens, lane = k_cal * act / (128.0 * grbm), thr / (64.0 * act)
+        per[f] = {"issue_density": round(dens, 4), "lane_use": round(lane, 4), "frac": round(dens * lane, 4),
+                  "step_ms_warmup": round(weights.get(f, 0.0), 3)}
+    per = {f: p for f, p in per.items() if p["step_ms_warmup"] > 0}  # the step's own kernels
+    wsum = sum(p["step_ms_warmup"] for p in per.values())
+    if not per or wsum <= 0:
+        return None
+    return {"frac": round(sum(p["frac"] * p["step_ms_warmup"] for p in per.values()) / wsum, 4), "kernels": per,
+            "def": "per kernel: (k x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE)) x (SQ_THREAD_CYCLES_VALU / (64 x "
+                   "SQ_ACTIVE_INST_VALU)), the executed fraction of the f32 lane-op peak; the step: weighted by each "
+                   "kernel's time in the warm-up step",
+            "source": "profiles/traffic.json[" + f"{W}x{H}x{spp}x{depth}x{world}" + "] (scripts/collect_traffic.sh) "
+                      "+ profiles/valu_calibration.json"}
+
+
 def launch_ranks(n: int) -> int:
     """`bench.py --gpus N` (N > 1) started without a launcher: run this same command as N ranks
     under torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) and return its exit
@@ -632,6 +680,9 @@ def main():
                                                      "source": valu[1]} if valu else None),
                          "kernels_ms_warmup_step": {k: round(v["total_ms"] / max(args.warmup, 1), 3)
                                                     for k, v in prof_warm.items()},
+                         "valu_exec": (load_valu_exec(W, H, args.spp, args.depth, world,
+                                                      {k: v["total_ms"] / max(args.warmup, 1) for k, v in prof_warm.items()})
+                                       if full else None),
                          "render_ms_steps": [round(x, 2) for x in render_ms]},
         }
         if world == 1 and not args.no_cpu_baseline:

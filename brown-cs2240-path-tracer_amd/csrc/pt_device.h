@@ -28,9 +28,26 @@ struct Ray {
     f3 o, d, inv;
 };
 
+// Diagnostic build only (make EXTRA=-DPT_TRACE_STATS=1 OUT_DIR=...; scripts/trace_stats.py): the lean
+// traversal's turns, timed with s_memtime and counted with their participating lanes, per kind
+// (TS_*), summed per wave in Counters::ts and flushed into g_trace_stats by k_wf_trace.
+#ifndef PT_TRACE_STATS
+#define PT_TRACE_STATS 0
+#endif
+enum { TS_NODE = 0, TS_LEAF, TS_BIG, TS_NONE, TS_POOLRUN, TS_LOOP, TS_COUNT };
 struct Counters {
     uint64_t samples, ext_queries, shadow_queries, nodes, tri_tests, box_tests;
+#if PT_TRACE_STATS
+    uint64_t ts[TS_COUNT][3];  // [kind][cycles, turns, lanes]
+#endif
 };
+#if PT_TRACE_STATS
+__device__ __forceinline__ void ts_add(Counters& c, int kind, uint64_t cyc, uint64_t lanes) {
+    c.ts[kind][0] += cyc;
+    c.ts[kind][1] += 1;
+    c.ts[kind][2] += lanes;
+}
+#endif
 
 // ray-bbox-intersection.wgsl:1-31 (Tavian's slab test; minNum/maxNum NaN handling)
 __device__ __forceinline__ float ray_box(const Ray& r, float mnx, float mny, float mnz, float mxx, float mxy, float mxz) {
@@ -934,6 +951,9 @@ __device__ __forceinline__ bool lean_leaf_pool(const SceneView& sc, const Ray& r
         if (bk != 0x7fffffff)
             atomicMin(reinterpret_cast<unsigned long long*>(keys + o),
                       ((unsigned long long)__builtin_bit_cast(uint32_t, bt) << 32) | (uint32_t)bk);
+#if PT_TRACE_STATS
+        ts_add(cnt, TS_POOLRUN, 0, (uint64_t)filled);  // lanes with a run in this test round
+#endif
         filled = 0;
     };
     int pgot = 0, plo = 0, phi = 0;  // a gathered round, merged later (chunk_leaf)
@@ -998,6 +1018,9 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
                 chunk_turn_multi<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);  // sc.lkeys: k_wf_trace's BIG instances
             } else
                 big_turn<COUNT, FAST_RCP>(sc, r, s, parked, stack, cnt);
+#if PT_TRACE_STATS
+            ts_add(cnt, TS_BIG, 0, (uint64_t)__popcll(parked));
+#endif
             return true;
         }
     }
@@ -1005,6 +1028,10 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
     const uint64_t want_node = __ballot(state == 0);
     if ((want_leaf | want_node) == 0) return false;
     bool decide = false;
+#if PT_TRACE_STATS
+    const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+    const bool leaf_turn = __popcll(want_leaf) >= sc.node_bias * __popcll(want_node);
+#endif
     if (__popcll(want_leaf) >= sc.node_bias * __popcll(want_node)) {  // wave-uniform
         if (CHUNKS && sc.leaf_pool && sc.lkeys && __ballot(1) == ~0ull)  // the wavefront kernel: the leaf entries pooled
             decide = lean_leaf_pool<PRUN, COUNT, FAST_RCP, BIG, PRE>(sc, r, s, state == TF_LEAF, cnt);
@@ -1014,6 +1041,10 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
         decide = lean_node_unit<COUNT, PRE>(sc, r, s, cnt);
     }
     if (decide) lean_decide(s, stack);
+#if PT_TRACE_STATS
+    ts_add(cnt, leaf_turn ? TS_LEAF : TS_NODE, __builtin_amdgcn_s_memtime() - ts0,
+           (uint64_t)__popcll(leaf_turn ? want_leaf : want_node));
+#endif
     return true;
 }
 

@@ -62,6 +62,9 @@ __device__ __forceinline__ void ph_iter(PhaseAcc& pa, int ph) {
 #define PH_PASS
 #define PH_ITER(ph) ((void)0)
 #endif
+#if PT_TRACE_STATS
+__device__ unsigned long long g_trace_stats[2][TS_COUNT][3];  // [shadow queue][kind][cycles, turns, lanes]
+#endif
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
@@ -303,7 +306,17 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
     typename TravSel<TRAV>::type s;
     trav_init(s, false);
     const uint64_t t_start = wall_clock64();
+#if PT_TRACE_STATS
+    uint64_t tl0 = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t guard = 0;; ++guard) {
+#if PT_TRACE_STATS
+        {
+            const uint64_t tl1 = __builtin_amdgcn_s_memtime();
+            if (guard) ts_add(c, TS_LOOP, tl1 - tl0, (uint64_t)__popcll(__ballot(has)));
+            tl0 = tl1;
+        }
+#endif
         // every wave reaches an exit: after kTraceWatchdog iterations or kTraceWatchdogTicks of
         // wall clock it reports instead of hanging (and later launches of the render skip)
         if (guard == watchdog ||
@@ -366,13 +379,22 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
             if (nv == 0 && cur == jl * kWinRays + wv && flushed >= (jl + 1) * kWinRays) break;  // all done
             continue;  // ring full with nothing in flight: the flush above frees it
         }
+#if PT_TRACE_STATS
+        if (!trav_advance<TRAV, COUNT, true, PRUN>(sc, r, s, stack, c)) ts_add(c, TS_NONE, 0, 0);
+#else
         trav_advance<TRAV, COUNT, true, PRUN>(sc, r, s, stack, c);
+#endif
         if (has && trav_finished(s)) {
             ring[sq & (nring - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;
         }
     }
     if (COUNT) flush_counters(c, cnt_out);
+#if PT_TRACE_STATS
+    if (!COUNT && lane == 0)
+        for (int k = 0; k < TS_COUNT; ++k)
+            for (int f = 0; f < 3; ++f) atomicAdd(&g_trace_stats[in_q ? 1 : 0][k][f], (unsigned long long)c.ts[k][f]);
+#endif
 }
 template <bool LDS, int TRAV, bool COUNT, uint32_t RING = kHitRing, int PRUN = 4>
 __global__ __launch_bounds__(kTraceBlock) void k_wf_trace(SceneView sc, WfBuffers wb, int in_q, Counters* cnt_out,
@@ -1271,6 +1293,20 @@ extern "C" int pt_phase_stats_read(unsigned long long* out, int reset) {
     if (reset) {
         static const unsigned long long zero[2][pt::PH_COUNT][3] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(pt::g_phase_stats), zero, sizeof zero) != hipSuccess) return -4;
+    }
+    return 0;
+}
+#endif
+
+#if PT_TRACE_STATS
+// diagnostic builds only: k_wf_trace's turn statistics since the last reset, [queue][kind][cycles,
+// turns, lanes] as 2 x TS_COUNT x 3 u64 (scripts/trace_stats.py)
+extern "C" int pt_trace_stats_read(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -4;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(pt::g_trace_stats), sizeof(pt::g_trace_stats)) != hipSuccess) return -4;
+    if (reset) {
+        static const unsigned long long zero[2][pt::TS_COUNT][3] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pt::g_trace_stats), zero, sizeof zero) != hipSuccess) return -4;
     }
     return 0;
 }

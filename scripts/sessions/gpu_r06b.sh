@@ -14,3 +14,7 @@ ab --scene CornellBox-Glossy --res 1024 --spp 32 --depth 16 > gpurun_out/r06b_ab
 ab --scene synthetic-1000 --res 1024 --spp 16 --depth 8 > gpurun_out/r06b_ab_syn1k.log 2>&1 || exit $?
 ab --scene synthetic-12500 --res 1024 --spp 16 --depth 8 > gpurun_out/r06b_ab_syn12k.log 2>&1 || exit $?
 cat gpurun_out/r06b_ab_*.log
+# the traversal kernel's turns (diagnostic build ablib/trace: make EXTRA=-DPT_TRACE_STATS=1)
+timeout -k 10 300 python -u scripts/trace_stats.py ablib/trace/libpt_hip.so --scene CornellBox-Glossy --spp 8 > gpurun_out/r06b_trace_stats_glossy.json 2>&1 || exit $?
+timeout -k 10 300 python -u scripts/trace_stats.py ablib/trace/libpt_hip.so --synthetic 12500 --spp 8 --depth 8 > gpurun_out/r06b_trace_stats_syn12k.json 2>&1 || exit $?
+cat gpurun_out/r06b_trace_stats_*.json
