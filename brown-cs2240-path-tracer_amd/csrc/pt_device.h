@@ -34,7 +34,7 @@ struct Ray {
 #ifndef PT_TRACE_STATS
 #define PT_TRACE_STATS 0
 #endif
-enum { TS_NODE = 0, TS_LEAF, TS_BIG, TS_NONE, TS_POOLRUN, TS_LOOP, TS_COUNT };
+enum { TS_NODE = 0, TS_LEAF, TS_BIG, TS_NONE, TS_POOLRUN, TS_LOOP, TS_BLOCKED, TS_STARVED, TS_COUNT };
 struct Counters {
     uint64_t samples, ext_queries, shadow_queries, nodes, tri_tests, box_tests;
 #if PT_TRACE_STATS

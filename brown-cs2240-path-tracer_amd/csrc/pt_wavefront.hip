@@ -345,6 +345,12 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
         }
         // hand the next entries to idle lanes (wave-uniform control)
         const uint64_t need = __ballot(!has);
+#if PT_TRACE_STATS
+        if (need && cur == jl * kWinRays + wv) {  // idle lanes and the window handed out: why no next one?
+            if (nv > 0 && (jl + 2) * kWinRays - flushed > nring) ts_add(c, TS_BLOCKED, 0, (uint64_t)__popcll(need));
+            else if (nv == 0) ts_add(c, TS_STARVED, 0, (uint64_t)__popcll(need));
+        }
+#endif
         if (need) {
             if (cur == jl * kWinRays + wv && nv > 0 && (jl + 2) * kWinRays - flushed <= nring) {
                 if (wl < nv) wray[2 * wl + half] = na;  // next window, if the hit ring has room

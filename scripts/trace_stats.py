@@ -11,6 +11,9 @@ per queue (extension / shadow) and kind: turns, the share of the loop's wall cyc
   none   — loop iterations with nothing to step (refill waits)
   poolrun— the pool's test rounds: lanes holding a run of RUN entries
   loop   — every loop iteration (cycles = the whole loop; lanes = lanes holding a ray)
+  blocked— iterations with idle lanes whose next window waits for the hit ring (a straggler of an
+           old window holds its flush); lanes = the idle ones
+  starved— iterations with idle lanes and no window left for the wave (the launch's tail)
 usage: trace_stats.py DIAG_LIB [--scene CornellBox-Glossy | --synthetic N] [--res 1024 --spp 8 --depth 16]
        [--opt NAME=VALUE ...]"""
 import argparse
@@ -25,7 +28,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "brown-cs2240-path-tracer_amd"))
 sys.path.insert(0, ROOT)
-KINDS = ["node", "leaf", "big", "none", "poolrun", "loop"]
+KINDS = ["node", "leaf", "big", "none", "poolrun", "loop", "blocked", "starved"]
 
 
 def main():
