@@ -262,11 +262,6 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
     // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-    // late flush (option trace_late; bit 16 of the `sparse` argument): a window whose stragglers hold
-    // the hit ring full while lanes idle is written back without them; a straggler then stores its
-    // own hit to the queue when it ends (one scattered store, rare)
-    const bool late_on = ((sparse >> 16) & 1) != 0;
-    sparse &= 0xffff;
     uint32_t wr = kWinRays;
     if (sparse > 0)
         while (wr > 1 && (uint64_t)count * (uint32_t)sparse < (uint64_t)nwaves * wr) wr >>= 1;
@@ -304,8 +299,6 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
     }
     uint32_t cur = 0;      // sequence number of the next entry to hand out (in window jl)
     uint32_t flushed = 0;  // sequence numbers below this are written back to wb.hitq
-    // sq: the lane's ray's sequence number; once its window went back without it (late flush), bit 31 |
-    // its queue entry (the hit's slot in wb.hitq) instead
     uint32_t sq = 0, p = 0;
     bool has = false;
     Ray r;
@@ -344,21 +337,10 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
         while (flushed < (jl + 1) * kWinRays) {
             const uint32_t jf = flushed / kWinRays;
             const bool handed = jf < jl || cur == jl * kWinRays + wv;
-            if (!handed) break;
-            uint32_t skip = 0;  // the window's entries still traced by the lanes made late here
-            const uint64_t strag = __ballot(has && sq < flushed + kWinRays);  // (late lanes: sq >= 2^31)
+            if (!handed || wave_any(has && sq < flushed + kWinRays)) break;
             const uint32_t wf = wtab[jf % kWinTab];
-            if (strag) {
-                // stragglers: wait for them, unless they keep idle lanes from the next window (late flush)
-                const bool blocked = late_on && __ballot(!has) != 0 && cur == jl * kWinRays + wv && nv > 0 &&
-                                     (jl + 2) * kWinRays - flushed > nring;
-                if (!blocked) break;
-                for (uint64_t m = strag; m; m &= m - 1)  // uniform, SGPRs: few lanes
-                    skip |= 1u << (__builtin_amdgcn_readlane((int)sq, (int)__builtin_ctzll(m)) - flushed);
-                if ((strag >> lane) & 1ull) sq = 0x80000000u | (wf * wr + (sq - flushed));
-            }
             const uint32_t fv = wcount(wf);
-            if (lane < fv && !((skip >> lane) & 1u)) wb.hitq[wf * wr + lane] = ring[(flushed + lane) & (nring - 1)];
+            if (lane < fv) wb.hitq[wf * wr + lane] = ring[(flushed + lane) & (nring - 1)];
             flushed += kWinRays;
         }
         // hand the next entries to idle lanes (wave-uniform control)
@@ -409,9 +391,7 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
         trav_advance<TRAV, COUNT, true, PRUN>(sc, r, s, stack, c);
 #endif
         if (has && trav_finished(s)) {
-            const int2 hv = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
-            if (sq >> 31) wb.hitq[sq & 0x7fffffffu] = hv;  // its window went back without it
-            else ring[sq & (nring - 1)] = hv;
+            ring[sq & (nring - 1)] = make_int2(s.best, __builtin_bit_cast(int, s.best_t));
             has = false;
         }
     }
@@ -1125,7 +1105,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     const int iters = 2 * (fp.max_depth + 1);
     // option trace_watchdog: tests of the failure report
     const uint32_t watchdog = ws.watchdog > 0 ? ws.watchdog : kTraceWatchdog;
-    const int sparse = std::max(0, std::min(ws.trace_sparse, 0xffff)) | (ws.trace_late ? 1 << 16 : 0);
+    const int sparse = std::max(0, std::min(ws.trace_sparse, 1 << 20));
     // option bf_slots < kBfSlots: tests of the recompute path
     const int bf_slots = ws.bf_slots >= 0 ? std::min(kBfSlots, ws.bf_slots) : kBfSlots;
     for (uint32_t fb = 0; fb < nframes; fb += F) {
@@ -1257,7 +1237,6 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.sort_bins = sort > 0 ? (sort >= 512 ? 512 : sort >= 64 ? 64 : 8) : 0;
     ws.trace_blocks = lo.trace_blocks;
     ws.trace_sparse = std::max(0, lo.trace_sparse);
-    ws.trace_late = lo.trace_late > 0;
     ws.region_perm = lo.region_perm > 0 ? 1 : 0;
     ws.trace_ring = lo.trace_ring;
     ws.bf_slots = lo.bf_slots;

@@ -145,10 +145,7 @@ KERNELS = {
     "mega_skip_lean16": {"PT_KERNEL": "mega", "PT_LEAF_SKIP": "1", "PT_TRAV": "lean16"},
     "wavefront_skip_1block_run2": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_WF_TRACE_BLOCKS": "1",
                                    "PT_POOL_RUN": "2"},
-    # the traversal kernel's late flush (option trace_late: a window whose stragglers hold the hit ring
-    # full is written back without them, each straggler storing its own hit): on the full grid, and on
-    # one block with the 128-entry ring (many windows per wave: the ring fills and flushes late often)
-    "wavefront_late": {"PT_KERNEL": "wavefront", "PT_TRACE_LATE": "1", "PT_MAILBOX": "0"},
+},
     "wavefront_late_1block_ring128": {"PT_KERNEL": "wavefront", "PT_TRACE_LATE": "1", "PT_MAILBOX": "0",
                                       "PT_WF_TRACE_BLOCKS": "1", "PT_TRACE_RING": "128"},
     "wavefront_late_sparse1_big8": {"PT_KERNEL": "wavefront", "PT_TRACE_LATE": "1", "PT_MAILBOX": "0",
@@ -161,7 +158,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
             "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
             "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS",
-            "PT_LEAF_REFINE", "PT_LEAF_SKIP", "PT_TRACE_LATE")
+            "PT_LEAF_REFINE", "PT_LEAF_SKIP")
 
 
 @pytest.fixture(params=list(KERNELS))
