@@ -145,11 +145,6 @@ KERNELS = {
     "mega_skip_lean16": {"PT_KERNEL": "mega", "PT_LEAF_SKIP": "1", "PT_TRAV": "lean16"},
     "wavefront_skip_1block_run2": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_WF_TRACE_BLOCKS": "1",
                                    "PT_POOL_RUN": "2"},
-},
-    "wavefront_late_1block_ring128": {"PT_KERNEL": "wavefront", "PT_TRACE_LATE": "1", "PT_MAILBOX": "0",
-                                      "PT_WF_TRACE_BLOCKS": "1", "PT_TRACE_RING": "128"},
-    "wavefront_late_sparse1_big8": {"PT_KERNEL": "wavefront", "PT_TRACE_LATE": "1", "PT_MAILBOX": "0",
-                                    "PT_TRACE_SPARSE": "1", "PT_BIG_LEAF": "8"},
 }
 
 
