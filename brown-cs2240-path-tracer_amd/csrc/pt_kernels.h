@@ -69,7 +69,6 @@ struct LaunchOpts {
     int bf_slots = -1;     // brute-force kernels: hit slots per lane (< kBfSlots: tests of the recompute path): -1 default
     int trace_blocks = 0;  // traversal / step kernels: cap on the grid (tests): 0 = occupancy-derived
     int trace_sparse = -1; // k_wf_trace: narrower windows when 32-entry ones keep < 1/n of the waves busy (n; 0 off): -1 default
-    int trace_dyn = -1;    // k_wf_trace: windows handed out by an atomic counter instead of statically: -1 default
     int region_perm = -1;  // k_wf_step_bf: camera batches dealt to regions by a permutation (WfBuffers::rq); -1 default
     int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
@@ -83,10 +82,7 @@ bool scene_fits_lds(const SceneView& sc);
 // path's state travels with its ray: queue entry i holds the ray AND the path state, and
 // a shade kernel writes the surviving path to its compacted slot of the other queue, so no
 // kernel gathers by path index.  Iterations alternate extension / shadow queues.
-enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_WATCHDOG = 2, WF_SNAP_CLAIM = 3, WF_RING = 4, WF_WIN0 = 5, WF_WIN1 = 6, WF_SNAP = 8,
-       WF_SNAP_WORDS = 16, WF_CTL_WORDS = 64 };
-// WF_WIN0 / WF_WIN1: k_wf_trace's next window of the extension / shadow queue when windows are handed
-// out dynamically (option trace_dyn); zeroed by the kernel that writes that queue
+enum { WF_COUNT0 = 0, WF_COUNT1 = 1, WF_WATCHDOG = 2, WF_SNAP_CLAIM = 3, WF_RING = 4, WF_SNAP = 8, WF_SNAP_WORDS = 16, WF_CTL_WORDS = 64 };
 // the control block holds WF_CTL_WORDS words per half of a dual-stream batch (wb_half)
 // iterations after which a trace wave gives up: it sets ctl[WF_WATCHDOG], the first such wave
 // leaves its scheduling state in ctl[WF_SNAP..], and the host reports an error
@@ -145,7 +141,6 @@ struct WfStreams {
     // per-call launch shape (LaunchOpts, filled by launch_wavefront)
     int trace_blocks = 0;  // cap on the trace / step grid (0: occupancy-derived)
     int trace_sparse = 0;  // k_wf_trace windows below 32 entries for short queues (LaunchOpts::trace_sparse)
-    bool trace_dyn = false;  // k_wf_trace windows handed out by an atomic counter (LaunchOpts::trace_dyn)
     int region_perm = 0;   // LaunchOpts::region_perm
     int trace_ring = 0;    // LaunchOpts::trace_ring
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)

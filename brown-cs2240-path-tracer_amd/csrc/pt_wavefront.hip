@@ -164,7 +164,6 @@ __global__ __launch_bounds__(256) void k_wf_generate(FrameParams fp, WfBuffers w
     if (p == 0) {
         wb.ctl[WF_COUNT0] = P;
         wb.ctl[WF_COUNT1] = 0;
-        wb.ctl[WF_WIN0] = 0;  // k_wf_trace's dynamic windows of this queue
     }
     // region layout (k_wf_step_bf, wb.nreg > 0): 64-path batch j goes to region j % nreg
     const uint32_t R = wb.nreg;
@@ -263,11 +262,6 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
     // the wave index is uniform: readfirstlane keeps everything derived from it in SGPRs
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-    // dynamic windows (option trace_dyn; bit 16 of `sparse`): each wave takes its next window from the
-    // queue's counter (one atomic per window) instead of the static interleave w, w + N, ...: a wave
-    // whose windows were cheap keeps working while others finish theirs
-    const bool dyn = ((sparse >> 16) & 1) != 0;
-    sparse &= 0xffff;
     uint32_t wr = kWinRays;
     if (sparse > 0)
         while (wr > 1 && (uint64_t)count * (uint32_t)sparse < (uint64_t)nwaves * wr) wr >>= 1;
@@ -276,16 +270,8 @@ __device__ __forceinline__ void wf_trace_body(SceneView sc, WfBuffers wb, int in
     const uint32_t lane = lane_id();
     constexpr uint32_t kNone = 0xffffffffu;
     uint32_t nstatic = 0;
-    uint32_t* const wctr = &wb.ctl[in_q ? WF_WIN1 : WF_WIN0];
     auto fetch = [&]() {  // this wave's next window (wave-uniform), or kNone
-        uint64_t wid;
-        if (dyn) {
-            uint32_t v = 0;
-            if (lane_id() == 0) v = atomicAdd(wctr, 1u);
-            wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-        } else {
-            wid = (uint64_t)(nstatic++) * nwaves + w;
-        }
+        const uint64_t wid = (uint64_t)(nstatic++) * nwaves + w;
         return wid < nwin ? (uint32_t)wid : kNone;
     };
     auto wcount = [&](uint32_t wid) { return min(wr, count - wid * wr); };
@@ -865,7 +851,6 @@ __global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneView sc, FramePar
     // EXT: extension queue -> shadow queue; else shadow queue -> extension queue
     const uint32_t count = wb.ctl[EXT ? WF_COUNT0 : WF_COUNT1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) wb.ctl[EXT ? WF_WIN1 : WF_WIN0] = 0;  // k_wf_trace's dynamic windows of the queue written here
     if (blockIdx.x * blockDim.x >= count) return;  // whole block past the queue
     const WfQueue& in = EXT ? wb.ext : wb.shd;
     const WfQueue& out = EXT ? wb.shd : wb.ext;
@@ -1120,7 +1105,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     const int iters = 2 * (fp.max_depth + 1);
     // option trace_watchdog: tests of the failure report
     const uint32_t watchdog = ws.watchdog > 0 ? ws.watchdog : kTraceWatchdog;
-    const int sparse = std::max(0, std::min(ws.trace_sparse, 0xffff)) | (ws.trace_dyn ? 1 << 16 : 0);
+    const int sparse = std::max(0, std::min(ws.trace_sparse, 1 << 20));
     // option bf_slots < kBfSlots: tests of the recompute path
     const int bf_slots = ws.bf_slots >= 0 ? std::min(kBfSlots, ws.bf_slots) : kBfSlots;
     for (uint32_t fb = 0; fb < nframes; fb += F) {
@@ -1252,7 +1237,6 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.sort_bins = sort > 0 ? (sort >= 512 ? 512 : sort >= 64 ? 64 : 8) : 0;
     ws.trace_blocks = lo.trace_blocks;
     ws.trace_sparse = std::max(0, lo.trace_sparse);
-    ws.trace_dyn = lo.trace_dyn > 0;
     ws.region_perm = lo.region_perm > 0 ? 1 : 0;
     ws.trace_ring = lo.trace_ring;
     ws.bf_slots = lo.bf_slots;
