@@ -1131,6 +1131,11 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
         if (s->leaf_sizes.size() > (size_t)kMaxPre && s->leaf_sizes[kMaxPre] >= T) T = s->leaf_sizes[kMaxPre] + 1;
         int np = 0;
         while (np < (int)s->pre.size() && s->pre[(size_t)np].n >= T) ++np;
+        // more big leaves than the table holds: the pass would raise the threshold to T and the big
+        // leaves left out (big_leaf <= n < T) would lose their chunk walks and cooperative turns, a
+        // cost the probe below does not weigh — AUTO keeps the traversal's own big-leaf machinery then
+        // (advisor r05; leaf_pre=1 still forces the pass)
+        if (pre_opt != 1 && T > view.big_leaf) np = 0;
         if (np > 0 && pre_opt != 1) {
             std::lock_guard<std::mutex> lk(s->pre_mu);
             ProbeCamera pc{};

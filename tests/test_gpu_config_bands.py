@@ -175,3 +175,29 @@ def test_cornellbox2_all_meshes_1024_depth16_rows_bitexact(tmp_path, ptopts):
         prof = s.profile_read()
     assert "k_wf_leafpass" in prof, prof
     assert_same_bits(img2, img, "leaf_pre=1 vs the default")
+
+
+def test_more_big_leaves_than_the_table_keeps_the_traversal(tmp_path, ptopts):
+    """More leaves of >= big_leaf entries than the leaf pass's table holds (CornellBox2 with every mesh
+    at big_leaf 64: ten such leaves, the table keeps 8): the pass would raise the threshold above the
+    ninth and strip the others of their chunk walks, so AUTO keeps the traversal's own big-leaf
+    machinery (advisor r05) — and the image is the oracle's, and the forced pass's, bit for bit."""
+    from conftest import pack_with_node
+    p = pack_with_node(os.path.join(SCENES, "scene_assets", "CornellBox2.xml"), str(tmp_path / "cb2"), "--all-meshes",
+                       "--native-bvh")
+    ptopts.set("big_leaf", "64")
+    meta = p.meta_for(256, 256)
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        img = s.render(meta, 0, 2, 1, 16, pt_amd.MODE_WAVEFRONT)
+        prof = s.profile_read()
+    assert "k_wf_trace" in prof and "k_wf_leafpass" not in prof, prof
+    ref, _ = oracle.render(p.triangle_data, p.bvh_data, meta, 0, 2, 1, 16, y0=120, y1=136, nthreads=ORACLE_THREADS)
+    assert_same_bits(img[120:136], ref, "CornellBox2 big_leaf 64 rows 120..136")
+    ptopts.set("leaf_pre", "1")
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.profile_enable(True)
+        img2 = s.render(meta, 0, 2, 1, 16, pt_amd.MODE_WAVEFRONT)
+        prof2 = s.profile_read()
+    assert "k_wf_leafpass" in prof2, prof2
+    assert_same_bits(img2, img, "leaf_pre=1 vs AUTO")
