@@ -89,7 +89,8 @@ def cpu_baseline(tri, bvh, meta, depth, target_s=12.0):
                       f"same workload (depth {depth}), {threads} OpenMP threads, {c['samples']} samples in {dt:.2f} s"}
 
 
-def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int, field: str = "hbm_bytes_per_launch"):
+def load_traffic(kernel_prefix, scene: str, bvh: str, W: int, H: int, spp: int, depth: int, world: int,
+                 field: str = "hbm_bytes_per_launch"):
     """Per-launch PMC figure of the render kernel (HBM bytes, or `valu_issue`) from the committed
     rocprofv3 passes (scripts/collect_traffic.sh -> profiles/traffic.json), when they match this
     configuration: (value, source) or None."""
@@ -100,7 +101,8 @@ def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int
     except (OSError, ValueError):
         return None
     key = f"{W}x{H}x{spp}x{depth}x{world}"
-    cands = {k: v for k, v in t.get(key, {}).items() if k.startswith(kernel_prefix) and field in v}
+    entry = traffic_entry(t, scene, bvh, key) or {}
+    cands = {k: v for k, v in entry.items() if k.startswith(kernel_prefix) and isinstance(v, dict) and field in v}
     # the timed instances: COUNT=false (template argument 4 of k_wf_step_bf<EXT, LDS, rcp, COUNT,
     # GEN> and of k_wf_trace<LDS, TRAV, COUNT, RING, PRUN> counted from 1 as 3; round 3's profiles name
     # a sixth k_wf_step_bf argument, the removed opt-in CULL, after COUNT); averaged per launch,
@@ -121,7 +123,7 @@ def load_traffic(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int
     timed = [k for k in cands if timed_instance(k)] or list(cands)
     if not timed:
         return None
-    src = "profiles/traffic.json[" + key + "]: " + t[key].get("_source", "rocprofv3 PMC passes (scripts/collect_traffic.sh)")
+    src = "profiles/traffic.json[" + key + "]: " + entry.get("_source", "rocprofv3 PMC passes (scripts/collect_traffic.sh)")
     wts = [cands[k].get("dispatches") for k in timed]
     if all(wts):
         return sum(cands[k][field] * w for k, w in zip(timed, wts)) / sum(wts), src
@@ -229,7 +231,20 @@ class GpuStateSampler:
                    for v in [[s[k] for s in self.samples if k in s]]}}
 
 
-def load_valu_exec(W: int, H: int, spp: int, depth: int, world: int, weights: dict):
+def traffic_entry(t: dict, scene: str, bvh: str, key: str):
+    """profiles/traffic.json's entry for this workload: the scene- and tree-qualified key (written by
+    scripts/summarize_traffic.py since round 6), else the plain size key when its source names the
+    same scene (older entries; reference trees only)."""
+    q = t.get(f"{scene}|{bvh}|{key}")
+    if q is not None:
+        return q
+    e = t.get(key)
+    if e and bvh == "reference" and f"({scene}.xml " in e.get("_source", ""):
+        return e
+    return None
+
+
+def load_valu_exec(scene: str, bvh: str, W: int, H: int, spp: int, depth: int, world: int, weights: dict):
     """The VALU work the step's kernels actually execute, from the committed PMC pass
     (scripts/collect_traffic.sh -> profiles/traffic.json, this configuration's key): per kernel family
     (k_wf_step, k_wf_trace, k_wf_leafpass, ...; instances summed by their dispatches) the
@@ -239,22 +254,34 @@ def load_valu_exec(W: int, H: int, spp: int, depth: int, world: int, weights: di
     (`weights`: family -> ms).  Unlike valu_alg (the reference's work at this rate) it counts what the
     kernels do, so it stays below 1.  None without a matching PMC pass."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
+    key = f"{W}x{H}x{spp}x{depth}x{world}"
     try:
         with open(path) as f:
-            t = json.load(f).get(f"{W}x{H}x{spp}x{depth}x{world}")
+            t = traffic_entry(json.load(f), scene, bvh, key)
         with open(os.path.join(ROOT, "profiles", "valu_calibration.json")) as f:
             k_cal = json.load(f)["k_active"]
     except (OSError, ValueError, KeyError):
         return None
     if not t:
         return None
+
+    def family(name):  # the bench's kernel names (pt_profile_read); None for the counted render's instances
+        f = name.split("<")[0]
+        args = [a.strip() for a in name[name.find("<") + 1:name.rfind(">")].split(",")] if "<" in name else []
+        counted = {"k_wf_step_bf": 3, "k_wf_trace": 2, "k_wf_trace_pre": 2, "k_wf_shade": 1, "k_wf_generate": 0}
+        if f in counted and len(args) > counted[f] and args[counted[f]] == "true":
+            return None
+        if f == "k_wf_shade":
+            return "k_wf_shade_ext" if args and args[0] == "true" else "k_wf_shade_shadow"
+        return {"k_wf_step_bf": "k_wf_step", "k_wf_trace_pre": "k_wf_trace"}.get(f, f)
     fam = {}
     for name, e in t.items():
         v = e.get("valu_counters") if isinstance(e, dict) else None
         if not v or not v.get("GRBM_GUI_ACTIVE") or not v.get("SQ_ACTIVE_INST_VALU"):
             continue
-        f = name.split("<")[0]
-        f = "k_wf_step" if f == "k_wf_step_bf" else ("k_wf_trace" if f == "k_wf_trace_pre" else f)
+        f = family(name)
+        if f is None:
+            continue
         n = e.get("dispatches") or 1
         a = fam.setdefault(f, [0.0, 0.0, 0.0])
         a[0] += v["SQ_ACTIVE_INST_VALU"] * n
@@ -273,7 +300,7 @@ def load_valu_exec(W: int, H: int, spp: int, depth: int, world: int, weights: di
             "def": "per kernel: (k x SQ_ACTIVE_INST_VALU / (128 x GRBM_GUI_ACTIVE)) x (SQ_THREAD_CYCLES_VALU / (64 x "
                    "SQ_ACTIVE_INST_VALU)), the executed fraction of the f32 lane-op peak; the step: weighted by each "
                    "kernel's time in the warm-up step",
-            "source": "profiles/traffic.json[" + f"{W}x{H}x{spp}x{depth}x{world}" + "] (scripts/collect_traffic.sh) "
+            "source": f"profiles/traffic.json[{scene}|{bvh}|{key}] (scripts/collect_traffic.sh) "
                       "+ profiles/valu_calibration.json"}
 
 
@@ -292,11 +319,11 @@ def launch_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
-def traffic_note(kernel_prefix, W: int, H: int, spp: int, depth: int, world: int, field: str):
+def traffic_note(kernel_prefix, scene: str, bvh: str, W: int, H: int, spp: int, depth: int, world: int, field: str):
     """A text field of the render kernel's entry in profiles/traffic.json (e.g. the VALU calibration)."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
-            t = json.load(f).get(f"{W}x{H}x{spp}x{depth}x{world}", {})
+            t = traffic_entry(json.load(f), scene, bvh, f"{W}x{H}x{spp}x{depth}x{world}") or {}
     except (OSError, ValueError):
         return None
     for k, v in t.items():
@@ -590,9 +617,10 @@ def main():
         pre = prefixes.get(kernel, (kernel + "<",))
         # the committed PMC / trace figures describe the full configuration (not a rank's share)
         full = args.share_of <= 1
-        traffic = load_traffic(pre, W, H, args.spp, args.depth, world) if full else None
-        valu = load_traffic(pre, W, H, args.spp, args.depth, world, field="valu_issue") if full else None
-        valu_cal = traffic_note(pre, W, H, args.spp, args.depth, world, "valu_issue_calibration")
+        traffic = load_traffic(pre, args.scene, args.bvh, W, H, args.spp, args.depth, world) if full else None
+        valu = (load_traffic(pre, args.scene, args.bvh, W, H, args.spp, args.depth, world, field="valu_issue")
+                if full else None)
+        valu_cal = traffic_note(pre, args.scene, args.bvh, W, H, args.spp, args.depth, world, "valu_issue_calibration")
         tu = load_trace_union(W, H, args.spp, args.depth, world) if full else None
         if tu and tu.get("kernel") != kernel:
             tu = None
@@ -680,7 +708,7 @@ def main():
                                                      "source": valu[1]} if valu else None),
                          "kernels_ms_warmup_step": {k: round(v["total_ms"] / max(args.warmup, 1), 3)
                                                     for k, v in prof_warm.items()},
-                         "valu_exec": (load_valu_exec(W, H, args.spp, args.depth, world,
+                         "valu_exec": (load_valu_exec(args.scene, args.bvh, W, H, args.spp, args.depth, world,
                                                       {k: v["total_ms"] / max(args.warmup, 1) for k, v in prof_warm.items()})
                                        if full else None),
                          "render_ms_steps": [round(x, 2) for x in render_ms]},

@@ -25,7 +25,9 @@ def load(tag, counters):
     for f in glob.glob(f"{SRC}/{tag}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] in counters:
-                k = (r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Dispatch_Id"])
+                # (anonymous-namespace kernels, e.g. k_wf_leafpass: drop the namespace before the cut at "(")
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+                k = (name.split("(")[0].replace("void ", ""), r["Dispatch_Id"])
                 agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for (k, _), cs in agg.items():
@@ -54,6 +56,10 @@ def main():
     line = [json.loads(x) for x in open(f"{SRC}/fetch.log") if x.startswith("{")][0]
     m = re.search(r"(\d+)x(\d+) (\d+)spp depth (\d+)", line["config"]["workload"])
     key = f"{m.group(1)}x{m.group(2)}x{m.group(3)}x{m.group(4)}x{line['n_gpus']}"
+    # the same entry under a key that names the scene and tree too (bench.py reads this one first: the
+    # plain key is shared by every scene rendered at the same size, spp and depth)
+    scene = line["config"]["workload"].split(".xml")[0]
+    qkey = f"{scene}|{line['config'].get('bvh', 'reference')}|{key}"
     path = sys.argv[1] if len(sys.argv) > 1 else "profiles/traffic.json"
     t = json.load(open(path)) if os.path.exists(path) else {}
     t[key] = {"_source": "scripts/collect_traffic.sh: rocprofv3 --pmc passes FETCH_SIZE | WRITE_SIZE | SQ_ACTIVE_INST_VALU.. "
@@ -71,6 +77,7 @@ def main():
             e["valu_lane_util"] = v.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * v["SQ_ACTIVE_INST_VALU"]) if v.get("SQ_ACTIVE_INST_VALU") else None
             e["valu_counters"] = v
         t[key][short] = e
+    t[qkey] = t[key]
     json.dump(t, open(path, "w"), indent=1)
     print(json.dumps(t[key], indent=1))
 
