@@ -80,7 +80,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"pre_ratio", OPT_INT, nullptr},     {"leaf_refine", OPT_BOOL, nullptr},
     {"wf_paths", OPT_INT, nullptr},      {"wf_trace_blocks", OPT_INT, nullptr}, {"trace_watchdog", OPT_INT, nullptr},
     {"leaf_bvh", OPT_INT, nullptr},      {"leaf_walk", OPT_BOOL, nullptr},   {"leaf_pool", OPT_BOOL, nullptr},   {"pool_run", OPT_ENUM, "2|4"},
-    {"leaf_skip", OPT_BOOL, nullptr},    {"shade_lds", OPT_BOOL, nullptr},
+    {"leaf_skip", OPT_BOOL, nullptr},
     {"mb_uid_order", OPT_ENUM, "forward|reverse"},
     {"reduce", OPT_ENUM, "rccl|ordered"},
 };
@@ -918,7 +918,6 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
     lo.region_perm = o.flag("region_perm", kRegionPermDefault);
     lo.trace_ring = (int)o.num("trace_ring", 0);
-    lo.shade_lds = o.flag("shade_lds", 1);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);
     lo.bf_slots = (int)o.num("bf_slots", -1);

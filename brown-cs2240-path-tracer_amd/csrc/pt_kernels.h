@@ -69,7 +69,6 @@ struct LaunchOpts {
     int bf_slots = -1;     // brute-force kernels: hit slots per lane (< kBfSlots: tests of the recompute path): -1 default
     int trace_blocks = 0;  // traversal / step kernels: cap on the grid (tests): 0 = occupancy-derived
     int trace_sparse = -1; // k_wf_trace: narrower windows when 32-entry ones keep < 1/n of the waves busy (n; 0 off): -1 default
-    int shade_lds = 1;     // k_wf_shade: materials and lights staged in LDS when they fit (option shade_lds)
     int region_perm = -1;  // k_wf_step_bf: camera batches dealt to regions by a permutation (WfBuffers::rq); -1 default
     int trace_ring = 0;    // k_wf_trace's hit ring: 0 auto, 128 or 256
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
@@ -142,7 +141,6 @@ struct WfStreams {
     // per-call launch shape (LaunchOpts, filled by launch_wavefront)
     int trace_blocks = 0;  // cap on the trace / step grid (0: occupancy-derived)
     int trace_sparse = 0;  // k_wf_trace windows below 32 entries for short queues (LaunchOpts::trace_sparse)
-    bool shade_lds = true;  // k_wf_shade stages materials and lights in LDS (LaunchOpts::shade_lds)
     int region_perm = 0;   // LaunchOpts::region_perm
     int trace_ring = 0;    // LaunchOpts::trace_ring
     int bf_slots = -1;     // hit slots per lane of the brute-force kernels (-1: kBfSlots)

@@ -845,32 +845,13 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
 // 8M-path batch) cost more than the shading itself.
 constexpr uint32_t kShadeBlock = 1024;
 
-// k_wf_shade's materials and lights in LDS (option shade_lds, default on) when they fit: each entry's
-// path logic reads its material(s) and, after an extension hit, a light triangle — loads that
-// otherwise wait behind the hit record's own round trip
-constexpr uint32_t kShadeLdsMax = 16 * 1024;
-__host__ __device__ inline uint32_t shade_lds_bytes(const SceneView& sc) {
-    return (uint32_t)(sc.n_mats * sizeof(Material) + (sc.n_lights + 1) * sizeof(Light));
-}
-
 template <bool EXT, bool COUNT>
 __global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneView sc, FrameParams fp, WfBuffers wb, Counters* cnt_out,
-                                                          int bins, int stage) {
+                                                          int bins) {
     // EXT: extension queue -> shadow queue; else shadow queue -> extension queue
     const uint32_t count = wb.ctl[EXT ? WF_COUNT0 : WF_COUNT1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x * blockDim.x >= count) return;  // whole block past the queue
-    if (stage) {  // block-uniform: materials, then the light table, copied into LDS (same bytes)
-        extern __shared__ __attribute__((aligned(16))) char shade_smem[];
-        float4* dst = reinterpret_cast<float4*>(shade_smem);
-        const uint32_t nm = (uint32_t)(sc.n_mats * sizeof(Material) / 16), nl = (uint32_t)((sc.n_lights + 1) * sizeof(Light) / 16);
-        const float4* ms = reinterpret_cast<const float4*>(sc.mats);
-        const float4* ls = reinterpret_cast<const float4*>(sc.lights);
-        for (uint32_t k = threadIdx.x; k < nm + nl; k += blockDim.x) dst[k] = k < nm ? ms[k] : ls[k - nm];
-        __syncthreads();
-        sc.mats = reinterpret_cast<const Material*>(shade_smem);
-        sc.lights = reinterpret_cast<const Light*>(shade_smem + 16 * (size_t)nm);
-    }
     const WfQueue& in = EXT ? wb.ext : wb.shd;
     const WfQueue& out = EXT ? wb.shd : wb.ext;
     uint32_t* out_count = &wb.ctl[EXT ? WF_COUNT1 : WF_COUNT0];
@@ -1217,13 +1198,12 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 }
 #undef PT_TRACE
             }
-            const uint32_t sl = ws.shade_lds && shade_lds_bytes(sc) <= kShadeLdsMax ? shade_lds_bytes(sc) : 0u;
             if ((it & 1) == 0)
-                PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), sl, st, sc, fp,
-                          w, cnt, ws.sort_bins, sl ? 1 : 0);
+                PT_LAUNCH(KID_WF_SHADE_EXT, st, (k_wf_shade<true, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc, fp,
+                          w, cnt, ws.sort_bins);
             else
-                PT_LAUNCH(KID_WF_SHADE_SHADOW, st, (k_wf_shade<false, COUNT>), dim3(sblocks), dim3(kShadeBlock), sl, st, sc,
-                          fp, w, cnt, ws.sort_bins, sl ? 1 : 0);
+                PT_LAUNCH(KID_WF_SHADE_SHADOW, st, (k_wf_shade<false, COUNT>), dim3(sblocks), dim3(kShadeBlock), 0, st, sc,
+                          fp, w, cnt, ws.sort_bins);
             return hipSuccess;
         };
         for (int it = 0; it < iters; ++it) {
@@ -1257,7 +1237,6 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.sort_bins = sort > 0 ? (sort >= 512 ? 512 : sort >= 64 ? 64 : 8) : 0;
     ws.trace_blocks = lo.trace_blocks;
     ws.trace_sparse = std::max(0, lo.trace_sparse);
-    ws.shade_lds = lo.shade_lds != 0;
     ws.region_perm = lo.region_perm > 0 ? 1 : 0;
     ws.trace_ring = lo.trace_ring;
     ws.bf_slots = lo.bf_slots;

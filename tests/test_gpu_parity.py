@@ -145,10 +145,6 @@ KERNELS = {
     "mega_skip_lean16": {"PT_KERNEL": "mega", "PT_LEAF_SKIP": "1", "PT_TRAV": "lean16"},
     "wavefront_skip_1block_run2": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_WF_TRACE_BLOCKS": "1",
                                    "PT_POOL_RUN": "2"},
-    # the shade kernels' materials and lights from global memory instead of LDS (option shade_lds)
-    "wavefront_noshadelds": {"PT_KERNEL": "wavefront", "PT_SHADE_LDS": "0", "PT_MAILBOX": "0"},
-    "wavefront_shadelds_1block_sort8": {"PT_KERNEL": "wavefront", "PT_SHADE_LDS": "1", "PT_MAILBOX": "0",
-                                        "PT_WF_TRACE_BLOCKS": "1", "PT_SORT": "8"},
 }
 
 
@@ -157,7 +153,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
             "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
             "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS",
-            "PT_LEAF_REFINE", "PT_LEAF_SKIP", "PT_SHADE_LDS")
+            "PT_LEAF_REFINE", "PT_LEAF_SKIP")
 
 
 @pytest.fixture(params=list(KERNELS))
