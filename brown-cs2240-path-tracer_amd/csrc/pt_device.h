@@ -1039,6 +1039,14 @@ __device__ __forceinline__ bool trav_step_lean(const SceneView& sc, const Ray& r
             decide = lean_leaf_loop<K, COUNT, FAST_RCP, BIG, PRE>(sc, r, s, cnt);
     } else if (state == 0) {
         decide = lean_node_unit<COUNT, PRE>(sc, r, s, cnt);
+        // further steps in the same turn for lanes that stay in node state (SceneView::node_steps)
+        for (int k = 1; k < sc.node_steps; ++k) {  // uniform
+            if (decide) lean_decide(s, stack);
+            decide = false;
+            const bool node = (s.fl & (TF_LEAF | TF_DONE | ((BIG && !PRE) ? TF_PARK : 0))) == 0;
+            if (!wave_any(node)) break;
+            if (node) decide = lean_node_unit<COUNT, PRE>(sc, r, s, cnt);
+        }
     }
     if (decide) lean_decide(s, stack);
 #if PT_TRACE_STATS

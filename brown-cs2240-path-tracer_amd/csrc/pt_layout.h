@@ -156,6 +156,9 @@ struct SceneView {
     // (1 = plain majority; a leaf turn costs up to K triangle tests, a node turn one node
     // step, so node turns that feed lanes into their leaves pay off); 0 = pipeline default
     int32_t node_bias;
+    // node steps per node turn of the lean traversal (option node_steps; 1 = one): lanes still in node
+    // state after a step take the next in the same turn, without the loop's bookkeeping in between
+    int32_t node_steps;
     // mailbox (SceneView::mailbox != 0 when the scene has <= 64 distinct leaf entries): the
     // record of uid u is tris[mb_base + u]; lmask at byte offset off_lmask (inside the span)
     int32_t mailbox;

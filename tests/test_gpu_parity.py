@@ -145,6 +145,11 @@ KERNELS = {
     "mega_skip_lean16": {"PT_KERNEL": "mega", "PT_LEAF_SKIP": "1", "PT_TRAV": "lean16"},
     "wavefront_skip_1block_run2": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_WF_TRACE_BLOCKS": "1",
                                    "PT_POOL_RUN": "2"},
+    # several node steps per node turn of the lean traversal (option node_steps)
+    "wavefront_nodesteps2": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "2", "PT_MAILBOX": "0"},
+    "wavefront_nodesteps3_big8_1block": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "3", "PT_MAILBOX": "0",
+                                         "PT_BIG_LEAF": "8", "PT_WF_TRACE_BLOCKS": "1"},
+    "mega_nodesteps2_lean4": {"PT_KERNEL": "mega", "PT_NODE_STEPS": "2", "PT_TRAV": "lean4"},
 }
 
 
@@ -153,7 +158,7 @@ ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS"
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
             "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
             "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS",
-            "PT_LEAF_REFINE", "PT_LEAF_SKIP")
+            "PT_LEAF_REFINE", "PT_LEAF_SKIP", "PT_NODE_STEPS")
 
 
 @pytest.fixture(params=list(KERNELS))
