@@ -782,7 +782,7 @@ int pt_scene_create(const float* triangle_data, size_t triangle_len, const float
     s->view.max_stack = (int32_t)L.info.max_stack;
     s->view.fast_rcp = L.fast_rcp ? 1 : 0;
     s->view.node_bias = 0;  // per-pipeline default (launch_wavefront / launch_megakernel)
-    s->view.node_steps = 1;
+    s->view.node_steps = 0;  // per-pipeline default (launch_wavefront / launch_megakernel)
     s->view.off_tris = (uint32_t)(o_tris - o_nodes);
     s->view.off_mats = (uint32_t)(o_mats - o_nodes);
     s->view.off_lights = (uint32_t)(o_lights - o_nodes);
@@ -1074,7 +1074,7 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     SceneView view = s->view;
     const Opts o = opts_snapshot();
     if (o.has("node_bias")) view.node_bias = std::max(1L, o.num("node_bias", 1));  // A/B runs
-    view.node_steps = (int32_t)std::max(1L, std::min(4L, o.num("node_steps", 1)));
+    if (o.has("node_steps")) view.node_steps = (int32_t)std::max(1L, std::min(8L, o.num("node_steps", 1)));
     // big leaves (lean traversal): a ray reaching a leaf of >= big_leaf entries has it tested by the
     // whole wave (pt_device.h big_turn); default 128 (MedievalBoat 2.3x, in-process A/B; 64 is 1.5 %
     // faster there but 12 % slower on the 1M-triangle synthetic scene, whose many 64..127-entry

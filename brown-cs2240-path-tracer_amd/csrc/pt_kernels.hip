@@ -404,6 +404,9 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& scene, const
                              hipStream_t stream) {
     SceneView sc = scene;
     if (sc.node_bias <= 0) sc.node_bias = kMegaNodeBias;
+    // one node step per turn: more lose in the megakernel (Glossy 256^2: 3 steps -9 %, 8 -15 %,
+    // profiles/r06h_ab_glossy_small_mega.log)
+    if (sc.node_steps <= 0) sc.node_steps = 1;
     if (!accum) { nframes = 1; stride = 1; }
     if (lo.literal) {
         dim3 grid((fp.width + 15) / 16, (fp.height + 15) / 16), block(kMegaBlock);

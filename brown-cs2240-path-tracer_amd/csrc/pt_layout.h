@@ -156,7 +156,8 @@ struct SceneView {
     // (1 = plain majority; a leaf turn costs up to K triangle tests, a node turn one node
     // step, so node turns that feed lanes into their leaves pay off); 0 = pipeline default
     int32_t node_bias;
-    // node steps per node turn of the lean traversal (option node_steps; 1 = one): lanes still in node
+    // node steps per node turn of the lean traversal (option node_steps, 1..8; 0 = the pipeline's
+    // default: 4 wavefront, 1 megakernel): lanes still in node
     // state after a step take the next in the same turn, without the loop's bookkeeping in between
     int32_t node_steps;
     // mailbox (SceneView::mailbox != 0 when the scene has <= 64 distinct leaf entries): the

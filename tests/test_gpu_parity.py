@@ -145,8 +145,12 @@ KERNELS = {
     "mega_skip_lean16": {"PT_KERNEL": "mega", "PT_LEAF_SKIP": "1", "PT_TRAV": "lean16"},
     "wavefront_skip_1block_run2": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_WF_TRACE_BLOCKS": "1",
                                    "PT_POOL_RUN": "2"},
-    # several node steps per node turn of the lean traversal (option node_steps)
+    # node steps per node turn of the lean traversal (option node_steps; wavefront default 4, megakernel 1)
+    "wavefront_nodesteps1": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "1", "PT_MAILBOX": "0"},
     "wavefront_nodesteps2": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "2", "PT_MAILBOX": "0"},
+    "wavefront_nodesteps8_nopool": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "8", "PT_MAILBOX": "0",
+                                    "PT_LEAF_POOL": "0"},
+    "mega_nodesteps4": {"PT_KERNEL": "mega", "PT_NODE_STEPS": "4"},
     "wavefront_nodesteps3_big8_1block": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "3", "PT_MAILBOX": "0",
                                          "PT_BIG_LEAF": "8", "PT_WF_TRACE_BLOCKS": "1"},
     "mega_nodesteps2_lean4": {"PT_KERNEL": "mega", "PT_NODE_STEPS": "2", "PT_TRAV": "lean4"},
