@@ -986,7 +986,8 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     size_t oq[6];
     for (int k = 0; k < 6; ++k) oq[k] = take((k % 3 == 0 ? 32 : 16) * qn);
     const size_t o_p0 = take(16 * qn), o_p1 = take(16 * qn), o_p2 = take(8 * qn), o_hit = take(8 * qn),
-                 o_ctl = take(4 * kMaxParts * WF_CTL_WORDS), o_rcnt = take(4 * kMaxParts * 3 * kRegions);
+                 o_ctl = take(4 * kMaxParts * WF_CTL_WORDS), o_rcnt = take(4 * kMaxParts * 3 * kRegions),
+                 o_cam = take(2 * 64 * sizeof(float4));
     if (hipMalloc(&s->d_wf, off) != hipSuccess) {
         s->d_wf = nullptr;
         (void)hipGetLastError();  // the failed allocation is reported here, not by a later call
@@ -1002,6 +1003,7 @@ int ensure_wavefront(pt_scene* s, uint64_t paths) {
     w.hitq = reinterpret_cast<int2*>(b + o_hit);
     w.ctl = reinterpret_cast<uint32_t*>(b + o_ctl);
     w.rcnt = reinterpret_cast<uint32_t*>(b + o_rcnt);
+    w.camtab = f4(o_cam);
     if (hipMemset(w.ctl, 0, 4 * kMaxParts * WF_CTL_WORDS) != hipSuccess ||
         hipMemset(w.rcnt, 0, 4 * kMaxParts * 3 * kRegions) != hipSuccess)
         return fail(PT_ERR_HIP, "hipMemset wavefront control words");

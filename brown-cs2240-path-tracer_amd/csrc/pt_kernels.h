@@ -121,6 +121,8 @@ struct WfBuffers {
     // whole buffer's qcap: a part's pres is offset like its queues); nullptr when the scene has none
     uint64_t* pres;
     uint32_t pres_stride;
+    // per distinct entry, the camera-origin parts of the triangle test (k_wf_camtab; 2 x 64 float4)
+    float4* camtab;
 };
 constexpr uint32_t kRegions = 512;
 // queue slack (entries per part = 64 * this): regions of R <= kRegions hold ceil(batches / R)

@@ -513,11 +513,29 @@ __device__ __forceinline__ int bf_replay_stackless(const SceneView& sc, const Ra
     return best;
 }
 
+// Camera batches (CAM: every ray of the batch starts at the camera, fp.cam — the fused kernel's GEN
+// launch): the parts of the triangle test that depend on the origin and the entry only — s = o - v0,
+// s x e1 and e2 . (s x e1) — are the same for every camera ray, so k_wf_camtab computes them once
+// per render per entry, with the same functions in the same order (so the same bits), and phase 1
+// reads them through the scalar cache: camtab[2u] = (s, e2 . (s x e1)), camtab[2u + 1] = (s x e1, 0).
+__global__ void k_wf_camtab(SceneView sc, FrameParams fp, float4* camtab) {
+    const int u = (int)threadIdx.x;
+    if (u >= sc.n_tris - sc.mb_base) return;
+    const TriRec tr = load_tri(sc.tris, sc.mb_base + u);
+    const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
+    const f3 o = mk(fp.cam[0], fp.cam[1], fp.cam[2]);  // camera_ray's origin
+    const f3 sv = o - v0;
+    const f3 sce1 = cross(sv, e1);
+    camtab[2 * u] = make_float4(sv.x, sv.y, sv.z, dot(e2, sce1));
+    camtab[2 * u + 1] = make_float4(sce1.x, sce1.y, sce1.z, 0.0f);
+}
+
 // Closest hit of the 64 rays of one batch (lane = ray; `valid` false lanes give no hit):
 // phase 1 + phase 2 above.  Returns the record (or -1) and its t in t_out.
-template <bool FAST_RCP, bool COUNT>
+template <bool FAST_RCP, bool COUNT, bool CAM = false>
 __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris, const Ray& r, bool valid, float* slot,
-                                          int nslots, const LStack32& stack, Counters& c, float& t_out PH_PARAM) {
+                                          int nslots, const LStack32& stack, Counters& c, float& t_out,
+                                          const float4* camtab PH_PARAM) {
     const int U = sc.n_tris - sc.mb_base;
     // phase 1: every distinct entry against all 64 rays.  The test is tri_hit's arithmetic cut
     // after u: when no lane passes the det and u tests (the early-out chain of
@@ -530,10 +548,15 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
         PH_ITER(PH_P1);
         const TriRec tr = load_tri_scalar(gtris, sc.mb_base + u);
         const f3 v0 = mk(tr.a.x, tr.a.y, tr.a.z), e1 = mk(tr.a.w, tr.b.x, tr.b.y), e2 = mk(tr.b.z, tr.b.w, tr.c);
+        float4 ca = make_float4(0, 0, 0, 0);
+        if constexpr (CAM) {
+            const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(camtab + 2 * u);
+            ca = make_float4(f[0], f[1], f[2], f[3]);
+        }
         const f3 rce2 = cross(r.d, e2);
         const float det = dot(e1, rce2);
         const float inv_det = FAST_RCP ? rcp_rn(det) : 1.0f / det;
-        const f3 sv = r.o - v0;
+        const f3 sv = CAM ? mk(ca.x, ca.y, ca.z) : r.o - v0;
         const float bu = inv_det * dot(sv, rce2);
         const bool ok_det = !(det > -1e-8f && det < 1e-8f), ok_lo = !(bu < 0.0f), ok_hi = !(bu > 1.0f);
         const bool ok_u = valid & ok_det & ok_lo & ok_hi;
@@ -543,9 +566,18 @@ __device__ __forceinline__ int bf_closest(const SceneView& sc, const Tri* gtris,
              __builtin_amdgcn_ballot_w64(ok_lo) & __builtin_amdgcn_ballot_w64(ok_hi)) == 0)
             continue;  // wave-uniform
         PH_ITER(PH_P1FULL);
-        const f3 sce1 = cross(sv, e1);
+        f3 sce1;
+        float tn;
+        if constexpr (CAM) {
+            const __attribute__((address_space(4))) float* f = (const __attribute__((address_space(4))) float*)(camtab + 2 * u + 1);
+            sce1 = mk(f[0], f[1], f[2]);
+            tn = ca.w;
+        } else {
+            sce1 = cross(sv, e1);
+            tn = dot(e2, sce1);
+        }
         const float bv = inv_det * dot(r.d, sce1);
-        const float t = inv_det * dot(e2, sce1);
+        const float t = inv_det * tn;
         const bool h = ok_u & !(bv < 0.0f) & !(bu + bv > 1.0f) & (t > 1e-8f);
         if (h) {
             if (nh < nslots) slot[64 * nh] = t;
@@ -640,7 +672,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_wf_trace_bf(SceneView sc, WfBuf
 #if PT_PHASE_STATS
         PhaseAcc pa{};
 #endif
-        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t PH_PASS);
+        const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t, nullptr PH_PASS);
         if (valid) wb.hitq[e] = make_int2(rec, __builtin_bit_cast(int, t));
     }
     if (COUNT) flush_counters(c, cnt_out);
@@ -720,7 +752,8 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
         pa.v[PH_COUNT][0] = t1;  // phase 1's start, for bf_closest
     }
 #endif
-    const int rec = bf_closest<FAST_RCP, COUNT>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t PH_PASS);
+    // GEN: every batch is a camera batch (the GEN launch reads no queue: genk >= 0 throughout)
+    const int rec = bf_closest<FAST_RCP, COUNT, GEN>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t, wb.camtab PH_PASS);
 #if PT_PHASE_STATS
     uint64_t t3 = ph_now();
     pa.v[PH_REPLAY][0] += t3 - pa.v[PH_COUNT][0];
@@ -1111,6 +1144,12 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     const int sparse = std::max(0, std::min(ws.trace_sparse, 1 << 20));
     // option bf_slots < kBfSlots: tests of the recompute path
     const int bf_slots = ws.bf_slots >= 0 ? std::min(kBfSlots, ws.bf_slots) : kBfSlots;
+    if constexpr (TRAV >= 400) {  // the camera batches' table (k_wf_camtab), before every part's GEN launch
+        if (ws.fuse_gen) {
+            if (sc.n_tris - sc.mb_base > 64) return hipErrorInvalidValue;  // mailbox scenes: <= 64 entries
+            hipLaunchKernelGGL(k_wf_camtab, dim3(1), dim3(64), 0, stream, sc, fp, wb.camtab);
+        }
+    }
     for (uint32_t fb = 0; fb < nframes; fb += F) {
         const uint32_t Fb = std::min(F, nframes - fb);
         // frames of the batch dealt to the parts in contiguous runs (part h: frames fb + f0[h] ..)
