@@ -73,7 +73,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"lds", OPT_BOOL, nullptr},          {"fastrcp", OPT_BOOL, nullptr},     {"dual", OPT_BOOL, nullptr},
     {"fuse", OPT_BOOL, nullptr},         {"fuse_gen", OPT_BOOL, nullptr},    {"bf", OPT_BOOL, nullptr},
     {"mailbox", OPT_BOOL, nullptr},      {"bf_stackless", OPT_BOOL, nullptr}, {"trace_sparse", OPT_INT, nullptr},
-    {"region_perm", OPT_BOOL, nullptr},  {"persist", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
+    {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"node_steps", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"leaf_pre", OPT_INT, nullptr},      {"leaf_blocks", OPT_INT, nullptr},  {"leaf_pairs", OPT_INT, nullptr},
@@ -897,8 +897,6 @@ constexpr int kTraceSparseDefault = 4;
 // 4096^2, 512 neighbouring pixels of one row (an eighth of it) on one CU; permuted, batches far
 // apart: 4096^2 2475 -> 2679 Msamples/s, 1024^2 and Mirror unchanged (profiles/r03h_ab_region_perm.txt)
 constexpr int kRegionPermDefault = 1;
-// the fused kernel's whole path chain in one launch per batch (option persist; pt_wavefront.hip k_wf_persist)
-constexpr int kPersistDefault = 0;
 
 LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView& view) {
     LaunchOpts lo;
@@ -920,7 +918,6 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.sort = (int)o.num("sort", lo.sort);  // 1 / 8: direction octant; 64: + origin octant; 512: + 4^3 origin cells
     lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
     lo.region_perm = o.flag("region_perm", kRegionPermDefault);
-    lo.persist = o.flag("persist", kPersistDefault);
     lo.trace_ring = (int)o.num("trace_ring", 0);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);

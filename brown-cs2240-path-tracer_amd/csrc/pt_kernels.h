@@ -74,7 +74,6 @@ struct LaunchOpts {
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
     int leaf_blocks = 0;   // k_wf_leafpass grid (A/B): 0 = occupancy-derived
     int leaf_pairs = 5;    // k_wf_leafpass walks chunked leaves by (ray, chunk) pairs (option leaf_pairs; | 4: leaf_refine)
-    int persist = -1;      // fused kernel: the batch's whole path chain in one launch (k_wf_persist): -1 default
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -127,9 +126,8 @@ struct WfBuffers {
 };
 constexpr uint32_t kRegions = 512;
 // queue slack (entries per part = 64 * this): regions of R <= kRegions hold ceil(batches / R)
-// 64-entry batches each, and so do k_wf_persist's one region per wave (R = the grid's waves, 8,192
-// on MI355X: 128 entries of slack per region)
-constexpr uint32_t kQueueSlackRegions = 16384;
+// 64-entry batches each
+constexpr uint32_t kQueueSlackRegions = 4096;
 constexpr size_t kWfBytesPerPath = 64 + 64 + 40 + 8 + 12;
 
 // Dual-stream wavefront: two streams owned by the scene, created back to back so that HIP's
@@ -151,7 +149,6 @@ struct WfStreams {
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
     int leaf_blocks = 0;   // LaunchOpts::leaf_blocks
     int leaf_pairs = 5;    // LaunchOpts::leaf_pairs
-    bool persist = false;  // LaunchOpts::persist
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

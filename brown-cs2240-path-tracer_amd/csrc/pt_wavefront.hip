@@ -694,8 +694,7 @@ struct GenArgs {
 };
 // genk (GEN instances; wave-uniform): >= 0 makes this batch camera batch genk of the region
 // instead of queue batch b (the first launch); -1 reads the queue.
-// PRIV (k_wf_persist): `append` is the wave's own count, called by every lane (wave-uniform).
-template <bool EXT, bool FAST_RCP, bool COUNT, bool GEN = false, bool PRIV = false, class Append>
+template <bool EXT, bool FAST_RCP, bool COUNT, bool GEN = false, class Append>
 __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gtris, const FrameParams& fp,
                                               const WfBuffers& wb, size_t rbase, uint32_t b, uint32_t count,
                                               const BfLds& l, int nslots, Counters& c, Append append,
@@ -799,12 +798,8 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
     const uint64_t keep = __ballot(more);
     if (keep) {  // wave-uniform
         uint32_t base = 0;
-        if constexpr (PRIV) {
-            base = append((uint32_t)__popcll(keep));
-        } else {
-            if (lane == 0) base = append((uint32_t)__popcll(keep));
-            base = __shfl(base, 0, 64);
-        }
+        if (lane == 0) base = append((uint32_t)__popcll(keep));
+        base = __shfl(base, 0, 64);
         if (more) {
             PH_ITER(PH_APPEND);
             const uint32_t j = (uint32_t)rbase + base + rank_below(keep);
@@ -876,64 +871,6 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
             for (int f = 0; f < 3; ++f) atomicAdd(&g_phase_stats[EXT ? 1 : 0][ph][f], (unsigned long long)pa.v[ph][f]);
     }
 #endif
-}
-
-// The whole path chain of a batch in ONE launch (option persist): one region per wave (R = the
-// grid's waves), and each wave runs its region through every bounce itself — its camera batches
-// (GEN), then its shadow batches, its extension batches, ... — appending to its own region of the
-// other queue at offsets it counts itself (no atomics: the count stays in the wave), until its
-// region is empty.  A region's output never exceeds its input, so the region of a queue holds it
-// throughout.  Between two half-bounces the wave's own queue writes are made visible to its own
-// reads by a fence (other lanes of the wave read them).  Every path runs the same bf_step_batch
-// as in the per-bounce launches, so the same bits; what goes is the 2 (depth + 1) launches per
-// batch and their tails (each launch ends with its slowest region; here a wave ends with its own).
-template <bool LDS, bool FAST_RCP, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_wf_persist(
-    SceneView sc, FrameParams fp, WfBuffers wb, int iters, Counters* cnt_out, int nslots, uint32_t frame0, uint32_t stride,
-    uint32_t fbase, uint32_t P, bool raw_salt) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const BfLds l = bf_lds(smem, sc);
-    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-    const uint32_t R = wb.nreg;  // = the grid's waves (host)
-    const uint32_t nbat = (P + 63) / 64;
-    const uint32_t tg = (uint32_t)((uint64_t)w * wb.rq % R);  // this wave's camera batches: tg, tg + R, ...
-    const uint32_t ncam = tg < nbat ? (nbat - tg + R - 1) / R : 0u;
-    const size_t rbase = (size_t)w * wb.rstride;
-    if (w == 0 && lane_id() == 0) { wb.ctl[WF_COUNT0] = P; wb.ctl[WF_COUNT1] = 0; }
-    const Tri* gtris = sc.tris;
-    if (LDS) stage_scene_lds(sc, l.scene);
-    const GenArgs ga{frame0, stride, fbase, R, tg, P, raw_salt};
-    Counters c = {};
-#if PT_PHASE_STATS
-    PhaseAcc pa{};  // (not flushed: the phase tables come from the per-bounce launches)
-#endif
-    uint32_t count = 0;
-    for (int it = 0; it < iters; ++it) {
-        uint32_t nout = 0;
-        auto append = [&](uint32_t n) { const uint32_t o = nout; nout += n; return o; };
-        if (it == 0) {
-            for (uint32_t b = 0; b < ncam; ++b)
-                bf_step_batch<true, FAST_RCP, COUNT, true, true>(sc, gtris, fp, wb, rbase, b, 0u, l, nslots, c, append, ga,
-                                                                 (int64_t)b PH_PASS);
-        } else {
-            const uint32_t nb = (count + 63) / 64;
-            for (uint32_t b = 0; b < nb; ++b) {
-                if (it & 1)
-                    bf_step_batch<false, FAST_RCP, COUNT, false, true>(sc, gtris, fp, wb, rbase, b, count, l, nslots, c,
-                                                                       append, ga, (int64_t)-1 PH_PASS);
-                else
-                    bf_step_batch<true, FAST_RCP, COUNT, false, true>(sc, gtris, fp, wb, rbase, b, count, l, nslots, c,
-                                                                      append, ga, (int64_t)-1 PH_PASS);
-            }
-        }
-        count = __builtin_amdgcn_readfirstlane(nout);
-        if (count == 0) break;  // wave-uniform: the region's paths have all ended
-        // this half-bounce's queue writes, before the next one reads them: the readers are lanes of
-        // the same wave, so workgroup scope (an agent-scope fence writes back the L2 at every call)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    if (COUNT) flush_counters(c, cnt_out);
 }
 
 // Shade blocks are 1024 threads so that compaction takes one atomicAdd per 1024 entries: all
@@ -1175,10 +1112,6 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     // shade kernels, a VALU-bound trace runs beside an HBM-bound shade)
     int np = ws.aux[0] != nullptr ? ws.nparts : 1;
     while (np > 1 && (nframes < (uint32_t)np || wb.capacity / np < npix)) np /= 2;
-    // option persist (the fused kernel): the whole batch in one launch of k_wf_persist, one part
-    bool persist = false;
-    if constexpr (TRAV >= 400) persist = ws.persist && ws.fuse_gen;
-    if (persist) np = 1;
     const uint32_t F = np * std::max<uint32_t>(1, std::min<uint32_t>((nframes + np - 1) / np, (uint32_t)(wb.capacity / np / npix)));
     // k_wf_trace's instance: the 256-entry hit ring when its extra 8 KB per block cost no block per
     // CU (option trace_ring: 128 / 256 forces one)
@@ -1211,19 +1144,6 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
     const int sparse = std::max(0, std::min(ws.trace_sparse, 1 << 20));
     // option bf_slots < kBfSlots: tests of the recompute path
     const int bf_slots = ws.bf_slots >= 0 ? std::min(kBfSlots, ws.bf_slots) : kBfSlots;
-    // k_wf_persist: one region per wave, the grid its own occupancy (a block that waits for another
-    // to finish doubles the launch); each region must hold its camera batches (queue slack)
-    if constexpr (TRAV >= 400) {
-        if (persist) {
-            tblocks = occupancy_blocks((const void*)k_wf_persist<LDS, ((TRAV / 10) & 1) != 0, COUNT>, lds);
-            if (ws.trace_blocks > 0) tblocks = std::min(tblocks, ws.trace_blocks);
-        }
-    }
-    const uint32_t pwaves = (uint32_t)tblocks * (kTraceBlock / 64);
-    if (persist) {
-        const uint64_t nbat = ((uint64_t)F * npix + 63) / 64;
-        if ((nbat + pwaves - 1) / pwaves * 64 > wb.qcap / pwaves / 64 * 64) persist = false;  // (then one part)
-    }
     if constexpr (TRAV >= 400) {  // the camera batches' table (k_wf_camtab), before every part's GEN launch
         if (ws.fuse_gen) {
             if (sc.n_tris - sc.mb_base > 64) return hipErrorInvalidValue;  // mailbox scenes: <= 64 entries
@@ -1247,7 +1167,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
             ++nh;
         }
         if constexpr (TRAV >= 400) {  // region-partitioned queues (k_wf_step_bf)
-            const uint32_t R = persist ? pwaves : std::min<uint32_t>(kRegions, pwaves);
+            const uint32_t R = std::min<uint32_t>(kRegions, (uint32_t)tblocks * (kTraceBlock / 64));
             // region_perm: region r takes camera batches r q mod R (q ~ 0.618 R, coprime with R), so
             // the 8 waves of a block (8 neighbouring regions) work on batches far apart in the image
             uint32_t q = 1, qi = 1;
@@ -1256,7 +1176,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 q = std::max<uint32_t>(1, (uint32_t)(R * 0.6180339887498949));
                 while (gcd(q, R) != 1) ++q;
                 qi = 1;
-                while ((uint64_t)q * qi % R != 1) ++qi;  // R <= 512, or the grid's waves (persist)
+                while ((uint64_t)q * qi % R != 1) ++qi;  // R <= 512
             }
             for (int h = 0; h < nh; ++h) {
                 pv[h].w.nreg = R;
@@ -1272,17 +1192,6 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
         // the fused kernel's first launch makes the camera paths itself (GEN); it appends into
         // count slot 1, zeroed here (k_wf_generate zeroes it otherwise)
         const bool fgen = TRAV >= 400 && ws.fuse_gen;
-        if constexpr (TRAV >= 400) {
-            if (persist) {  // the whole chain in one launch (nh == 1)
-                constexpr bool rcp = ((TRAV / 10) & 1) != 0;
-                PT_LAUNCH(KID_WF_STEP, pv[0].st, (k_wf_persist<LDS, rcp, COUNT>), dim3(tblocks), dim3(kTraceBlock), lds,
-                          pv[0].st, sc, fp, pv[0].w, iters, cnt, bf_slots, frame0, stride, pv[0].fbase, pv[0].P, !accum);
-                if (fb == 0) HIP_RETURN_IF(hipGetLastError());
-                PT_LAUNCH(KID_WF_ACCUM, stream, k_wf_accum, dim3((npix + 255) / 256), dim3(256), 0, stream, wb.rad, out, npix,
-                          Fb, accum);
-                continue;
-            }
-        }
         for (int h = 0; h < nh; ++h) {
             if (fgen)
                 HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rcnt + kRegions, 0, kRegions * sizeof(uint32_t), pv[h].st));
@@ -1371,7 +1280,6 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.trace_blocks = lo.trace_blocks;
     ws.trace_sparse = std::max(0, lo.trace_sparse);
     ws.region_perm = lo.region_perm > 0 ? 1 : 0;
-    ws.persist = lo.persist > 0;
     ws.trace_ring = lo.trace_ring;
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;

@@ -151,16 +151,6 @@ KERNELS = {
     "wavefront_nodesteps8_nopool": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "8", "PT_MAILBOX": "0",
                                     "PT_LEAF_POOL": "0"},
     "mega_nodesteps4": {"PT_KERNEL": "mega", "PT_NODE_STEPS": "4"},
-    # the fused kernel's whole path chain in one launch per batch (option persist: one region per
-    # wave, k_wf_persist): the default grid, one block (4 regions), without the region permutation,
-    # and with persist asked for where it cannot run (camera paths from k_wf_generate)
-    "wavefront_persist": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1"},
-    "wavefront_persist_1block": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1", "PT_WF_TRACE_BLOCKS": "1"},
-    "wavefront_persist_noperm_3blocks": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1", "PT_REGION_PERM": "0",
-                                         "PT_WF_TRACE_BLOCKS": "3"},
-    "wavefront_persist_nofusegen": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1", "PT_FUSE_GEN": "0"},
-    "wavefront_nopersist": {"PT_KERNEL": "wavefront", "PT_PERSIST": "0"},
-    "wavefront_persist_smallbatch": {"PT_KERNEL": "wavefront", "PT_PERSIST": "1", "PT_WF_PATHS": "8192"},
     "wavefront_nodesteps3_big8_1block": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "3", "PT_MAILBOX": "0",
                                          "PT_BIG_LEAF": "8", "PT_WF_TRACE_BLOCKS": "1"},
     "mega_nodesteps2_lean4": {"PT_KERNEL": "mega", "PT_NODE_STEPS": "2", "PT_TRAV": "lean4"},
@@ -170,7 +160,7 @@ KERNELS = {
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
-            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL", "PT_PERSIST",
+            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
             "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS",
             "PT_LEAF_REFINE", "PT_LEAF_SKIP", "PT_NODE_STEPS")
 
@@ -392,21 +382,12 @@ def test_profile_records_every_launch(packed, ptopts):
     assert wf["k_wf_step"]["launches"] == 2 * 2 * (depth + 1)
     assert wf["k_wf_generate"]["launches"] == 2 and wf["k_wf_accum"]["launches"] == 1
     ptopts.set("PT_FUSE_GEN", "1")  # the first step launch makes the camera paths
-    ptopts.set("PT_PERSIST", "0")
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
         s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
         wfg = s.profile_read()
     assert set(wfg) == {"k_wf_step", "k_wf_accum"}
     assert wfg["k_wf_step"]["launches"] == 2 * 2 * (depth + 1) and wfg["k_wf_accum"]["launches"] == 1
-    ptopts.set("PT_PERSIST", "1")  # the whole path chain in one launch (k_wf_persist)
-    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
-        s.profile_enable(True)
-        s.render(meta, 0, 4, 1, depth, pt_amd.MODE_WAVEFRONT)
-        wfp = s.profile_read()
-    assert set(wfp) == {"k_wf_step", "k_wf_accum"}
-    assert wfp["k_wf_step"]["launches"] == 1 and wfp["k_wf_accum"]["launches"] == 1
-    ptopts.set("PT_PERSIST", "0")
     ptopts.set("PT_FUSE", "0")  # separate trace and shade kernels
     with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
         s.profile_enable(True)
@@ -415,7 +396,7 @@ def test_profile_records_every_launch(packed, ptopts):
     assert set(wf2) == {"k_wf_generate", "k_wf_trace", "k_wf_shade_ext", "k_wf_shade_shadow", "k_wf_accum"}
     assert wf2["k_wf_trace"]["launches"] == 2 * 2 * (depth + 1)
     assert wf2["k_wf_shade_ext"]["launches"] == wf2["k_wf_shade_shadow"]["launches"] == 2 * (depth + 1)
-    for v in list(mega.values()) + list(wf.values()) + list(wfg.values()) + list(wfp.values()) + list(wf2.values()):
+    for v in list(mega.values()) + list(wf.values()) + list(wfg.values()) + list(wf2.values()):
         assert 0.0 < v["min_ms"] <= v["avg_ms"] <= v["max_ms"] and v["total_ms"] > 0.0
 
 
