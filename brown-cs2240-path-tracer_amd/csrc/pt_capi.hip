@@ -73,7 +73,7 @@ constexpr OptSpec kOptSpecs[] = {
     {"lds", OPT_BOOL, nullptr},          {"fastrcp", OPT_BOOL, nullptr},     {"dual", OPT_BOOL, nullptr},
     {"fuse", OPT_BOOL, nullptr},         {"fuse_gen", OPT_BOOL, nullptr},    {"bf", OPT_BOOL, nullptr},
     {"mailbox", OPT_BOOL, nullptr},      {"bf_stackless", OPT_BOOL, nullptr}, {"trace_sparse", OPT_INT, nullptr},
-    {"region_perm", OPT_BOOL, nullptr},  {"trace_ring", OPT_INT, nullptr},
+    {"region_perm", OPT_BOOL, nullptr},  {"regen", OPT_INT, nullptr},  {"trace_ring", OPT_INT, nullptr},
     {"parts", OPT_INT, nullptr},         {"sort", OPT_INT, nullptr},
     {"node_bias", OPT_INT, nullptr},     {"node_steps", OPT_INT, nullptr},     {"big_leaf", OPT_INT, nullptr},     {"bf_slots", OPT_INT, nullptr},
     {"leaf_pre", OPT_INT, nullptr},      {"leaf_blocks", OPT_INT, nullptr},  {"leaf_pairs", OPT_INT, nullptr},
@@ -918,6 +918,7 @@ LaunchOpts launch_opts(const Opts& o, int mode, uint64_t paths, const SceneView&
     lo.sort = (int)o.num("sort", lo.sort);  // 1 / 8: direction octant; 64: + origin octant; 512: + 4^3 origin cells
     lo.trace_sparse = (int)o.num("trace_sparse", kTraceSparseDefault);
     lo.region_perm = o.flag("region_perm", kRegionPermDefault);
+    lo.regen = (int)std::max(0L, std::min(1L << 20, o.num("regen", 0)));
     lo.trace_ring = (int)o.num("trace_ring", 0);
     lo.trace_blocks = (int)o.num("wf_trace_blocks", 0);
     lo.watchdog = (uint32_t)o.num("trace_watchdog", 0);

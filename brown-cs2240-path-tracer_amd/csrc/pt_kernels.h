@@ -74,6 +74,7 @@ struct LaunchOpts {
     uint32_t watchdog = 0; // k_wf_trace iterations before a wave gives up (tests of the failure report): 0 default
     int leaf_blocks = 0;   // k_wf_leafpass grid (A/B): 0 = occupancy-derived
     int leaf_pairs = 5;    // k_wf_leafpass walks chunked leaves by (ray, chunk) pairs (option leaf_pairs; | 4: leaf_refine)
+    int regen = 0;         // fused kernel: camera batches per region admitted by every extension launch (0: all at once)
 };
 
 bool scene_fits_lds(const SceneView& sc);
@@ -149,6 +150,7 @@ struct WfStreams {
     uint32_t watchdog = 0; // k_wf_trace iteration limit (0: kTraceWatchdog)
     int leaf_blocks = 0;   // LaunchOpts::leaf_blocks
     int leaf_pairs = 5;    // LaunchOpts::leaf_pairs
+    int regen = 0;         // LaunchOpts::regen
 };
 hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& sc, const FrameParams& fp, const WfBuffers& wb,
                             uint32_t frame0, uint32_t nframes, uint32_t stride, bool accum, bool count, float* out,

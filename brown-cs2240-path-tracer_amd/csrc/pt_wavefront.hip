@@ -694,7 +694,8 @@ struct GenArgs {
 };
 // genk (GEN instances; wave-uniform): >= 0 makes this batch camera batch genk of the region
 // instead of queue batch b (the first launch); -1 reads the queue.
-template <bool EXT, bool FAST_RCP, bool COUNT, bool GEN = false, class Append>
+// CAM: the batch's rays are camera rays (a fresh batch of the first launch: bf_closest's table)
+template <bool EXT, bool FAST_RCP, bool COUNT, bool GEN = false, bool CAM = GEN, class Append>
 __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gtris, const FrameParams& fp,
                                               const WfBuffers& wb, size_t rbase, uint32_t b, uint32_t count,
                                               const BfLds& l, int nslots, Counters& c, Append append,
@@ -752,8 +753,8 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
         pa.v[PH_COUNT][0] = t1;  // phase 1's start, for bf_closest
     }
 #endif
-    // GEN: every batch is a camera batch (the GEN launch reads no queue: genk >= 0 throughout)
-    const int rec = bf_closest<FAST_RCP, COUNT, GEN>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t, wb.camtab PH_PASS);
+    // CAM: a camera batch (the first launch reads no queue: genk >= 0 throughout)
+    const int rec = bf_closest<FAST_RCP, COUNT, CAM>(sc, gtris, r, valid, l.slot, nslots, l.stack, c, t, wb.camtab PH_PASS);
 #if PT_PHASE_STATS
     uint64_t t3 = ph_now();
     pa.v[PH_REPLAY][0] += t3 - pa.v[PH_COUNT][0];
@@ -825,10 +826,15 @@ __device__ __forceinline__ void bf_step_batch(const SceneView& sc, const Tri* gt
 // at 64 it keeps 8 waves/SIMD with no VGPR spills (a few SGPR spills to VGPR lanes): +7 %
 // GEN: the first launch makes the camera paths itself (bf_step_batch GEN; replaces
 // k_wf_generate): region counts in closed form, the output counts zeroed by the host.
-template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT, bool GEN = false>
+// GEN 2 (option regen = q): streaming regeneration — every extension launch j = it / 2 also admits
+// the region's camera batches j q .. (j + 1) q - 1 behind its queued survivors, so the launches stay
+// full until the camera batches run out (the host launches 2 (ceil(max camera batches / q) +
+// max_depth) iterations).  Those launches mix queued and camera batches: no camera table.
+template <bool EXT, bool LDS, bool FAST_RCP, bool COUNT, int GEN = 0>
 __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_wf_step_bf(SceneView sc, FrameParams fp, WfBuffers wb, int it,
                                                            Counters* cnt_out, int nslots, uint32_t frame0,
-                                                           uint32_t stride, uint32_t fbase, uint32_t P, bool raw_salt) {
+                                                           uint32_t stride, uint32_t fbase, uint32_t P, bool raw_salt,
+                                                           uint32_t q) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const BfLds l = bf_lds(smem, sc);
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
@@ -839,13 +845,19 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     const uint32_t nbat = (P + 63) / 64;
     const uint32_t tg = (uint32_t)((uint64_t)rg * wb.rq % R);  // region rg's camera batches: tg, tg + R, ...
     const uint32_t ncam = tg < nbat ? (nbat - tg + R - 1) / R : 0u;
-    uint32_t count, nqb, nnew = 0;
-    if constexpr (GEN) {  // k_wf_generate's closed-form count of region rg
+    uint32_t count, nqb, nnew = 0, k0 = 0;
+    if constexpr (GEN == 1) {  // the first launch: every camera batch of region rg
         const uint32_t last = tg + (ncam - 1) * R;
         count = ncam == 0 ? 0u : ncam * 64 - ((last == nbat - 1 && (P & 63)) ? 64 - (P & 63) : 0u);
         if (w == 0 && lane_id() == 0) { wb.ctl[WF_COUNT0] = P; wb.ctl[WF_COUNT1] = 0; }
         nqb = 0;
         nnew = ncam;
+    } else if constexpr (GEN == 2) {  // queued survivors (none in the first launch), then admissions
+        count = it == 0 ? 0u : wb.rcnt[(it % 3) * kRegions + rg];
+        nqb = (count + 63) / 64;
+        k0 = (uint32_t)(it / 2) * q;
+        nnew = ncam > k0 ? min(q, ncam - k0) : 0u;
+        if (it == 0 && w == 0 && lane_id() == 0) { wb.ctl[WF_COUNT0] = P; wb.ctl[WF_COUNT1] = 0; }
     } else {
         count = wb.rcnt[(it % 3) * kRegions + rg];
         nqb = (count + 63) / 64;
@@ -860,9 +872,9 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(8, 
     PhaseAcc pa{};
 #endif
     for (uint32_t b = g; b < nb; b += G)  // this region's batches, interleaved over its waves
-        bf_step_batch<EXT, FAST_RCP, COUNT, GEN>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l, nslots, c,
-                                                 [&](uint32_t n) { return atomicAdd(out_count, n); }, ga,
-                                                 b < nqb ? (int64_t)-1 : (int64_t)(b - nqb) PH_PASS);
+        bf_step_batch<EXT, FAST_RCP, COUNT, GEN != 0, GEN == 1>(sc, gtris, fp, wb, (size_t)rg * wb.rstride, b, count, l,
+                                                                nslots, c, [&](uint32_t n) { return atomicAdd(out_count, n); },
+                                                                ga, b < nqb ? (int64_t)-1 : (int64_t)(k0 + b - nqb) PH_PASS);
     if (COUNT) flush_counters(c, cnt_out);
 #if PT_PHASE_STATS
     if (!COUNT && lane_id() == 0) {
@@ -1192,6 +1204,21 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
         // the fused kernel's first launch makes the camera paths itself (GEN); it appends into
         // count slot 1, zeroed here (k_wf_generate zeroes it otherwise)
         const bool fgen = TRAV >= 400 && ws.fuse_gen;
+        // option regen (fused kernel, camera paths made in the kernel): q camera batches per region
+        // admitted by each extension launch; regen_cam = the most camera batches of any region
+        uint32_t regen_q = 0, regen_cam = 0;
+        int iters_b = iters;
+        if (TRAV >= 400 && fgen && ws.regen > 0) {
+            for (int h = 0; h < nh; ++h) {
+                const uint32_t nbat = (pv[h].P + 63) / 64;
+                regen_cam = std::max(regen_cam, (nbat + pv[h].w.nreg - 1) / pv[h].w.nreg);
+            }
+            regen_q = (uint32_t)ws.regen;
+            if (regen_q < regen_cam)  // J admitting launches, the last admission's paths need max_depth + 1 more
+                iters_b = 2 * ((int)((regen_cam + regen_q - 1) / regen_q) + fp.max_depth);
+            else
+                regen_q = 0;  // one launch admits them all: the plain first launch
+        }
         for (int h = 0; h < nh; ++h) {
             if (fgen)
                 HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rcnt + kRegions, 0, kRegions * sizeof(uint32_t), pv[h].st));
@@ -1209,10 +1236,11 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
             if constexpr (TRAV >= 400) {  // trace + shade in one launch
                 constexpr bool rcp = ((TRAV / 10) & 1) != 0;
 #define PT_STEP(E, G) PT_LAUNCH(KID_WF_STEP, st, (k_wf_step_bf<E, LDS, rcp, COUNT, G>), dim3(tblocks), dim3(kTraceBlock), \
-                                lds, st, sc, fp, w, it, cnt, bf_slots, frame0, stride, pv[h].fbase, pv[h].P, !accum)
-                if (fgen && it == 0) PT_STEP(true, true);
-                else if ((it & 1) == 0) PT_STEP(true, false);
-                else PT_STEP(false, false);
+                                lds, st, sc, fp, w, it, cnt, bf_slots, frame0, stride, pv[h].fbase, pv[h].P, !accum, regen_q)
+                if (regen_q > 0 && (it & 1) == 0 && (uint32_t)(it / 2) * regen_q < regen_cam) PT_STEP(true, 2);
+                else if (fgen && it == 0) PT_STEP(true, 1);
+                else if ((it & 1) == 0) PT_STEP(true, 0);
+                else PT_STEP(false, 0);
 #undef PT_STEP
                 return hipSuccess;
             } else if constexpr (TRAV >= 300) {
@@ -1248,7 +1276,7 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                           fp, w, cnt, ws.sort_bins);
             return hipSuccess;
         };
-        for (int it = 0; it < iters; ++it) {
+        for (int it = 0; it < iters_b; ++it) {
             for (int h = 0; h < nh; ++h) HIP_RETURN_IF(step(h, it));
             // a launch that cannot run (e.g. a configuration error) fails here, after the first
             // iteration, instead of leaving the later launches to read counts it never wrote
@@ -1280,6 +1308,7 @@ hipError_t launch_wavefront(const LaunchOpts& lo, const SceneView& scene, const 
     ws.trace_blocks = lo.trace_blocks;
     ws.trace_sparse = std::max(0, lo.trace_sparse);
     ws.region_perm = lo.region_perm > 0 ? 1 : 0;
+    ws.regen = std::max(0, lo.regen);
     ws.trace_ring = lo.trace_ring;
     ws.bf_slots = lo.bf_slots;
     ws.watchdog = lo.watchdog;

@@ -95,10 +95,14 @@ def test_layout_options():
     experiments removed in round 4 are unknown names."""
     pt_amd.reset_options()
     try:
-        for name in ("packet", "persist", "regen", "regen_bf", "cull", "tiles", "scatter", "batch_pipe",
+        for name in ("packet", "persist", "regen_bf", "cull", "tiles", "scatter", "batch_pipe",
                      "trace_dyn", "stagger", "pipe", "ifif", "stack16"):
             with pytest.raises(pt_amd.PtError):
                 pt_amd.set_option(name, "1")
+        pt_amd.set_option("regen", 64)  # round 6: the fused kernel's streaming regeneration (an integer)
+        assert pt_amd.get_option("regen") == "64"
+        with pytest.raises(pt_amd.PtError):
+            pt_amd.set_option("regen", "x")
         for name in ("region_perm",):
             pt_amd.set_option(name, 0)
             assert pt_amd.get_option(name) == "0"

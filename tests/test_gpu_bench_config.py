@@ -27,7 +27,7 @@ pytestmark = pytest.mark.gpu
 
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
-            "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_BF_STACKLESS", "PT_SORT", "PT_LEAF_POOL", "PT_POOL_RUN")
+            "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_BF_STACKLESS", "PT_SORT", "PT_LEAF_POOL", "PT_POOL_RUN", "PT_REGEN")
 ORACLE_THREADS = 16  # the GPU box's CPU share
 
 

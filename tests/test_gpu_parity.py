@@ -151,6 +151,14 @@ KERNELS = {
     "wavefront_nodesteps8_nopool": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "8", "PT_MAILBOX": "0",
                                     "PT_LEAF_POOL": "0"},
     "mega_nodesteps4": {"PT_KERNEL": "mega", "PT_NODE_STEPS": "4"},
+    # streaming regeneration in the fused kernel (option regen = camera batches per region admitted by
+    # each extension launch; small grids so that the regions hold many camera batches)
+    "wavefront_regen8_1block": {"PT_KERNEL": "wavefront", "PT_REGEN": "8", "PT_WF_TRACE_BLOCKS": "1"},
+    "wavefront_regen3_2blocks_noperm": {"PT_KERNEL": "wavefront", "PT_REGEN": "3", "PT_WF_TRACE_BLOCKS": "2",
+                                        "PT_REGION_PERM": "0"},
+    "wavefront_regen1_1block_1part": {"PT_KERNEL": "wavefront", "PT_REGEN": "1", "PT_WF_TRACE_BLOCKS": "1",
+                                      "PT_PARTS": "1"},
+    "wavefront_regen64": {"PT_KERNEL": "wavefront", "PT_REGEN": "64"},
     "wavefront_nodesteps3_big8_1block": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "3", "PT_MAILBOX": "0",
                                          "PT_BIG_LEAF": "8", "PT_WF_TRACE_BLOCKS": "1"},
     "mega_nodesteps2_lean4": {"PT_KERNEL": "mega", "PT_NODE_STEPS": "2", "PT_TRAV": "lean4"},
@@ -160,7 +168,7 @@ KERNELS = {
 ENV_KEYS = ("PT_KERNEL", "PT_TRAV", "PT_LDS", "PT_FASTRCP", "PT_WF_TRACE_BLOCKS", "PT_NODE_BIAS",
             "PT_DUAL", "PT_MAILBOX", "PT_MB_UID_ORDER", "PT_BF", "PT_BF_SLOTS", "PT_FUSE", "PT_PARTS",
             "PT_FUSE_GEN", "PT_WF_PATHS", "PT_BIG_LEAF", "PT_TRACE_WATCHDOG", "PT_REDUCE", "PT_BF_STACKLESS",
-            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL",
+            "PT_SORT", "PT_TRACE_SPARSE", "PT_LEAF_BVH", "PT_LEAF_WALK", "PT_REGION_PERM", "PT_TRACE_RING", "PT_LEAF_POOL", "PT_REGEN",
             "PT_POOL_RUN", "PT_LEAF_PRE", "PT_LEAF_BLOCKS", "PT_LEAF_PAIRS",
             "PT_LEAF_REFINE", "PT_LEAF_SKIP", "PT_NODE_STEPS")
 
