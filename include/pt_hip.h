@@ -148,9 +148,12 @@ int pt_set_hw_queues(int n);
  *   "kernel"        auto | mega | wavefront | literal    pipeline (auto = PT_MODE_* and the scene)
  *   "trav"          nested|flat1|pred|lean|lean2|lean4|lean8|lean16|lean32   traversal flavour
  *   "lds" "fastrcp" "dual" "fuse" "fuse_gen" "bf" "mailbox" "bf_stackless" "region_perm"
- *   "leaf_walk" "leaf_pool"                                                 0 | 1 switches
+ *   "leaf_walk" "leaf_pool" "leaf_skip"                                     0 | 1 switches
  *   "parts" "sort" "node_bias" "big_leaf" "bf_slots" "wf_paths" "wf_trace_blocks" "trace_sparse"
- *   "trace_ring" "trace_watchdog"                                           integers
+ *   "trace_ring" "trace_watchdog" "node_steps" "regen"                      integers
+ *                                       (node_steps 1..8: node steps per node turn of the lean
+ *                                        traversal; regen: camera batches per region admitted by
+ *                                        every extension launch of the fused kernel, 0 = off)
  *   "mb_uid_order"  forward | reverse   (read by pt_scene_create: uid numbering of mailbox scenes)
  *   "leaf_bvh"      integer             (read by pt_scene_create: leaves with a leaf BVH, >= this many entries)
  *   "pool_run"      2 | 4               (entries per run of the pooled leaf turns; default per scene)
