@@ -413,6 +413,8 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no per-launch HIP events")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option (pt_set_option) for A/B and profiling runs; repeatable")
+    ap.add_argument("--readback", choices=["pt", "torch"], default="pt",
+                    help="the step's accumulator-to-host copy: pt_readback_async (16 blocks) or torch's copy_")
     ap.add_argument("--share-of", type=int, default=0, metavar="N",
                     help="one GPU renders exactly rank --share-rank's frames of an N-rank run (frames r, r+N, ...; no "
                          "reduce): the per-rank share whose time bounds N-GPU strong scaling (DESIGN.md section 7)")
@@ -513,7 +515,10 @@ def main():
         if hosts[k] is not None:
             with torch.cuda.stream(copy_stream):
                 copy_stream.wait_event(done)
-                hosts[k].copy_(a, non_blocking=True)
+                if args.readback == "pt":  # pt_readback_async: a 16-block copy kernel
+                    scene.readback_async(a.data_ptr(), a.numel(), hosts[k].data_ptr(), copy_stream.cuda_stream)
+                else:  # the runtime's copy (a blit kernel of ~512 blocks on this stack)
+                    hosts[k].copy_(a, non_blocking=True)
                 done = torch.cuda.Event()
                 done.record(copy_stream)
         slot_free[k] = done
@@ -648,6 +653,8 @@ def main():
                        "timed_to": "accumulator on the host (rank 0: pinned device-to-host copy after the "
                                    "reduce, every step's inside the timed region; step k's copy overlaps step "
                                    "k + 1's render, two accumulators)",
+                       "readback": ("pt_readback_async (16-block copy kernel)" if args.readback == "pt"
+                                    else "torch copy_ (runtime blit)"),
                        "ranks": ranks_seen, "backend": backend if world > 1 else None,
                        "options": dict(kv.partition("=")[::2] for kv in args.opt) or None,
                        "scene_triangles": int((int(tri[4]) - int(tri[3])) // 4), "bvh_floats": int(bvh.size),

@@ -1313,6 +1313,21 @@ int pt_tonemap_async(pt_scene* s, const float* d_accum, size_t npix, uint32_t sa
     return PT_OK;
 }
 
+int pt_readback_async(pt_scene* s, const float* d_src, size_t n, float* h_dst, void* stream) {
+    if (!s) return fail(PT_ERR_INVALID, "null scene");
+    if (n == 0) return PT_OK;
+    if (!d_src || !h_dst) return fail(PT_ERR_INVALID, "null argument");
+    if (((uintptr_t)d_src | (uintptr_t)h_dst) & 15u) return fail(PT_ERR_INVALID, "buffers must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(s->device));
+    void* hd = nullptr;  // pinned host memory: its address in the device's view
+    if (hipHostGetDevicePointer(&hd, h_dst, 0) != hipSuccess || !hd) {
+        (void)hipGetLastError();
+        return fail(PT_ERR_INVALID, "h_dst is not pinned (page-locked) host memory");
+    }
+    HIP_TRY(launch_readback(d_src, static_cast<float*>(hd), n, static_cast<hipStream_t>(stream)));
+    return PT_OK;
+}
+
 int pt_render_image(pt_scene* s, const float meta[48], uint32_t frame0, uint32_t nframes, uint32_t frame_stride,
                     int max_depth, int mode, uint8_t* rgba, pt_counters* counters) {
     if (!s || !rgba || !meta) return fail(PT_ERR_INVALID, "null argument");

@@ -36,6 +36,27 @@ hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t*
     return hipGetLastError();
 }
 
+// The accumulator to pinned host memory (pt_readback_async): a copy by a few blocks, each thread
+// storing 16-B words straight over PCIe.  The runtime's own copy of a 12 MB accumulator is a blit
+// kernel of 512 blocks that holds its CU slots for the whole PCIe transfer (0.2-1.2 ms in a kernel
+// trace of the bench, r06m), beside the next step's render; PCIe is the bound either way.
+constexpr int kReadbackBlocks = 16;
+__global__ __launch_bounds__(256) void k_readback(const float4* __restrict__ src, float4* __restrict__ dst, size_t n4,
+                                                  const float* __restrict__ src_tail, float* __restrict__ dst_tail,
+                                                  uint32_t ntail) {
+    const size_t step = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += step) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < ntail) dst_tail[threadIdx.x] = src_tail[threadIdx.x];
+}
+hipError_t launch_readback(const float* d_src, float* h_dst_dev, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const size_t n4 = n / 4;
+    const uint32_t ntail = (uint32_t)(n - 4 * n4);
+    hipLaunchKernelGGL(k_readback, dim3(kReadbackBlocks), dim3(256), 0, stream, reinterpret_cast<const float4*>(d_src),
+                       reinterpret_cast<float4*>(h_dst_dev), n4, d_src + 4 * n4, h_dst_dev + 4 * n4, ntail);
+    return hipGetLastError();
+}
+
 // dst += src, f32, element-wise (the ordered multi-device reduction of pt_render_multi: partial
 // accumulators added onto device 0's in device order)
 __global__ __launch_bounds__(256) void k_accum_add(float4* __restrict__ dst, const float4* __restrict__ src, size_t n4) {

@@ -164,6 +164,8 @@ hipError_t launch_megakernel(const LaunchOpts& lo, const SceneView& sc, const Fr
 
 // display transform of program-raymarch.ts:295-316 on device (pt_image.hip)
 hipError_t launch_tonemap(const float* acc, size_t npix, uint32_t runs, uint8_t* rgba, hipStream_t stream);
+// n floats from device memory to pinned host memory (h_dst_dev: its device address; pt_image.hip)
+hipError_t launch_readback(const float* d_src, float* h_dst_dev, size_t n, hipStream_t stream);
 // dst[i] += src[i] for i < n (f32; both on the stream's device; pt_image.hip)
 hipError_t launch_accum_add(float* dst, const float* src, size_t n, hipStream_t stream);
 

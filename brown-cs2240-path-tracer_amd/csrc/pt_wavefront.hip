@@ -1197,13 +1197,19 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
                 pv[h].w.rqi = qi;
             }
         }
+        // the fused kernel's first launch makes the camera paths itself (GEN); it appends into
+        // count slot 1, zeroed here (k_wf_generate zeroes it otherwise) — on the caller's stream
+        // before the fork: on a part's stream the second part's memset waited ~0.5 ms for a CU slot
+        // behind the first part's first launch, and the parts ran that far apart (a kernel trace of
+        // the bench, r06m)
+        const bool fgen = TRAV >= 400 && ws.fuse_gen;
+        if (fgen)
+            for (int h = 0; h < nh; ++h)
+                HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rcnt + kRegions, 0, kRegions * sizeof(uint32_t), stream));
         if (np > 1) {
             HIP_RETURN_IF(hipEventRecord(ws.fork, stream));
             for (int h = 0; h < nh; ++h) HIP_RETURN_IF(hipStreamWaitEvent(pv[h].st, ws.fork, 0));
         }
-        // the fused kernel's first launch makes the camera paths itself (GEN); it appends into
-        // count slot 1, zeroed here (k_wf_generate zeroes it otherwise)
-        const bool fgen = TRAV >= 400 && ws.fuse_gen;
         // option regen (fused kernel, camera paths made in the kernel): q camera batches per region
         // admitted by each extension launch; regen_cam = the most camera batches of any region
         uint32_t regen_q = 0, regen_cam = 0;
@@ -1219,14 +1225,10 @@ static hipError_t wf_render_t(const SceneView& sc_in, const FrameParams& fp, con
             else
                 regen_q = 0;  // one launch admits them all: the plain first launch
         }
-        for (int h = 0; h < nh; ++h) {
-            if (fgen)
-                HIP_RETURN_IF(hipMemsetAsync(pv[h].w.rcnt + kRegions, 0, kRegions * sizeof(uint32_t), pv[h].st));
-            else
-                PT_LAUNCH(KID_WF_GENERATE, pv[h].st, (k_wf_generate<COUNT>),
-                          dim3((std::max(pv[h].P, pv[h].w.nreg) + 255) / 256), dim3(256), 0, pv[h].st,
-                          fp, pv[h].w, frame0, stride, pv[h].fbase, pv[h].P, !accum, cnt);
-        }
+        for (int h = 0; h < nh && !fgen; ++h)
+            PT_LAUNCH(KID_WF_GENERATE, pv[h].st, (k_wf_generate<COUNT>),
+                      dim3((std::max(pv[h].P, pv[h].w.nreg) + 255) / 256), dim3(256), 0, pv[h].st,
+                      fp, pv[h].w, frame0, stride, pv[h].fbase, pv[h].P, !accum, cnt);
         // launch `it` of part h (in_q: the queue the trace kernels read, it & 1)
         auto step = [&](int h, int it) -> hipError_t {
             const int in_q = it & 1;

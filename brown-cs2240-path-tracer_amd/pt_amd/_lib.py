@@ -121,6 +121,7 @@ def load_library():
     L.pt_bvh_build_sah.argtypes = [p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_bvh_build_sah2.argtypes = [p, sz, p, sz, p, sz, p, sz, ctypes.POINTER(sz)]
     L.pt_tonemap_async.argtypes = [p, p, sz, u32, p, p]
+    L.pt_readback_async.argtypes = [p, p, sz, p, p]
     L.pt_render_image.argtypes = [p, p, u32, u32, u32, i, i, p, p]
     L.pt_profile_read.argtypes = [p, ctypes.POINTER(KernelTime), i, ctypes.POINTER(i)]
     L.pt_scene_set_vertex_normals.argtypes = [p, i]
@@ -136,7 +137,7 @@ def load_library():
     L.pt_scene_leaf_bvh.argtypes = [p, i, i32p, i32p, i32p]
     L.pt_selftest_leaf.argtypes = [p, i, i, u32, u32, p]
     for fn in ("pt_scene_leaf_bvh", "pt_selftest_leaf", "pt_selftest_valu", "pt_set_option", "pt_get_option", "pt_release_communicators", "pt_scene_check", "pt_set_hw_queues", "pt_render_multi", "pt_bvh_build_sah", "pt_bvh_build_sah2", "pt_device_count", "pt_scene_create", "pt_scene_get_info", "pt_render", "pt_render_async", "pt_frame",
-               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_render_image",
+               "pt_frame_async", "pt_tonemap", "pt_selftest_math", "pt_profile_enable", "pt_profile_select", "pt_profile_read", "pt_selftest_rcp", "pt_bvh_build", "pt_tonemap_async", "pt_readback_async", "pt_render_image",
                "pt_scene_set_vertex_normals"):
         getattr(L, fn).restype = i
     _lib = L
@@ -312,6 +313,11 @@ class Scene:
         _check(self._lib.pt_render_image(self._h, _ptr(meta), frame0, nframes, stride, max_depth, mode, _ptr(out),
                                          ctypes.byref(c) if counters else None))
         return (out, c.as_dict()) if counters else out
+
+    def readback_async(self, d_src_ptr: int, n: int, h_dst_ptr: int, stream_ptr: int = 0):
+        """n floats from device memory to pinned host memory on `stream` (pt_readback_async)."""
+        _check(self._lib.pt_readback_async(self._h, ctypes.c_void_p(d_src_ptr), n, ctypes.c_void_p(h_dst_ptr),
+                                           ctypes.c_void_p(stream_ptr or None)))
 
     def tonemap_async(self, d_accum_ptr: int, npix: int, sample_runs: int, d_rgba_ptr: int, stream_ptr: int = 0):
         """Device tone map between caller-owned device buffers (e.g. torch tensors)."""

@@ -209,6 +209,14 @@ int pt_tonemap(const float* accum, size_t npix, uint32_t sample_runs, uint8_t* r
 int pt_tonemap_async(pt_scene* scene, const float* d_accum, size_t npix, uint32_t sample_runs, uint8_t* d_rgba,
                      void* stream);
 
+/* The accumulator (or any n floats) from device memory to PINNED host memory, asynchronous on
+ * `stream`: the reference maps its accumulation buffer back to the host after every frame
+ * (program-raymarch.ts:262-293).  A copy kernel of a few blocks, so that a readback pipelined
+ * with the next render holds few of its CU slots (the runtime's blit copy holds ~512 blocks for
+ * the whole PCIe transfer).  Both pointers 16-byte aligned; h_dst must be page-locked
+ * (hipHostMalloc / torch pin_memory), else PT_ERR_INVALID. */
+int pt_readback_async(pt_scene* scene, const float* d_src, size_t n, float* h_dst, void* stream);
+
 /* programEntry's result in one call: render frames frame0 + i*stride (i < nframes) into a
  * zeroed accumulator and return the displayed image (tone map with sample_runs = nframes)
  * as host RGBA u8 [H][W][4] — only the image crosses PCIe.  counters: nullable.  Blocking. */

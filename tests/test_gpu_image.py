@@ -42,3 +42,25 @@ def test_render_image_equals_render_then_host_tonemap(packed, mode):
         acc, c2 = s.render(meta, 0, 8, 1, 8, mode, counters=True)
     assert np.array_equal(img, pt_amd.tonemap(acc, 8).reshape(img.shape))
     assert c1 == c2
+
+
+@pytest.mark.parametrize("n", [0, 3, 4, 1023, 3 * 96 * 64, 3 * 1024 * 1024 + 2])
+def test_readback_to_pinned_host(packed, n):
+    """pt_readback_async (the accumulator to pinned host memory, program-raymarch.ts:262-293): the
+    same bytes as the device buffer, any length (a tail of < 4 floats included)."""
+    torch = pytest.importorskip("torch")
+    p = packed["CornellBox"]
+    src = torch.arange(n, dtype=torch.float32, device="cuda") * 0.5 - 3.0
+    dst = torch.full((max(n, 1),), -7.0, dtype=torch.float32).pin_memory()
+    st = torch.cuda.Stream()
+    with pt_amd.Scene(p.triangle_data, p.bvh_data) as s:
+        s.readback_async(src.data_ptr(), n, dst.data_ptr(), st.cuda_stream)
+        st.synchronize()
+        assert torch.equal(dst[:n], src.cpu())
+        if n == 0:
+            assert float(dst[0]) == -7.0
+            return
+        # pageable host memory is refused, not read through
+        pageable = torch.zeros(max(n, 4), dtype=torch.float32)
+        with pytest.raises(pt_amd.PtError):
+            s.readback_async(src.data_ptr(), n, pageable.data_ptr(), st.cuda_stream)
