@@ -395,8 +395,10 @@ def native_multi(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    # 10 timed steps (~1 s at configs[1]): the first step's ramp and the last step's per-launch events
+    # weigh half what they did over 5 (r06y2: 2,866 over 10 steps against 2,848 over 5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="CornellBox")
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--height", type=int, default=1024)
