@@ -1100,10 +1100,12 @@ int render_impl(pt_scene* s, const float* meta, uint32_t frame0, uint32_t nframe
     // where the leaves reference >= 32 Ki triangles and no leaf is big (100k +12 %, 1M +26 % against
     // runs of 4: r04aa_ab_run.log; 12.5k +3.7 % with node bias 1-2: r04ak_run2_bias.log), else 4
     // (Glossy 5 Ki references, 1k, and the boat — 52 Ki references, but big leaves walked in
-    // chunks — are 1-2 % faster with 4); option pool_run=2|4
+    // chunks — are 1-2 % faster with 4); option pool_run=2|4.  Round 6, with four node steps per node
+    // turn: runs of 2 on every tree without big leaves (Glossy +5 %, 1k +2.2 %, 12.5k +0.8 % over 4;
+    // the boat, whose big leaves go to the leaf pass, -0.7 %: profiles/r06ac_ab_*.log)
     {
         const bool pool = o.flag("leaf_pool", 1) != 0;
-        const bool run2 = s->info.max_leaf < 16 || (s->info.leaf_refs >= (1u << 15) && view.big_leaf == 0);
+        const bool run2 = s->info.max_leaf < 16 || view.big_leaf == 0;
         const long run = o.num("pool_run", run2 ? 2 : 4);
         view.leaf_pool = pool ? (int32_t)run : 0;
     }

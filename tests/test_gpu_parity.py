@@ -145,6 +145,8 @@ KERNELS = {
     "mega_skip_lean16": {"PT_KERNEL": "mega", "PT_LEAF_SKIP": "1", "PT_TRAV": "lean16"},
     "wavefront_skip_1block_run2": {"PT_KERNEL": "wavefront", "PT_LEAF_SKIP": "1", "PT_WF_TRACE_BLOCKS": "1",
                                    "PT_POOL_RUN": "2"},
+    # runs of 4 (the default only on trees with big leaves since round 6)
+    "wavefront_run4": {"PT_KERNEL": "wavefront", "PT_POOL_RUN": "4", "PT_MAILBOX": "0"},
     # node steps per node turn of the lean traversal (option node_steps; wavefront default 4, megakernel 1)
     "wavefront_nodesteps1": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "1", "PT_MAILBOX": "0"},
     "wavefront_nodesteps2": {"PT_KERNEL": "wavefront", "PT_NODE_STEPS": "2", "PT_MAILBOX": "0"},
